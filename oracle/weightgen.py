@@ -1,0 +1,95 @@
+"""TEST INFRASTRUCTURE (oracle side) -- counter-based synthetic weight generator.
+
+The reference loads real checkpoints (`split_model.py:81` from_pretrained,
+`qwen3_server_module.py:227-235` per-layer `layer_XX.pt` from the HF Hub).  None
+of that is reachable offline, so every parity check in this repo runs on
+synthetic weights produced by this generator.  The HIP side re-implements the
+exact same integer arithmetic (`inferd_amd/csrc/elementwise.hip`,
+`weightgen_kernel`), so weights never need to be shipped and the GPU-side
+generator is bit-checked against this file (tests/test_weightgen.py).
+
+Definition (all integer ops mod 2**64):
+    splitmix64(x): z = x + 0x9E3779B97F4A7C15
+                   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9
+                   z = (z ^ (z >> 27)) * 0x94D049BB133111EB
+                   return z ^ (z >> 31)
+    key(seed, tid)     = splitmix64((seed << 32) | tid)
+    u24(i)             = splitmix64(key + i) >> 40
+    t(i)   (fp32, exact) = u24 * 2**-23 - 1                  in [-1, 1)
+    w(i)   (fp32)        = fl(fl(t * scale) + center)        (two roundings, no FMA)
+    stored value         = bf16_rne(w(i))
+
+Only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s cpu_baseline leg may
+import anything under `oracle/`.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+_C1 = np.uint64(0x9E3779B97F4A7C15)
+_C2 = np.uint64(0xBF58476D1CE4E5B9)
+_C3 = np.uint64(0x94D049BB133111EB)
+
+# tensor ids: layer tensors are layer * 16 + index; globals live above 0xFFFF0000
+LAYER_TENSOR_IDS = {
+    "q_proj": 0, "k_proj": 1, "v_proj": 2, "o_proj": 3,
+    "q_norm": 4, "k_norm": 5,
+    "input_layernorm": 6, "post_attention_layernorm": 7,
+    "gate_proj": 8, "up_proj": 9, "down_proj": 10,
+}
+GLOBAL_TENSOR_IDS = {"embed_tokens": 0xFFFF0000, "norm": 0xFFFF0001, "lm_head": 0xFFFF0002}
+
+# (scale, center) per tensor kind.  Linear layers ~ U(-a, a) with std 0.02 (the HF
+# initializer_range); norm weights 1 +- 0.1 so the multiply is not the identity.
+LINEAR_SCALE = float(np.float32(0.02 * np.sqrt(3.0)))
+NORM_SCALE = 0.1
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + _C1
+        z = (z ^ (z >> np.uint64(30))) * _C2
+        z = (z ^ (z >> np.uint64(27))) * _C3
+        return z ^ (z >> np.uint64(31))
+
+
+def tensor_key(seed: int, tid: int) -> int:
+    x = np.array([((int(seed) & 0xFFFFFFFF) << 32) | (int(tid) & 0xFFFFFFFF)], dtype=np.uint64)
+    return int(splitmix64(x)[0])
+
+
+def uniform_fp32(seed: int, tid: int, n: int, scale: float, center: float = 0.0,
+                 offset: int = 0) -> np.ndarray:
+    """fp32 values w(offset .. offset+n-1) as defined in the module docstring."""
+    key = np.uint64(tensor_key(seed, tid))
+    idx = np.arange(offset, offset + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = splitmix64(idx + key)
+    u24 = (z >> np.uint64(40)).astype(np.float32)
+    t = u24 * np.float32(2.0 ** -23) - np.float32(1.0)          # exact
+    w = (t * np.float32(scale)).astype(np.float32)              # one rounding
+    w = (w + np.float32(center)).astype(np.float32)             # one rounding
+    return w
+
+
+def bf16_rne_bits(x: np.ndarray) -> np.ndarray:
+    """fp32 -> bf16 bit pattern (uint16), round-to-nearest-even (finite inputs)."""
+    u = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+    r = (u + np.uint64(0x7FFF) + ((u >> np.uint64(16)) & np.uint64(1))) >> np.uint64(16)
+    return r.astype(np.uint16)
+
+
+def bf16_bits_to_fp32(b: np.ndarray) -> np.ndarray:
+    return (b.astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+def tensor_spec(name: str) -> tuple[float, float]:
+    if name.endswith("norm") or name.endswith("layernorm"):
+        return NORM_SCALE, 1.0
+    return LINEAR_SCALE, 0.0
+
+
+def gen_tensor_bf16_bits(seed: int, tid: int, shape, name: str) -> np.ndarray:
+    scale, center = tensor_spec(name)
+    n = int(np.prod(shape))
+    return bf16_rne_bits(uniform_fp32(seed, tid, n, scale, center)).reshape(shape)

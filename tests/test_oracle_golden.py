@@ -1,0 +1,99 @@
+"""Pin the CPU oracle (oracle/qwen3_ref.py) to golden vectors produced by the
+reference's own modules (tests/golden/make_golden.py)."""
+import torch
+
+from golden_io import load, tensor
+from oracle import qwen3_ref as R
+
+SEED = 1234
+
+
+def _maxabs(a, b):
+    return (a.float() - b.float()).abs().max().item()
+
+
+def test_units_rmsnorm_rope_qkrope_mlp():
+    u = load("units.npz")
+    d = R.CONFIGS["qwen3-0.6b"]
+    w = R.gen_layer_weights(d, SEED, 0)["input_layernorm"]
+    for tag, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+        x = tensor(u[f"rms_{tag}_x"])
+        y = R.rms_norm(x, w.to(dt), d.eps)
+        assert torch.equal(y, tensor(u[f"rms_{tag}_y"])), tag
+        c, s = R.rope_cos_sin(d, torch.from_numpy(u["rope_pos"]), dt)
+        assert torch.equal(c, tensor(u[f"rope_{tag}_cos"]))
+        assert torch.equal(s, tensor(u[f"rope_{tag}_sin"]))
+    W = R.gen_layer_weights(d, SEED, 3)
+    q, k = tensor(u["qkr_q"]), tensor(u["qkr_k"])
+    pos = torch.from_numpy(u["qkr_pos"])
+    c, s = R.rope_cos_sin(d, pos, torch.bfloat16)
+    qn = R.rms_norm(q, W["q_norm"], d.eps).transpose(1, 2)
+    kn = R.rms_norm(k, W["k_norm"], d.eps).transpose(1, 2)
+    qe, ke = R.apply_rope(qn, kn, c, s)
+    assert torch.equal(qe, tensor(u["qkr_q_out"]))
+    assert torch.equal(ke, tensor(u["qkr_k_out"]))
+    y = R.mlp(tensor(u["mlp_x"]), W)
+    assert torch.equal(y, tensor(u["mlp_y"]))
+
+
+def test_tiny_petals_span_chain():
+    g = load("tiny_petals.npz")
+    d = R.CONFIGS["tiny"]
+    prompt = torch.from_numpy(g["prompt"])[None]
+    # fp32: the real PartitionedQwen2.forward chain (2 spans)
+    s0 = R.RefSpan(d, SEED, 0, 1, True, False, torch.float32, "sdpa")
+    s1 = R.RefSpan(d, SEED, 2, 3, False, True, torch.float32, "sdpa")
+    h0 = s0.forward(prompt)
+    assert _maxabs(h0, tensor(g["fp32_span0_hidden"])) < 1e-5
+    lg = s1.forward(h0)
+    assert _maxabs(lg, tensor(g["fp32_logits"])) < 1e-5
+    ids = prompt[0].tolist()
+    for _ in range(8):
+        x = torch.tensor([ids])
+        ids.append(R.greedy_token(s1.forward(s0.forward(x))))
+    assert ids[16:] == g["fp32_greedy_ids"].tolist()
+    # bf16 stage modules, per layer
+    b0 = R.RefSpan(d, SEED, 0, 1, True, False, torch.bfloat16, "sdpa")
+    b1 = R.RefSpan(d, SEED, 2, 3, False, True, torch.bfloat16, "sdpa")
+    per = []
+    h0 = b0.forward(prompt, per_layer=per)
+    lg = b1.forward(h0, per_layer=per)
+    for i, p in enumerate(per):
+        assert torch.equal(p, tensor(g[f"bf16_layer{i}"])), i
+    assert torch.equal(lg, tensor(g["bf16_logits"]))
+    ids = prompt[0].tolist()
+    for _ in range(8):
+        ids.append(R.greedy_token(b1.forward(b0.forward(torch.tensor([ids])))))
+    assert ids[16:] == g["bf16_greedy_ids"].tolist()
+    one = R.RefSpan(d, SEED, 0, 3, True, True, torch.float32, "sdpa")
+    assert _maxabs(one.forward(prompt), tensor(g["fp32_onespan_logits"])) < 1e-5
+
+
+def _check_server(name, cfg, tags):
+    g = load(name)
+    d = R.CONFIGS[cfg]
+    s, e = int(g["start"]), int(g["end"])
+    for tag, dt, tol in tags:
+        sp = R.RefSpan(d, SEED, s, e, False, False, dt, "eager")
+        ndec = sum(1 for k in g.files if k.startswith(f"{tag}_in_dec"))
+        outs = [sp.forward_cached("s", tensor(g[f"{tag}_in_prefill"]))]
+        for i in range(ndec):
+            outs.append(sp.forward_cached("s", tensor(g[f"{tag}_in_dec{i}"])))
+        for i, o in enumerate(outs):
+            ref = tensor(g[f"{tag}_out{i}"])
+            if tol == 0:
+                assert torch.equal(o, ref), (name, tag, i, _maxabs(o, ref))
+            else:
+                assert _maxabs(o, ref) <= tol, (name, tag, i, _maxabs(o, ref))
+
+
+def test_tiny_server_cached():
+    _check_server("tiny_server.npz", "tiny", (("fp32", torch.float32, 1e-5), ("bf16", torch.bfloat16, 0)))
+
+
+def test_q06_layer_cached():
+    _check_server("q06_layer.npz", "qwen3-0.6b", (("fp32", torch.float32, 1e-5), ("bf16", torch.bfloat16, 0)))
+
+
+def test_q8b_layer_cached():
+    _check_server("q8b_layer.npz", "qwen3-8b", (("bf16", torch.bfloat16, 0),))
