@@ -1,0 +1,165 @@
+/*
+ * inferd_span.h -- C-ABI of the MI355X (gfx950) Qwen3 layer-span engine.
+ *
+ * This is the drop-in boundary underneath InferD's span API.  The reference has no
+ * native code: its span compute is PyTorch/transformers called from Python
+ * (petals/partitioned_models.py, models/qwen3/server/qwen3_server_module.py).  Each
+ * entry point below names the reference interface it replaces.  The Python host side
+ * (inferd_amd/partitioned_models.py, inferd_amd/qwen3_server.py) binds this header
+ * with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  "device" pointers are HIP device memory; bf16
+ *    tensors are raw 16-bit patterns, row-major, contiguous.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).  Every call is
+ *    stream-ordered and asynchronous; nothing here synchronises the device.
+ *  - Every int-returning call returns INFERD_OK (0) or an INFERD_ERR_* code and leaves
+ *    a thread-local message readable through inferd_last_error().  No exception
+ *    crosses the ABI (the Python wrapper raises RuntimeError, as an exception in
+ *    PartitionedQwen2.forward propagates through task.py:54 to aiohttp as HTTP 500).
+ *  - Threading: one span handle is used from one host thread at a time (the reference
+ *    runs forward synchronously on the asyncio loop thread, task_scheduler.py:18).
+ */
+#ifndef INFERD_SPAN_H
+#define INFERD_SPAN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define INFERD_OK 0
+#define INFERD_ERR_ARG 1   /* bad argument / shape / unsupported configuration */
+#define INFERD_ERR_HIP 2   /* HIP runtime error (allocation, launch) */
+#define INFERD_ERR_STATE 3 /* handle not initialised */
+
+#define INFERD_KV_PAGE_TOKENS 64
+
+/* GEMM epilogues (inferd_gemm) */
+#define INFERD_EPI_NONE 0  /* C = bf16(A W^T)                                      */
+#define INFERD_EPI_RESID 1 /* C = bf16(bf16(A W^T) + R)                            */
+#define INFERD_EPI_SILU 2  /* W = [gate; up] (2N x K): C = bf16(silu(g) * u)       */
+
+/* Model + span geometry.  Replaces the span construction of split_model.py:92-108
+ * (span = layers[start_layer .. end_layer] of petals/inferd.yaml, plus embed for the
+ * first stage and final norm + lm_head for the last) and Qwen3Server(start, end)
+ * (qwen3_server_module.py:209-224).  Model constants: qwen3_config.py:10-24. */
+typedef struct InferdSpanConfig {
+  int32_t hidden;         /* HIDDEN_SIZE */
+  int32_t intermediate;   /* INTERMEDIATE_SIZE */
+  int32_t heads;          /* NUM_ATTENTION_HEADS */
+  int32_t kv_heads;       /* NUM_KEY_VALUE_HEADS */
+  int32_t head_dim;       /* HEAD_DIM (must be 128) */
+  int32_t vocab;          /* VOCAB_SIZE */
+  int32_t first_layer;    /* global index of the span's first layer (start_layer) */
+  int32_t n_layers;       /* end_layer - start_layer + 1 */
+  int32_t has_embed;      /* FirstStage: owns embed_tokens */
+  int32_t has_lm_head;    /* LastStage: owns final norm + lm_head */
+  float rms_eps;          /* RMS_NORM_EPS */
+  float rope_theta;       /* ROPE_THETA */
+  int32_t max_positions;  /* MAX_POSITION_EMBEDDINGS (rope table rows) */
+  int32_t kv_pages;       /* KV pool capacity, in INFERD_KV_PAGE_TOKENS-token pages */
+  int32_t max_tokens;     /* activation workspace rows (tokens per forward call) */
+  int32_t max_seqs;       /* sequences per forward call */
+} InferdSpanConfig;
+
+/* One forward call's batch: n_seqs sequences, their new tokens concatenated
+ * (n_tokens rows).  All arrays are device int32.  The KV cache of every sequence is a
+ * list of pages (block_table row); a token at `positions[i]` writes its K/V to global
+ * slot `slots[i]` = page * 64 + offset and attends to keys 0..positions[i] of its
+ * sequence.  This single descriptor covers the petals full-recompute call
+ * (partitioned_models.py:139-143: positions 0..T-1, fresh pages) and the cached
+ * prefill / single-token decode of Qwen3Server.send (qwen3_server_module.py:237-255,
+ * client.py:244-266). */
+typedef struct InferdBatch {
+  int32_t n_seqs;
+  int32_t n_tokens;
+  int32_t max_q_len;           /* max new tokens of one sequence */
+  int32_t max_ctx_len;         /* max of ctx_lens */
+  int32_t max_pages;           /* block_table row stride */
+  int32_t decode;              /* 1 iff every sequence has exactly one new token */
+  const int32_t* seq_start;    /* [n_seqs + 1] token-row offsets */
+  const int32_t* positions;    /* [n_tokens] */
+  const int32_t* slots;        /* [n_tokens] */
+  const int32_t* ctx_lens;     /* [n_seqs]: positions[last token] + 1 */
+  const int32_t* block_table;  /* [n_seqs][max_pages] */
+} InferdBatch;
+
+typedef struct InferdSpan InferdSpan;
+
+const char* inferd_last_error(void);
+int inferd_abi_version(void);
+
+/* ---- span lifetime (replaces torch.load of the pickled stage module,
+ *      partitioned_models.py:112-117, and Qwen3Server.__init__/_load_weights,
+ *      qwen3_server_module.py:209-235) ---------------------------------------------- */
+int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out);
+void inferd_span_destroy(InferdSpan* span);
+
+/* Fill every weight of the span from the counter-based generator (oracle/weightgen.py
+ * defines the same values) -- the offline stand-in for the HF checkpoint. */
+int inferd_span_init_synthetic(InferdSpan* span, uint64_t seed, void* stream);
+
+/* Load one weight from a row-major device bf16 tensor.  `layer` is span-local
+ * (0..n_layers-1) or -1 for embed_tokens / norm / lm_head.  `name` uses the reference's
+ * state-dict leaf names (qwen3_server_module.py:101-124, :169-176):
+ * q_proj k_proj v_proj o_proj q_norm k_norm input_layernorm post_attention_layernorm
+ * gate_proj up_proj down_proj | embed_tokens norm lm_head.  Projections are packed into
+ * the device fragment layout (fused [q;k;v] and [gate;up]). */
+int inferd_span_set_weight(InferdSpan* span, int32_t layer, const char* name,
+                           const void* src, int64_t rows, int64_t cols, void* stream);
+
+/* Span forward.  Replaces FirstStage/StageInner/LastStage.forward
+ * (partitioned_models.py:47-57, :66-75, :86-97) and Qwen3Server.send
+ * (qwen3_server_module.py:237-255).
+ *   ids       first span only: device int32 [n_tokens] token ids (embed gather)
+ *   x_in      other spans: device bf16 [n_tokens][hidden] hidden states
+ *   x_out     optional device bf16 [n_tokens][hidden]: hidden after the last layer
+ *   next_ids  last span only, optional: device int32 [n_seqs] greedy token of each
+ *             sequence's last row (norm -> lm_head -> argmax, partitioned_models.py:162);
+ *             ties resolve to the lowest index like torch.argmax
+ *   logits    last span only, optional: device bf16 [n_seqs][vocab] last-row logits
+ *   layer_out optional device bf16 [n_layers][n_tokens][hidden] per-layer capture */
+int inferd_span_forward(InferdSpan* span, const InferdBatch* batch, const int32_t* ids,
+                        const void* x_in, void* x_out, int32_t* next_ids, void* logits,
+                        void* layer_out, void* stream);
+
+/* Device base pointer of one layer's KV pool ([pages][K|V][kv_heads][64*128] bf16). */
+int inferd_span_kv_layer(InferdSpan* span, int32_t layer, void** out);
+/* Zero the KV pool. */
+int inferd_span_kv_clear(InferdSpan* span, void* stream);
+
+/* ---- single ops (the kernels the span forward chains; exported for parity tests) ---- */
+/* splitmix64 counter generator: dst[i] = bf16(fl(fl(t_i * scale) + center)) */
+int inferd_weightgen(void* dst, int64_t n, uint64_t seed, uint32_t tensor_id, float scale,
+                     float center, void* stream);
+/* row-major W[rows][cols] -> fragment-packed (rows % 16 == 0, cols % 32 == 0) and back */
+int inferd_pack_weight(const void* src, int64_t rows, int64_t cols, void* dst, void* stream);
+int inferd_unpack_weight(const void* src, int64_t rows, int64_t cols, void* dst, void* stream);
+/* Qwen3RMSNorm.forward (qwen3_server_module.py:19-25) over rows of length cols */
+int inferd_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t cols, float eps,
+                   void* stream);
+/* nn.Linear(bias=False) on a packed weight: C[m][n] = A[m][k] W[n][k]^T (+ epilogue) */
+int inferd_gemm(const void* a, const void* w_packed, void* c, const void* resid, int32_t m,
+                int32_t n, int32_t k, int32_t epilogue, void* stream);
+/* rope cos/sin tables [max_pos][64] bf16 (HF default rope, client.py:56-71) */
+int inferd_rope_table(float theta, int32_t head_dim, int32_t max_pos, void* cos_t, void* sin_t,
+                      void* stream);
+/* q/k RMSNorm + RoPE (qwen3_server_module.py:134-142) on a fused qkv row
+ * [q (H*128) | k (KV*128) | v (KV*128)], q -> q_out [M][H][128], k/v -> paged cache
+ * slots (DynamicCache.update, :144-148). slots may be NULL (no cache write). */
+int inferd_qk_norm_rope_kv(const void* qkv, const int32_t* positions, const int32_t* slots,
+                           const void* q_norm_w, const void* k_norm_w, const void* cos_t,
+                           const void* sin_t, void* q_out, void* kv_layer, int32_t m,
+                           int32_t heads, int32_t kv_heads, float eps, void* stream);
+/* causal GQA attention of q [M][H][128] over the paged cache -> out [M][H*128] */
+int inferd_attention(const void* q, const void* kv_layer, const InferdBatch* batch,
+                     int32_t heads, int32_t kv_heads, void* out, void* workspace,
+                     int64_t workspace_bytes, void* stream);
+int64_t inferd_attention_workspace_bytes(int32_t n_seqs, int32_t heads, int32_t max_ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INFERD_SPAN_H */

@@ -1,0 +1,91 @@
+"""ctypes binding of include/inferd_span.h (libinferd_span.so, built in-tree for gfx950).
+
+There is no fallback: if the library is missing or cannot be loaded, every product
+call raises.  Build it with `python -c "import __graft_entry__ as g; g.build()"` or
+`make -C inferd_amd/csrc`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libinferd_span.so")
+
+INFERD_OK = 0
+EPI_NONE, EPI_RESID, EPI_SILU = 0, 1, 2
+KV_PAGE = 64
+
+# symbol -> (restype, argtypes); the header is the source of truth
+c_i32, c_i64, c_u64, c_u32, c_f, c_p = C.c_int32, C.c_int64, C.c_uint64, C.c_uint32, C.c_float, C.c_void_p
+
+
+class SpanConfig(C.Structure):
+    _fields_ = [(n, c_i32) for n in ("hidden", "intermediate", "heads", "kv_heads", "head_dim", "vocab",
+                                     "first_layer", "n_layers", "has_embed", "has_lm_head")] + \
+               [("rms_eps", c_f), ("rope_theta", c_f)] + \
+               [(n, c_i32) for n in ("max_positions", "kv_pages", "max_tokens", "max_seqs")]
+
+
+class Batch(C.Structure):
+    _fields_ = [(n, c_i32) for n in ("n_seqs", "n_tokens", "max_q_len", "max_ctx_len", "max_pages", "decode")] + \
+               [(n, c_p) for n in ("seq_start", "positions", "slots", "ctx_lens", "block_table")]
+
+
+SIGNATURES = {
+    "inferd_last_error": (C.c_char_p, []),
+    "inferd_abi_version": (C.c_int, []),
+    "inferd_span_create": (C.c_int, [C.POINTER(SpanConfig), C.POINTER(c_p)]),
+    "inferd_span_destroy": (None, [c_p]),
+    "inferd_span_init_synthetic": (C.c_int, [c_p, c_u64, c_p]),
+    "inferd_span_set_weight": (C.c_int, [c_p, c_i32, C.c_char_p, c_p, c_i64, c_i64, c_p]),
+    "inferd_span_forward": (C.c_int, [c_p, C.POINTER(Batch), c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "inferd_span_kv_layer": (C.c_int, [c_p, c_i32, C.POINTER(c_p)]),
+    "inferd_span_kv_clear": (C.c_int, [c_p, c_p]),
+    "inferd_weightgen": (C.c_int, [c_p, c_i64, c_u64, c_u32, c_f, c_f, c_p]),
+    "inferd_pack_weight": (C.c_int, [c_p, c_i64, c_i64, c_p, c_p]),
+    "inferd_unpack_weight": (C.c_int, [c_p, c_i64, c_i64, c_p, c_p]),
+    "inferd_rmsnorm": (C.c_int, [c_p, c_p, c_p, c_i32, c_i32, c_f, c_p]),
+    "inferd_gemm": (C.c_int, [c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32, c_i32, c_p]),
+    "inferd_rope_table": (C.c_int, [c_f, c_i32, c_i32, c_p, c_p, c_p]),
+    "inferd_qk_norm_rope_kv": (C.c_int, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32, c_f, c_p]),
+    "inferd_attention": (C.c_int, [c_p, c_p, C.POINTER(Batch), c_i32, c_i32, c_p, c_p, c_i64, c_p]),
+    "inferd_attention_workspace_bytes": (c_i64, [c_i32, c_i32, c_i32]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the C-ABI library (raises OSError/RuntimeError when unavailable)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"libinferd_span.so not built ({path}); run __graft_entry__.build()")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != INFERD_OK:
+        msg = load().inferd_last_error()
+        raise RuntimeError(f"inferd error {rc}: {msg.decode() if msg else ''}")
+
+
+def ptr(t) -> int | None:
+    """device pointer of a torch tensor (None passes NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(stream=None) -> int | None:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

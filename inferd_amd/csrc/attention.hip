@@ -1,0 +1,259 @@
+// GQA attention over the paged KV cache (gfx950, v_mfma_f32_16x16x32_bf16).
+//
+// Reference: Qwen3Attention.forward + eager_attention_forward
+// (models/qwen3/server/qwen3_server_module.py:126-162, :67-89) and, for the petals span
+// path, HF SDPA with the bool causal mask of petals/partitioned_models.py:28-35.
+// Scores are kept in fp32 (SDPA semantics), softmax is online (flash style), P is
+// rounded to bf16 for the P*V MFMA, the output is normalised in fp32 and rounded once.
+//
+// Both kernels compute S^T = K * Q^T (token on the MFMA row, query column on the lane)
+// so that every per-query quantity (running max, sum, rescale) is lane-local and the
+// S^T accumulators ARE the B operand of O^T = V^T * P^T (the V page layout in common.h
+// is permuted to match).  The 16 MFMA columns are:
+//   decode : the n_rep query heads that share one kv head (<= 16) of one sequence
+//   prefill: 16 consecutive query rows of one head
+#include "common.h"
+#include "kernels.h"
+
+#define LOG2E 1.4426950408889634f
+
+// One 64-token page of online-softmax attention for one wave.
+// qf: Q^T fragments (4 k-steps of 32 dims); pos_lim: keys t with t <= pos_lim[col] are
+// visible (lane-local column limit).
+__device__ __forceinline__ void attend_page(const u16* __restrict__ kblk, const u16* __restrict__ vblk,
+                                            const bf16x8 (&qf)[4], int page_tok0, int lim,
+                                            float scale_log2, float& m_i, float& l_i,
+                                            f32x4 (&o)[8], int lane) {
+  const bf16x8* kb = (const bf16x8*)kblk + lane;
+  const bf16x8* vb = (const bf16x8*)vblk + lane;
+  bf16x8 kf[16], vf[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) kf[i] = kb[i * 64];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) vf[i] = vb[i * 64];
+  f32x4 sc[4];
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb) {
+    sc[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) sc[tb] = mfma16(kf[tb * 4 + ks], qf[ks], sc[tb]);
+  }
+  float pmax = -INFINITY;
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
+      const float s = (t <= lim) ? sc[tb][r] * scale_log2 : -INFINITY;
+      sc[tb][r] = s;
+      pmax = fmaxf(pmax, s);
+    }
+  pmax = fmaxf(pmax, __shfl_xor(pmax, 16));
+  pmax = fmaxf(pmax, __shfl_xor(pmax, 32));
+  const float m_new = fmaxf(m_i, pmax);
+  const float alpha = exp2f(m_i - m_new);
+  float psum = 0.f;
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = exp2f(sc[tb][r] - m_new);
+      sc[tb][r] = p;
+      psum += p;
+    }
+  psum += __shfl_xor(psum, 16);
+  psum += __shfl_xor(psum, 32);
+  l_i = l_i * alpha + psum;
+  m_i = m_new;
+#pragma unroll
+  for (int db = 0; db < 8; ++db) o[db] *= alpha;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    bf16x8 pf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pf[j] = (__bf16)sc[2 * kt][j];
+      pf[4 + j] = (__bf16)sc[2 * kt + 1][j];
+    }
+#pragma unroll
+    for (int db = 0; db < 8; ++db) o[db] = mfma16(vf[kt * 8 + db], pf, o[db]);
+  }
+}
+
+// ------------------------------------------------------------------ decode (1 token/seq)
+// grid (n_chunks, KV, B), 4 waves; wave w handles pages [chunk*4*ppw + w*ppw, +ppw).
+// Writes unnormalised partial O and (m, l) per (seq, kv head, chunk, head-in-group).
+__global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict__ q,
+                                                          const u16* __restrict__ kv,
+                                                          AttnBatch b, int H, int KV, int ppw,
+                                                          float scale_log2, int n_chunks,
+                                                          float* __restrict__ ws) {
+  __shared__ float sm_m[4][16], sm_l[4][16];
+  __shared__ float sm_o[4][16][HEAD_DIM + 4];
+  const int chunk = blockIdx.x, g = blockIdx.y, bseq = blockIdx.z;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n_rep = H / KV;
+  const int ctx = b.ctx_lens[bseq];
+  const int n_pages = (ctx + KV_PAGE - 1) / KV_PAGE;
+  const int p_begin = chunk * 4 * ppw;
+  if (p_begin >= n_pages) return;  // uniform over the workgroup
+  const int tok = b.seq_start[bseq + 1] - 1;
+  const int hn = lane & 15;
+  bf16x8 qf[4];
+  if (hn < n_rep) {
+    const u16* qp = q + ((int64_t)tok * H + g * n_rep + hn) * HEAD_DIM + 8 * (lane >> 4);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const bf16x8*)(qp + ks * 32);
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
+  }
+  float m_i = -INFINITY, l_i = 0.f;
+  f32x4 o[8];
+#pragma unroll
+  for (int db = 0; db < 8; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
+  for (int pp = 0; pp < ppw; ++pp) {
+    const int pi = p_begin + wave * ppw + pp;
+    if (pi >= n_pages) break;
+    const int phys = bt[pi];
+    const u16* kblk = kv + ((int64_t)(phys * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
+    const u16* vblk = kv + ((int64_t)(phys * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
+    attend_page(kblk, vblk, qf, pi * KV_PAGE, ctx - 1, scale_log2, m_i, l_i, o, lane);
+  }
+  // combine the 4 waves of this chunk through LDS
+  if (lane < 16) {
+    sm_m[wave][lane] = m_i;
+    sm_l[wave][lane] = l_i;
+  }
+#pragma unroll
+  for (int db = 0; db < 8; ++db)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sm_o[wave][hn][db * 16 + 4 * (lane >> 4) + r] = o[db][r];
+  __syncthreads();
+  float* wsb = ws + (((int64_t)bseq * KV + g) * n_chunks + chunk) * 16 * (HEAD_DIM + 2);
+  for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += 256) {
+    const int n = idx / HEAD_DIM, d = idx % HEAD_DIM;
+    float M = fmaxf(fmaxf(sm_m[0][n], sm_m[1][n]), fmaxf(sm_m[2][n], sm_m[3][n]));
+    float acc = 0.f, L = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = exp2f(sm_m[w][n] - M);
+      acc += sm_o[w][n][d] * f;
+      L += sm_l[w][n] * f;
+    }
+    wsb[n * (HEAD_DIM + 2) + d] = acc;
+    if (d == 0) {
+      wsb[n * (HEAD_DIM + 2) + HEAD_DIM] = M;
+      wsb[n * (HEAD_DIM + 2) + HEAD_DIM + 1] = L;
+    }
+  }
+}
+
+// grid (H, B), 128 threads: merge the chunks of one (seq, head) and normalise.
+__global__ __launch_bounds__(128) void attn_decode_combine_kernel(AttnBatch b, int H, int KV,
+                                                                  int ppw, int n_chunks,
+                                                                  const float* __restrict__ ws,
+                                                                  u16* __restrict__ out) {
+  const int h = blockIdx.x, bseq = blockIdx.y, d = threadIdx.x;
+  const int n_rep = H / KV, g = h / n_rep, n = h % n_rep;
+  const int ctx = b.ctx_lens[bseq];
+  const int n_pages = (ctx + KV_PAGE - 1) / KV_PAGE;
+  const int nc = (n_pages + 4 * ppw - 1) / (4 * ppw);
+  const float* base = ws + ((int64_t)bseq * KV + g) * n_chunks * 16 * (HEAD_DIM + 2) + n * (HEAD_DIM + 2);
+  float M = -INFINITY;
+  for (int c = 0; c < nc; ++c) M = fmaxf(M, base[(int64_t)c * 16 * (HEAD_DIM + 2) + HEAD_DIM]);
+  float acc = 0.f, L = 0.f;
+  for (int c = 0; c < nc; ++c) {
+    const float* p = base + (int64_t)c * 16 * (HEAD_DIM + 2);
+    const float f = exp2f(p[HEAD_DIM] - M);
+    acc += p[d] * f;
+    L += p[HEAD_DIM + 1] * f;
+  }
+  const int tok = b.seq_start[bseq + 1] - 1;
+  out[(int64_t)tok * H * HEAD_DIM + h * HEAD_DIM + d] = f2bf(acc / L);
+}
+
+static int decode_ppw(int B, int KV, int max_ctx) {
+  const int n_pages = (max_ctx + KV_PAGE - 1) / KV_PAGE;
+  // aim for >= ~4096 waves in flight over the chip
+  int ppw = (B * KV * n_pages + 4095) / 4096;
+  if (ppw < 1) ppw = 1;
+  if (ppw > 16) ppw = 16;
+  return ppw;
+}
+
+size_t attn_decode_ws_bytes(int B, int H, int max_ctx) {
+  // upper bound over kv-head counts: chunks computed with ppw = 1
+  const int n_pages = (max_ctx + KV_PAGE - 1) / KV_PAGE;
+  const int n_chunks = (n_pages + 3) / 4;
+  return (size_t)B * H * n_chunks * 16 * (HEAD_DIM + 2) * sizeof(float);
+}
+
+void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
+                        float scale, u16* out, float* ws, hipStream_t s) {
+  const int ppw = decode_ppw(b.B, KV, b.max_ctx);
+  const int n_pages = (b.max_ctx + KV_PAGE - 1) / KV_PAGE;
+  const int n_chunks = (n_pages + 4 * ppw - 1) / (4 * ppw);
+  hipLaunchKernelGGL(attn_decode_kernel, dim3(n_chunks, KV, b.B), dim3(256), 0, s, q, kv_layer, b,
+                     H, KV, ppw, scale * LOG2E, n_chunks, ws);
+  hipLaunchKernelGGL(attn_decode_combine_kernel, dim3(H, b.B), dim3(HEAD_DIM), 0, s, b, H, KV, ppw,
+                     n_chunks, (const float*)ws, out);
+}
+
+// ------------------------------------------------------------------ prefill (causal)
+// grid (ceil(max_q_len/64), H, B), 4 waves; wave w owns query rows [64*bx + 16*w, +16)
+// of one head; walks every page up to the block's largest position.
+__global__ __launch_bounds__(256) void attn_prefill_kernel(const u16* __restrict__ q,
+                                                           const u16* __restrict__ kv,
+                                                           AttnBatch b, int H, int KV,
+                                                           float scale_log2,
+                                                           u16* __restrict__ out) {
+  const int bseq = blockIdx.z, h = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n_rep = H / KV, g = h / n_rep;
+  const int t0 = b.seq_start[bseq];
+  const int T = b.seq_start[bseq + 1] - t0;
+  const int r0 = blockIdx.x * 64 + wave * 16;
+  if (r0 >= T) return;  // no barriers in this kernel
+  const int row = r0 + (lane & 15);
+  const bool valid = row < T;
+  const int tokrow = t0 + (valid ? row : T - 1);
+  const int qpos = b.positions[tokrow];
+  int maxpos = qpos;
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) maxpos = max(maxpos, __shfl_xor(maxpos, o, 16));
+  bf16x8 qf[4];
+  const u16* qp = q + ((int64_t)tokrow * H + h) * HEAD_DIM + 8 * (lane >> 4);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const bf16x8*)(qp + ks * 32);
+  float m_i = -INFINITY, l_i = 0.f;
+  f32x4 o[8];
+#pragma unroll
+  for (int db = 0; db < 8; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
+  const int n_pages = maxpos / KV_PAGE + 1;
+  for (int pi = 0; pi < n_pages; ++pi) {
+    const int phys = bt[pi];
+    const u16* kblk = kv + ((int64_t)(phys * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
+    const u16* vblk = kv + ((int64_t)(phys * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
+    attend_page(kblk, vblk, qf, pi * KV_PAGE, qpos, scale_log2, m_i, l_i, o, lane);
+  }
+  if (!valid) return;
+  const float inv = 1.0f / l_i;
+  u16* op = out + (int64_t)tokrow * H * HEAD_DIM + h * HEAD_DIM;
+#pragma unroll
+  for (int db = 0; db < 8; ++db) {
+    u16x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = f2bf(o[db][r] * inv);
+    *(u16x4*)(op + db * 16 + 4 * (lane >> 4)) = v;
+  }
+}
+
+void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
+                         float scale, u16* out, hipStream_t s) {
+  dim3 g((b.max_q_len + 63) / 64, H, b.B);
+  hipLaunchKernelGGL(attn_prefill_kernel, g, dim3(256), 0, s, q, kv_layer, b, H, KV,
+                     scale * LOG2E, out);
+}

@@ -1,0 +1,57 @@
+// Host-side launchers of the span kernels (internal C++ interface; the public
+// boundary is the extern "C" API in include/inferd_span.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef unsigned short u16;
+
+enum GemmEpilogue {
+  EPI_NONE = 0,    // C = bf16(acc)
+  EPI_RESID = 1,   // C = bf16(bf16(acc) + R)              (o_proj / down_proj + residual)
+  EPI_SILU = 2,    // C = bf16(bf16(silu(bf16(g))) * bf16(u)) with [gate; up] packed weight
+  EPI_ARGMAX = 3,  // per-row partial argmax keys of bf16(acc) (+ optional bf16 logits in C)
+};
+
+// elementwise.hip
+void launch_weightgen(u16* dst, int64_t n, uint64_t key, float scale, float center, hipStream_t s);
+void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s);
+void launch_unpack(const u16* src, int N, int K, u16* dst, hipStream_t s);
+void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
+                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s);
+void launch_rope_table(const float* inv_freq, int max_pos, u16* cos_t, u16* sin_t, hipStream_t s);
+void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positions,
+                            const int32_t* slots, const u16* qn_w, const u16* kn_w,
+                            const u16* cos_t, const u16* sin_t, u16* q_out, u16* kv_layer, int M,
+                            int H, int KV, float eps, hipStream_t s);
+void launch_embed(const int32_t* ids, const u16* table, int M, int N, int vocab, u16* out,
+                  int32_t* err, hipStream_t s);
+void launch_argmax_decode(const unsigned long long* keys, int B, int32_t* ids, hipStream_t s);
+
+// gemm.hip.  Wp is fragment-packed (common.h).  N counts OUTPUT columns: for EPI_SILU the
+// packed weight holds 2N rows ([gate; up]).  For EPI_ARGMAX `partial` receives
+// (N/16) x M keys and `amax_keys` the per-row reduction (M <= 64).
+void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C,
+                 int64_t ldc, const u16* R, int64_t ldr, int epi, unsigned long long* partial,
+                 hipStream_t s);
+void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
+                          int32_t* ids, hipStream_t s);
+
+// attention.hip
+struct AttnBatch {
+  const int32_t* seq_start;    // [B+1] first token row of each sequence
+  const int32_t* positions;    // [M]
+  const int32_t* ctx_lens;     // [B] keys visible to the LAST token of the sequence
+  const int32_t* block_table;  // [B][max_pages]
+  int max_pages;
+  int B;
+  int M;
+  int max_q_len;
+  int max_ctx;
+};
+// q [M][H][128] bf16 -> out [M][H*128] bf16.  kv_layer: this layer's pool base.
+void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
+                        float scale, u16* out, float* ws, hipStream_t s);
+size_t attn_decode_ws_bytes(int B, int H, int max_ctx);
+void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
+                         float scale, u16* out, hipStream_t s);

@@ -1,0 +1,488 @@
+// Span runtime + C-ABI (include/inferd_span.h).
+//
+// An InferdSpan owns everything one pipeline stage needs on its GPU: the layer weights
+// in the fragment-packed layout (fused [q;k;v] and [gate;up]), the embedding table
+// (first span), final norm + packed lm_head (last span), the bf16 rope tables, the
+// paged KV pool and the activation workspace.  inferd_span_forward chains the kernels
+// of one Qwen3 decoder layer per span layer
+// (qwen3_server_module.py:179-206):
+//     rmsnorm -> qkv gemm -> qk-norm+rope+kv-write -> attention -> o gemm (+resid)
+//     -> rmsnorm -> gate/up gemm (+SwiGLU) -> down gemm (+resid)
+// with no allocation and no host synchronisation on the hot path.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/inferd_span.h"
+#include "common.h"
+#include "kernels.h"
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      return fail(INFERD_ERR_HIP, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
+  } while (0)
+
+#define LAUNCH_CHECK()                                                                            \
+  do {                                                                                            \
+    hipError_t _e = hipGetLastError();                                                            \
+    if (_e != hipSuccess)                                                                         \
+      return fail(INFERD_ERR_HIP, std::string("kernel launch failed: ") + hipGetErrorString(_e)); \
+  } while (0)
+
+extern "C" const char* inferd_last_error(void) { return g_err.c_str(); }
+extern "C" int inferd_abi_version(void) { return 1; }
+
+namespace {
+
+struct LayerW {
+  u16* qkv = nullptr;     // packed [(H+2KV)*128][hidden]
+  u16* o = nullptr;       // packed [hidden][H*128]
+  u16* gateup = nullptr;  // packed [2*I][hidden]
+  u16* down = nullptr;    // packed [hidden][I]
+  u16* in_ln = nullptr;
+  u16* post_ln = nullptr;
+  u16* q_norm = nullptr;
+  u16* k_norm = nullptr;
+};
+
+// tensor ids shared with oracle/weightgen.py
+enum { T_Q = 0, T_K, T_V, T_O, T_QN, T_KN, T_INLN, T_POSTLN, T_GATE, T_UP, T_DOWN };
+const uint32_t T_EMBED = 0xFFFF0000u, T_NORM = 0xFFFF0001u, T_LM = 0xFFFF0002u;
+const float LINEAR_SCALE = 0.034641016151377546f;  // float32(0.02 * sqrt(3))
+const float NORM_SCALE = 0.1f;
+
+uint64_t tensor_key(uint64_t seed, uint32_t tid) {
+  return splitmix64(((seed & 0xFFFFFFFFull) << 32) | (uint64_t)tid);
+}
+
+}  // namespace
+
+struct InferdSpan {
+  InferdSpanConfig cfg;
+  std::vector<LayerW> layers;
+  u16* embed = nullptr;
+  u16* final_norm = nullptr;
+  u16* lm_head = nullptr;
+  u16* cos_t = nullptr;
+  u16* sin_t = nullptr;
+  u16* kv_pool = nullptr;
+  size_t kv_layer_elems = 0;
+  // workspace
+  u16 *xn = nullptr, *qkv = nullptr, *q = nullptr, *attn = nullptr, *act = nullptr, *h = nullptr,
+      *last = nullptr;
+  float* attn_ws = nullptr;
+  size_t attn_ws_bytes = 0;
+  unsigned long long* argmax_partial = nullptr;
+  int32_t* err = nullptr;
+  std::vector<void*> allocs;
+
+  ~InferdSpan() {
+    for (void* p : allocs) (void)hipFree(p);
+  }
+  int alloc(void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes < 256 ? 256 : bytes);
+    if (e != hipSuccess) {
+      *p = nullptr;
+      return fail(INFERD_ERR_HIP, "hipMalloc(" + std::to_string(bytes) + ") failed: " + hipGetErrorString(e));
+    }
+    allocs.push_back(*p);
+    return INFERD_OK;
+  }
+  int qkv_rows() const { return (cfg.heads + 2 * cfg.kv_heads) * HEAD_DIM; }
+};
+
+#define ALLOC(ptr, bytes)                                   \
+  do {                                                      \
+    int _rc = s->alloc((void**)&(ptr), (size_t)(bytes));    \
+    if (_rc) return _rc;                                    \
+  } while (0)
+
+extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out) {
+  if (!cfg || !out) return fail(INFERD_ERR_ARG, "null argument");
+  const InferdSpanConfig& c = *cfg;
+  if (c.head_dim != HEAD_DIM) return fail(INFERD_ERR_ARG, "head_dim must be 128");
+  if (c.kv_heads <= 0 || c.heads % c.kv_heads != 0 || c.heads / c.kv_heads > 16)
+    return fail(INFERD_ERR_ARG, "heads must be a multiple of kv_heads with group size <= 16");
+  if (c.hidden % 128 || c.intermediate % 64 || c.vocab % 16)
+    return fail(INFERD_ERR_ARG, "hidden % 128, intermediate % 64 and vocab % 16 must be 0");
+  if (c.n_layers < 0 || c.max_tokens <= 0 || c.max_seqs <= 0 || c.kv_pages <= 0 || c.max_positions <= 0)
+    return fail(INFERD_ERR_ARG, "bad span sizes");
+  InferdSpan* s = new InferdSpan();
+  s->cfg = c;
+  const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
+  s->layers.resize(c.n_layers);
+  int rc = 0;
+  auto bail = [&](int code) {
+    delete s;
+    return code;
+  };
+#define SALLOC(ptr, bytes)                                  \
+  do {                                                      \
+    rc = s->alloc((void**)&(ptr), (size_t)(bytes));         \
+    if (rc) return bail(rc);                                \
+  } while (0)
+  for (auto& L : s->layers) {
+    SALLOC(L.qkv, (size_t)s->qkv_rows() * h * 2);
+    SALLOC(L.o, (size_t)h * H * HEAD_DIM * 2);
+    SALLOC(L.gateup, (size_t)2 * I * h * 2);
+    SALLOC(L.down, (size_t)h * I * 2);
+    SALLOC(L.in_ln, (size_t)h * 2);
+    SALLOC(L.post_ln, (size_t)h * 2);
+    SALLOC(L.q_norm, HEAD_DIM * 2);
+    SALLOC(L.k_norm, HEAD_DIM * 2);
+  }
+  if (c.has_embed) SALLOC(s->embed, (size_t)c.vocab * h * 2);
+  if (c.has_lm_head) {
+    SALLOC(s->final_norm, (size_t)h * 2);
+    SALLOC(s->lm_head, (size_t)c.vocab * h * 2);
+  }
+  // rope tables
+  SALLOC(s->cos_t, (size_t)c.max_positions * 64 * 2);
+  SALLOC(s->sin_t, (size_t)c.max_positions * 64 * 2);
+  {
+    float inv[64];
+    for (int i = 0; i < 64; ++i) {
+      // HF default rope: 1 / theta ** (arange(0, d, 2) / d) evaluated in fp32 (torch pow)
+      float e = (float)(2 * i) / (float)HEAD_DIM;
+      inv[i] = 1.0f / powf(c.rope_theta, e);
+    }
+    float* dinv = nullptr;
+    SALLOC(dinv, sizeof(inv));
+    if (hipMemcpy(dinv, inv, sizeof(inv), hipMemcpyHostToDevice) != hipSuccess)
+      return bail(fail(INFERD_ERR_HIP, "rope upload failed"));
+    launch_rope_table(dinv, c.max_positions, s->cos_t, s->sin_t, 0);
+  }
+  // KV pool
+  s->kv_layer_elems = (size_t)c.kv_pages * 2 * KV * KV_BLOCK_ELEMS;
+  if (c.n_layers > 0) {
+    SALLOC(s->kv_pool, s->kv_layer_elems * c.n_layers * 2);
+    if (hipMemset(s->kv_pool, 0, s->kv_layer_elems * c.n_layers * 2) != hipSuccess)
+      return bail(fail(INFERD_ERR_HIP, "kv memset failed"));
+  }
+  // workspace
+  const size_t Mx = c.max_tokens;
+  SALLOC(s->xn, Mx * h * 2);
+  SALLOC(s->qkv, Mx * s->qkv_rows() * 2);
+  SALLOC(s->q, Mx * H * HEAD_DIM * 2);
+  SALLOC(s->attn, Mx * H * HEAD_DIM * 2);
+  SALLOC(s->act, Mx * I * 2);
+  SALLOC(s->h, Mx * h * 2);
+  SALLOC(s->last, (size_t)c.max_seqs * h * 2);
+  s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
+  SALLOC(s->attn_ws, s->attn_ws_bytes);
+  if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
+  SALLOC(s->err, 256);
+  if (hipMemset(s->err, 0, 4) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
+  if (hipDeviceSynchronize() != hipSuccess) return bail(fail(INFERD_ERR_HIP, "init sync failed"));
+  *out = s;
+  return INFERD_OK;
+#undef SALLOC
+}
+
+extern "C" void inferd_span_destroy(InferdSpan* span) { delete span; }
+
+// ------------------------------------------------------------------ weights
+namespace {
+struct Target {
+  u16* dst;       // destination base
+  int packed;     // 1: fragment-pack at n-tile offset
+  int64_t rows, cols;
+  uint32_t tid_idx;
+};
+
+int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
+  const InferdSpanConfig& c = s->cfg;
+  const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
+  if (layer < 0) {
+    if (!strcmp(name, "embed_tokens") && s->embed) { *t = {s->embed, 0, c.vocab, h, T_EMBED}; return 0; }
+    if (!strcmp(name, "norm") && s->final_norm) { *t = {s->final_norm, 0, 1, h, T_NORM}; return 0; }
+    if (!strcmp(name, "lm_head") && s->lm_head) { *t = {s->lm_head, 1, c.vocab, h, T_LM}; return 0; }
+    return fail(INFERD_ERR_ARG, std::string("unknown/unowned global weight ") + name);
+  }
+  if (layer >= c.n_layers) return fail(INFERD_ERR_ARG, "layer index out of span");
+  LayerW& L = s->layers[layer];
+  const int64_t qrows = (int64_t)H * HEAD_DIM, kvrows = (int64_t)KV * HEAD_DIM;
+  if (!strcmp(name, "q_proj")) { *t = {L.qkv, 1, qrows, h, T_Q}; return 0; }
+  if (!strcmp(name, "k_proj")) { *t = {L.qkv + qrows * h, 1, kvrows, h, T_K}; return 0; }
+  if (!strcmp(name, "v_proj")) { *t = {L.qkv + (qrows + kvrows) * h, 1, kvrows, h, T_V}; return 0; }
+  if (!strcmp(name, "o_proj")) { *t = {L.o, 1, h, qrows, T_O}; return 0; }
+  if (!strcmp(name, "gate_proj")) { *t = {L.gateup, 1, I, h, T_GATE}; return 0; }
+  if (!strcmp(name, "up_proj")) { *t = {L.gateup + (int64_t)I * h, 1, I, h, T_UP}; return 0; }
+  if (!strcmp(name, "down_proj")) { *t = {L.down, 1, h, I, T_DOWN}; return 0; }
+  if (!strcmp(name, "q_norm")) { *t = {L.q_norm, 0, 1, HEAD_DIM, T_QN}; return 0; }
+  if (!strcmp(name, "k_norm")) { *t = {L.k_norm, 0, 1, HEAD_DIM, T_KN}; return 0; }
+  if (!strcmp(name, "input_layernorm")) { *t = {L.in_ln, 0, 1, h, T_INLN}; return 0; }
+  if (!strcmp(name, "post_attention_layernorm")) { *t = {L.post_ln, 0, 1, h, T_POSTLN}; return 0; }
+  return fail(INFERD_ERR_ARG, std::string("unknown layer weight ") + name);
+}
+// packed sub-blocks start at an n-tile boundary: offset rows*K elements == (rows/16)*KT*512
+}  // namespace
+
+extern "C" int inferd_span_set_weight(InferdSpan* s, int32_t layer, const char* name,
+                                      const void* src, int64_t rows, int64_t cols, void* stream) {
+  if (!s || !name || !src) return fail(INFERD_ERR_ARG, "null argument");
+  Target t;
+  if (resolve(s, layer, name, &t)) return INFERD_ERR_ARG;
+  if (rows != t.rows || cols != t.cols)
+    return fail(INFERD_ERR_ARG, std::string("shape mismatch for ") + name + ": expected " +
+                                    std::to_string(t.rows) + "x" + std::to_string(t.cols));
+  hipStream_t st = (hipStream_t)stream;
+  if (t.packed)
+    launch_pack((const u16*)src, cols, (int)rows, (int)cols, t.dst, st);
+  else
+    HIP_TRY(hipMemcpyAsync(t.dst, src, rows * cols * 2, hipMemcpyDeviceToDevice, st));
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* stream) {
+  if (!s) return fail(INFERD_ERR_ARG, "null span");
+  hipStream_t st = (hipStream_t)stream;
+  const InferdSpanConfig& c = s->cfg;
+  // temp buffer for the largest row-major tensor that needs packing
+  int64_t biggest = (int64_t)c.hidden * (c.intermediate > c.heads * HEAD_DIM ? c.intermediate : c.heads * HEAD_DIM);
+  if (c.has_lm_head && (int64_t)c.vocab * c.hidden > biggest) biggest = (int64_t)c.vocab * c.hidden;
+  u16* tmp = nullptr;
+  HIP_TRY(hipMalloc((void**)&tmp, biggest * 2));
+  static const char* layer_names[] = {"q_proj", "k_proj", "v_proj", "o_proj", "q_norm", "k_norm",
+                                      "input_layernorm", "post_attention_layernorm", "gate_proj",
+                                      "up_proj", "down_proj"};
+  auto gen = [&](int layer, const char* name) -> int {
+    Target t;
+    if (resolve(s, layer, name, &t)) return INFERD_ERR_ARG;
+    const bool is_norm = strstr(name, "norm") != nullptr;
+    const float scale = is_norm ? NORM_SCALE : LINEAR_SCALE;
+    const float center = is_norm ? 1.0f : 0.0f;
+    const uint32_t tid = layer < 0 ? t.tid_idx : (uint32_t)((c.first_layer + layer) * 16 + t.tid_idx);
+    const uint64_t key = tensor_key(seed, tid);
+    const int64_t n = t.rows * t.cols;
+    if (t.packed) {
+      launch_weightgen(tmp, n, key, scale, center, st);
+      launch_pack(tmp, t.cols, (int)t.rows, (int)t.cols, t.dst, st);
+    } else {
+      launch_weightgen(t.dst, n, key, scale, center, st);
+    }
+    return INFERD_OK;
+  };
+  int rc = 0;
+  for (int l = 0; l < c.n_layers && !rc; ++l)
+    for (const char* nm : layer_names)
+      if ((rc = gen(l, nm))) break;
+  if (!rc && c.has_embed) rc = gen(-1, "embed_tokens");
+  if (!rc && c.has_lm_head) rc = gen(-1, "norm");
+  if (!rc && c.has_lm_head) rc = gen(-1, "lm_head");
+  hipError_t e = hipStreamSynchronize(st);
+  (void)hipFree(tmp);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(INFERD_ERR_HIP, std::string("synthetic init: ") + hipGetErrorString(e));
+  return INFERD_OK;
+}
+
+// ------------------------------------------------------------------ forward
+static int check_batch(const InferdSpan* s, const InferdBatch* b) {
+  const InferdSpanConfig& c = s->cfg;
+  if (!b) return fail(INFERD_ERR_ARG, "null batch");
+  if (b->n_tokens <= 0 || b->n_tokens > c.max_tokens)
+    return fail(INFERD_ERR_ARG, "n_tokens out of range (max_tokens=" + std::to_string(c.max_tokens) + ")");
+  if (b->n_seqs <= 0 || b->n_seqs > c.max_seqs) return fail(INFERD_ERR_ARG, "n_seqs out of range");
+  if (b->max_ctx_len <= 0 || b->max_ctx_len > c.max_positions)
+    return fail(INFERD_ERR_ARG, "max_ctx_len out of range");
+  if (b->decode && b->n_tokens != b->n_seqs) return fail(INFERD_ERR_ARG, "decode batch needs one token per sequence");
+  if (!b->seq_start || !b->positions || !b->ctx_lens || !b->block_table)
+    return fail(INFERD_ERR_ARG, "batch arrays missing");
+  if ((int64_t)b->max_pages * KV_PAGE < b->max_ctx_len) return fail(INFERD_ERR_ARG, "block table too narrow");
+  return INFERD_OK;
+}
+
+static AttnBatch to_attn(const InferdBatch* b) {
+  AttnBatch a;
+  a.seq_start = b->seq_start;
+  a.positions = b->positions;
+  a.ctx_lens = b->ctx_lens;
+  a.block_table = b->block_table;
+  a.max_pages = b->max_pages;
+  a.B = b->n_seqs;
+  a.M = b->n_tokens;
+  a.max_q_len = b->max_q_len;
+  a.max_ctx = b->max_ctx_len;
+  return a;
+}
+
+extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const int32_t* ids,
+                                   const void* x_in, void* x_out, int32_t* next_ids, void* logits,
+                                   void* layer_out, void* stream) {
+  if (!s) return fail(INFERD_ERR_ARG, "null span");
+  int rc = check_batch(s, b);
+  if (rc) return rc;
+  const InferdSpanConfig& c = s->cfg;
+  hipStream_t st = (hipStream_t)stream;
+  const int M = b->n_tokens, B = b->n_seqs;
+  const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
+  const int qkvN = s->qkv_rows();
+  const float scale = 1.0f / sqrtf((float)HEAD_DIM);
+  const u16* x;
+  if (c.has_embed) {
+    if (!ids) return fail(INFERD_ERR_ARG, "first span needs token ids");
+    launch_embed(ids, s->embed, M, h, c.vocab, s->h, s->err, st);
+    x = s->h;
+  } else {
+    if (!x_in) return fail(INFERD_ERR_ARG, "span needs x_in hidden states");
+    x = (const u16*)x_in;
+  }
+  if (c.n_layers == 0 && x_out && x != x_out)
+    HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
+  const AttnBatch ab = to_attn(b);
+  for (int l = 0; l < c.n_layers; ++l) {
+    const LayerW& W = s->layers[l];
+    u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
+    launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
+    launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st);
+    launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
+                           s->sin_t, s->q, kv_l, M, H, KV, c.rms_eps, st);
+    if (b->decode)
+      launch_attn_decode(s->q, kv_l, ab, H, KV, scale, s->attn, s->attn_ws, st);
+    else
+      launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
+    // h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
+    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);
+    launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
+    launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st);
+    u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
+    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, st);
+    x = out;
+    if (layer_out)
+      HIP_TRY(hipMemcpyAsync((u16*)layer_out + (size_t)l * M * h, x, (size_t)M * h * 2,
+                             hipMemcpyDeviceToDevice, st));
+    LAUNCH_CHECK();
+  }
+  if (c.has_lm_head && (next_ids || logits)) {
+    if (B > 64) return fail(INFERD_ERR_ARG, "lm_head argmax supports <= 64 sequences per call");
+    // last row of each sequence: seq_start[b+1] - 1
+    launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st);
+    launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
+                s->argmax_partial, st);
+    if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
+  }
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_span_kv_layer(InferdSpan* s, int32_t layer, void** out) {
+  if (!s || !out) return fail(INFERD_ERR_ARG, "null argument");
+  if (layer < 0 || layer >= s->cfg.n_layers) return fail(INFERD_ERR_ARG, "layer out of range");
+  *out = s->kv_pool + s->kv_layer_elems * layer;
+  return INFERD_OK;
+}
+
+extern "C" int inferd_span_kv_clear(InferdSpan* s, void* stream) {
+  if (!s) return fail(INFERD_ERR_ARG, "null span");
+  if (s->kv_pool)
+    HIP_TRY(hipMemsetAsync(s->kv_pool, 0, s->kv_layer_elems * s->cfg.n_layers * 2, (hipStream_t)stream));
+  return INFERD_OK;
+}
+
+// ------------------------------------------------------------------ single ops
+extern "C" int inferd_weightgen(void* dst, int64_t n, uint64_t seed, uint32_t tensor_id, float scale,
+                                float center, void* stream) {
+  if (!dst || n < 0) return fail(INFERD_ERR_ARG, "bad weightgen args");
+  launch_weightgen((u16*)dst, n, tensor_key(seed, tensor_id), scale, center, (hipStream_t)stream);
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_pack_weight(const void* src, int64_t rows, int64_t cols, void* dst, void* stream) {
+  if (!src || !dst || rows % 16 || cols % 32) return fail(INFERD_ERR_ARG, "pack needs rows%16==0, cols%32==0");
+  launch_pack((const u16*)src, cols, (int)rows, (int)cols, (u16*)dst, (hipStream_t)stream);
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_unpack_weight(const void* src, int64_t rows, int64_t cols, void* dst, void* stream) {
+  if (!src || !dst || rows % 16 || cols % 32) return fail(INFERD_ERR_ARG, "unpack needs rows%16==0, cols%32==0");
+  launch_unpack((const u16*)src, (int)rows, (int)cols, (u16*)dst, (hipStream_t)stream);
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t cols, float eps,
+                              void* stream) {
+  if (!x || !w || !y || rows <= 0 || cols % 8 || cols > 16384) return fail(INFERD_ERR_ARG, "bad rmsnorm args");
+  launch_rmsnorm((const u16*)x, cols, nullptr, 0, (const u16*)w, (u16*)y, cols, rows, cols, eps,
+                 (hipStream_t)stream);
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_gemm(const void* a, const void* w, void* c, const void* r, int32_t m, int32_t n,
+                           int32_t k, int32_t epi, void* stream) {
+  if (!a || !w || !c || m <= 0 || n % 16 || k % 32) return fail(INFERD_ERR_ARG, "gemm needs n%16==0, k%32==0");
+  if (epi < 0 || epi > 2) return fail(INFERD_ERR_ARG, "bad epilogue");
+  if (epi == INFERD_EPI_RESID && !r) return fail(INFERD_ERR_ARG, "resid epilogue needs R");
+  launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr,
+              (hipStream_t)stream);
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_rope_table(float theta, int32_t head_dim, int32_t max_pos, void* cos_t, void* sin_t,
+                                 void* stream) {
+  if (head_dim != HEAD_DIM || max_pos <= 0 || !cos_t || !sin_t) return fail(INFERD_ERR_ARG, "bad rope args");
+  float inv[64];
+  for (int i = 0; i < 64; ++i) inv[i] = 1.0f / powf(theta, (float)(2 * i) / (float)HEAD_DIM);
+  float* dinv = nullptr;
+  HIP_TRY(hipMalloc((void**)&dinv, sizeof(inv)));
+  HIP_TRY(hipMemcpy(dinv, inv, sizeof(inv), hipMemcpyHostToDevice));
+  launch_rope_table(dinv, max_pos, (u16*)cos_t, (u16*)sin_t, (hipStream_t)stream);
+  hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  (void)hipFree(dinv);
+  if (e != hipSuccess) return fail(INFERD_ERR_HIP, hipGetErrorString(e));
+  return INFERD_OK;
+}
+
+extern "C" int inferd_qk_norm_rope_kv(const void* qkv, const int32_t* positions, const int32_t* slots,
+                                      const void* qn, const void* kn, const void* cos_t, const void* sin_t,
+                                      void* q_out, void* kv_layer, int32_t m, int32_t H, int32_t KV, float eps,
+                                      void* stream) {
+  if (!qkv || !positions || !qn || !kn || !cos_t || !sin_t || !q_out || m <= 0 || KV <= 0 || H % KV)
+    return fail(INFERD_ERR_ARG, "bad qk_norm_rope_kv args");
+  if (slots && !kv_layer) return fail(INFERD_ERR_ARG, "slots given without a kv pool");
+  const int ld = (H + 2 * KV) * HEAD_DIM;
+  launch_qk_norm_rope_kv((const u16*)qkv, ld, positions, slots, (const u16*)qn, (const u16*)kn,
+                         (const u16*)cos_t, (const u16*)sin_t, (u16*)q_out, (u16*)kv_layer, m, H, KV, eps,
+                         (hipStream_t)stream);
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int64_t inferd_attention_workspace_bytes(int32_t n_seqs, int32_t heads, int32_t max_ctx) {
+  return (int64_t)attn_decode_ws_bytes(n_seqs, heads, max_ctx);
+}
+
+extern "C" int inferd_attention(const void* q, const void* kv_layer, const InferdBatch* b, int32_t H,
+                                int32_t KV, void* out, void* ws, int64_t ws_bytes, void* stream) {
+  if (!q || !kv_layer || !b || !out || KV <= 0 || H % KV || H / KV > 16) return fail(INFERD_ERR_ARG, "bad attention args");
+  const AttnBatch ab = to_attn(b);
+  const float scale = 1.0f / sqrtf((float)HEAD_DIM);
+  if (b->decode) {
+    if (!ws || ws_bytes < (int64_t)attn_decode_ws_bytes(b->n_seqs, H, b->max_ctx_len))
+      return fail(INFERD_ERR_ARG, "decode attention workspace too small");
+    launch_attn_decode((const u16*)q, (const u16*)kv_layer, ab, H, KV, scale, (u16*)out, (float*)ws,
+                       (hipStream_t)stream);
+  } else {
+    launch_attn_prefill((const u16*)q, (const u16*)kv_layer, ab, H, KV, scale, (u16*)out, (hipStream_t)stream);
+  }
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}

@@ -1,0 +1,229 @@
+"""Host-side span runtime: one InferdSpan handle (C-ABI) per pipeline stage, a paged KV
+pool allocator and the per-session cache table.
+
+Semantics mirrored from the reference:
+  * a span is `layers[start_layer .. end_layer]` plus embed (first) / final norm +
+    lm_head (last)                                   -- split_model.py:92-102
+  * per-session KV cache keyed by session id, prefill then single-token steps whose
+    positions continue from the cached length        -- qwen3_server_module.py:220,253;
+                                                        client.py:244-266
+  * a session-less call is a stateless full recompute (positions 0..T-1) whose cache
+    pages are released afterwards                    -- partitioned_models.py:139-151
+Device memory for activations is torch (plumbing); all compute runs in
+libinferd_span.so.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib
+from ._lib import KV_PAGE
+
+
+@dataclass(frozen=True)
+class ModelDims:
+    """Qwen3 model constants (0.6B row == models/qwen3/qwen3_config.py:10-24)."""
+    name: str
+    hidden: int
+    intermediate: int
+    heads: int
+    kv_heads: int
+    layers: int
+    vocab: int
+    head_dim: int = 128
+    eps: float = 1e-6
+    rope_theta: float = 1_000_000.0
+    max_positions: int = 40960
+
+    def params_per_layer(self) -> int:
+        h, I, H, KV, d = self.hidden, self.intermediate, self.heads, self.kv_heads, self.head_dim
+        return h * (H + 2 * KV) * d + H * d * h + 3 * h * I + 2 * h + 2 * d
+
+
+MODELS = {
+    "tiny": ModelDims("tiny", 256, 512, 4, 2, 4, 1024),
+    "qwen3-0.6b": ModelDims("qwen3-0.6b", 1024, 3072, 16, 8, 28, 151936),
+    "qwen3-8b": ModelDims("qwen3-8b", 4096, 12288, 32, 8, 36, 151936),
+    "qwen3-32b": ModelDims("qwen3-32b", 5120, 25600, 64, 8, 64, 151936),
+}
+
+
+class PagePool:
+    """Free list over the span's KV pages (all layers of a span share page ids)."""
+
+    def __init__(self, n_pages: int):
+        self.n_pages = n_pages
+        self._free = list(range(n_pages - 1, -1, -1))
+
+    def alloc(self, n: int) -> list:
+        if n > len(self._free):
+            raise RuntimeError(f"KV pool exhausted: need {n} pages, {len(self._free)} free of {self.n_pages}")
+        return [self._free.pop() for _ in range(n)]
+
+    def free(self, pages):
+        self._free.extend(reversed(pages))
+
+    @property
+    def n_free(self) -> int:
+        return len(self._free)
+
+
+@dataclass
+class SeqState:
+    pages: list = field(default_factory=list)
+    length: int = 0   # tokens already in the cache
+
+
+def build_batch(seqs, device):
+    """seqs: list of (SeqState, n_new) with pages already reserved.
+    Returns (Batch struct, device int32 tensor backing its arrays)."""
+    B = len(seqs)
+    M = sum(n for _, n in seqs)
+    max_pages = max(1, max(len(st.pages) for st, _ in seqs))
+    seq_start, positions, slots, ctx = [0], [], [], []
+    for st, n in seqs:
+        for i in range(n):
+            p = st.length + i
+            positions.append(p)
+            slots.append(st.pages[p // KV_PAGE] * KV_PAGE + p % KV_PAGE)
+        seq_start.append(seq_start[-1] + n)
+        ctx.append(st.length + n)
+    table = []
+    for st, _ in seqs:
+        table.extend(st.pages + [0] * (max_pages - len(st.pages)))
+    host = torch.tensor(seq_start + positions + slots + ctx + table, dtype=torch.int32)
+    dev = host.to(device)
+    o = [0, B + 1, B + 1 + M, B + 1 + 2 * M, B + 1 + 2 * M + B]
+    base = dev.data_ptr()
+    b = _lib.Batch(n_seqs=B, n_tokens=M, max_q_len=max(n for _, n in seqs), max_ctx_len=max(ctx),
+                   max_pages=max_pages, decode=int(all(n == 1 for _, n in seqs)),
+                   seq_start=base + 4 * o[0], positions=base + 4 * o[1], slots=base + 4 * o[2],
+                   ctx_lens=base + 4 * o[3], block_table=base + 4 * o[4])
+    return b, dev
+
+
+class SpanRuntime:
+    """One layer span on one GPU (FirstStage / StageInner / LastStage compute)."""
+
+    def __init__(self, dims: ModelDims, first_layer: int, n_layers: int, *, has_embed: bool,
+                 has_lm_head: bool, kv_pages: int = 256, max_tokens: int = 4096, max_seqs: int = 64,
+                 max_positions: int | None = None, device: str | torch.device = "cuda"):
+        self.lib = _lib.load()
+        self.dims = dims
+        self.first_layer, self.n_layers = first_layer, n_layers
+        self.has_embed, self.has_lm_head = has_embed, has_lm_head
+        self.device = torch.device(device)
+        self.max_tokens, self.max_seqs = max_tokens, max_seqs
+        self.max_positions = max_positions or dims.max_positions
+        cfg = _lib.SpanConfig(hidden=dims.hidden, intermediate=dims.intermediate, heads=dims.heads,
+                              kv_heads=dims.kv_heads, head_dim=dims.head_dim, vocab=dims.vocab,
+                              first_layer=first_layer, n_layers=n_layers, has_embed=int(has_embed),
+                              has_lm_head=int(has_lm_head), rms_eps=dims.eps, rope_theta=dims.rope_theta,
+                              max_positions=self.max_positions, kv_pages=kv_pages,
+                              max_tokens=max_tokens, max_seqs=max_seqs)
+        h = _lib.c_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.inferd_span_create(cfg, h))
+        self.handle = h
+        self.pool = PagePool(kv_pages)
+        self.sessions: dict = {}
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            self.lib.inferd_span_destroy(h)
+            self.handle = None
+
+    # ----------------------------------------------------------------- weights
+    def init_synthetic(self, seed: int):
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.inferd_span_init_synthetic(self.handle, seed, _lib.stream_ptr()))
+
+    def set_weight(self, layer: int, name: str, w: torch.Tensor):
+        """layer: span-local index or -1 for embed_tokens / norm / lm_head."""
+        w = w.to(device=self.device, dtype=torch.bfloat16).contiguous()
+        rows, cols = (1, w.shape[0]) if w.dim() == 1 else tuple(w.shape)
+        _lib.check(self.lib.inferd_span_set_weight(self.handle, layer, name.encode(), w.data_ptr(),
+                                                   rows, cols, _lib.stream_ptr()))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def load_layer_state_dict(self, layer: int, sd: dict):
+        """Keys as in Qwen3DecoderLayer (qwen3_server_module.py:165-176): self_attn.q_proj.weight ..."""
+        for k, v in sd.items():
+            leaf = k.split(".")[-2] if k.endswith(".weight") else k
+            self.set_weight(layer, leaf, v)
+
+    # ----------------------------------------------------------------- sessions
+    def release(self, session_id):
+        st = self.sessions.pop(session_id, None)
+        if st is not None:
+            self.pool.free(st.pages)
+
+    def release_all(self):
+        for sid in list(self.sessions):
+            self.release(sid)
+
+    def _reserve(self, st: SeqState, n_new: int):
+        need = (st.length + n_new + KV_PAGE - 1) // KV_PAGE - len(st.pages)
+        if need > 0:
+            st.pages.extend(self.pool.alloc(need))
+
+    def build_batch(self, seqs):
+        return build_batch(seqs, self.device)
+
+    # ----------------------------------------------------------------- forward
+    @torch.no_grad()
+    def forward(self, requests, ids: torch.Tensor | None = None, x: torch.Tensor | None = None, *,
+                want_hidden: bool = True, want_next_ids: bool = False, want_logits: bool = False,
+                want_layers: bool = False) -> dict:
+        """requests: list of (session_id or None, n_new_tokens), tokens concatenated in order.
+        ids: int tensor [M] (first span); x: bf16 [M, hidden] (other spans)."""
+        d = self.dims
+        temp = []
+        seqs = []
+        for sid, n in requests:
+            if sid is None:
+                st = SeqState()
+                temp.append(st)
+            else:
+                st = self.sessions.setdefault(sid, SeqState())
+            self._reserve(st, n)
+            seqs.append((st, n))
+        try:
+            batch, keep = self.build_batch(seqs)
+            M, B = batch.n_tokens, batch.n_seqs
+            dev = self.device
+            ids_d = None
+            if self.has_embed:
+                ids_d = ids.to(device=dev, dtype=torch.int32).reshape(-1).contiguous()
+                assert ids_d.numel() == M
+            x_d = None
+            if not self.has_embed:
+                x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(M, d.hidden).contiguous()
+            out = {}
+            hid = torch.empty((M, d.hidden), dtype=torch.bfloat16, device=dev) if want_hidden else None
+            nid = torch.empty((B,), dtype=torch.int32, device=dev) if (want_next_ids and self.has_lm_head) else None
+            lg = torch.empty((B, d.vocab), dtype=torch.bfloat16, device=dev) if (want_logits and self.has_lm_head) else None
+            lay = torch.empty((self.n_layers, M, d.hidden), dtype=torch.bfloat16, device=dev) if want_layers else None
+            with torch.cuda.device(dev):
+                _lib.check(self.lib.inferd_span_forward(self.handle, batch, _lib.ptr(ids_d), _lib.ptr(x_d),
+                                                        _lib.ptr(hid), _lib.ptr(nid), _lib.ptr(lg),
+                                                        _lib.ptr(lay), _lib.stream_ptr()))
+            for st, n in seqs:
+                st.length += n
+            if hid is not None:
+                out["hidden"] = hid
+            if nid is not None:
+                out["next_ids"] = nid
+            if lg is not None:
+                out["logits"] = lg
+            if lay is not None:
+                out["layers"] = lay
+            out["_keep"] = (keep, ids_d, x_d)
+            return out
+        finally:
+            for st in temp:
+                self.pool.free(st.pages)
+                st.pages = []

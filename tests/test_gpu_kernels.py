@@ -1,0 +1,252 @@
+"""Per-kernel parity of the HIP path (through the C-ABI) against the CPU oracle.
+
+Tolerances: integer/layout ops bit-exact; elementwise bf16 ops reproduce the
+reference's rounding points and must match the oracle bit-for-bit on all but a
+vanishing fraction of elements (1 bf16 ulp allowed where transcendental / reduction
+order differs); GEMM / attention compare to an fp32 reference of the same bf16
+inputs with a relative tolerance stated per test.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import qwen3_ref as R
+from oracle import weightgen as wg
+
+pytestmark = pytest.mark.gpu
+
+SEED = 1234
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from inferd_amd import _lib
+    return _lib
+
+
+def bf16_ulp_diff(a, b):
+    """max difference in bf16 ulps (monotone int16 ordering)."""
+    ai = a.view(torch.int16).to(torch.int32)
+    bi = b.view(torch.int16).to(torch.int32)
+    ai = torch.where(ai < 0, -32768 - ai, ai)
+    bi = torch.where(bi < 0, -32768 - bi, bi)
+    return (ai - bi).abs()
+
+
+def test_weightgen_bit_exact(lib):
+    for tid, name, n in ((7, "q_proj", 100003), (0xFFFF0001, "norm", 4096), (3 * 16 + 4, "q_norm", 128)):
+        scale, center = wg.tensor_spec(name)
+        out = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        lib.check(lib.load().inferd_weightgen(out.data_ptr(), n, SEED, tid, scale, center, lib.stream_ptr()))
+        ref = wg.bf16_rne_bits(wg.uniform_fp32(SEED, tid, n, scale, center))
+        got = out.cpu().view(torch.int16).numpy().view(np.uint16)
+        assert np.array_equal(got, ref), name
+
+
+def test_pack_unpack_roundtrip(lib):
+    L = lib.load()
+    for N, K in ((16, 32), (48, 96), (4096, 1024)):
+        w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+        p = torch.empty_like(w)
+        u = torch.empty_like(w)
+        lib.check(L.inferd_pack_weight(w.data_ptr(), N, K, p.data_ptr(), lib.stream_ptr()))
+        lib.check(L.inferd_unpack_weight(p.data_ptr(), N, K, u.data_ptr(), lib.stream_ptr()))
+        assert torch.equal(w, u)
+        # spot-check the documented fragment layout: tile (nt,kt), lane l, elem j
+        pc, wc = p.cpu().view(-1), w.cpu()
+        KT = K // 32
+        for nt, kt, l, j in ((0, 0, 0, 0), (0, 0, 17, 3), (N // 16 - 1, KT - 1, 63, 7)):
+            assert pc[(nt * KT + kt) * 512 + l * 8 + j] == wc[16 * nt + (l & 15), 32 * kt + 8 * (l >> 4) + j]
+
+
+def test_rmsnorm_matches_oracle(lib):
+    L = lib.load()
+    d = R.CONFIGS["qwen3-8b"]
+    for rows, cols, scale in ((16, 4096, 1.0), (7, 1024, 30.0), (3, 5120, 0.01), (2, 256, 5.0)):
+        x = (torch.randn(rows, cols) * scale).to(torch.bfloat16)
+        w = (1 + 0.1 * torch.randn(cols)).to(torch.bfloat16)
+        ref = R.rms_norm(x, w, d.eps)
+        y = torch.empty(rows, cols, dtype=torch.bfloat16, device=DEV)
+        xd, wd = x.to(DEV), w.to(DEV)
+        lib.check(L.inferd_rmsnorm(xd.data_ptr(), wd.data_ptr(), y.data_ptr(), rows, cols, d.eps,
+                                   lib.stream_ptr()))
+        ulp = bf16_ulp_diff(y.cpu(), ref)
+        assert ulp.max() <= 1 and (ulp > 0).float().mean() < 2e-3, (rows, cols, ulp.max(), (ulp > 0).float().mean())
+
+
+def test_rmsnorm_golden(lib):
+    from golden_io import load, tensor
+    u = load("units.npz")
+    L = lib.load()
+    d = R.CONFIGS["qwen3-0.6b"]
+    x = tensor(u["rms_bf16_x"])
+    w = R.gen_layer_weights(d, SEED, 0)["input_layernorm"]
+    y = torch.empty_like(x, device=DEV)
+    xd, wd = x.to(DEV), w.to(DEV)
+    lib.check(L.inferd_rmsnorm(xd.data_ptr(), wd.data_ptr(), y.data_ptr(), x.shape[0], x.shape[1],
+                               d.eps, lib.stream_ptr()))
+    ulp = bf16_ulp_diff(y.cpu(), tensor(u["rms_bf16_y"]))
+    assert ulp.max() <= 1 and (ulp > 0).float().mean() < 2e-3
+
+
+def _gemm(lib, a, w, epi, r=None):
+    L = lib.load()
+    N, K = w.shape
+    n_out = N // 2 if epi == lib.EPI_SILU else N
+    wp = torch.empty_like(w)
+    lib.check(L.inferd_pack_weight(w.data_ptr(), N, K, wp.data_ptr(), lib.stream_ptr()))
+    c = torch.empty(a.shape[0], n_out, dtype=torch.bfloat16, device=DEV)
+    lib.check(L.inferd_gemm(a.data_ptr(), wp.data_ptr(), c.data_ptr(), None if r is None else r.data_ptr(),
+                            a.shape[0], n_out, K, epi, lib.stream_ptr()))
+    return c
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 33, 64, 65, 200, 1000])
+@pytest.mark.parametrize("N,K", [(256, 256), (1024, 4096), (384, 1024)])
+def test_gemm_plain_and_resid(lib, M, N, K):
+    torch.manual_seed(M * 7 + N)
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.03).to(torch.bfloat16)
+    ref = a.float() @ w.float().t()
+    c = _gemm(lib, a, w, lib.EPI_NONE)
+    err = (c.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-3, err
+    # bf16 rounding of an fp32 accumulator: within 1 ulp of the rounded fp32 reference
+    assert (bf16_ulp_diff(c.cpu(), ref.to(torch.bfloat16).cpu()) > 1).float().mean() < 1e-3
+    r = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    c2 = _gemm(lib, a, w, lib.EPI_RESID, r)
+    ref2 = (ref.to(torch.bfloat16).float() + r.float()).to(torch.bfloat16)
+    assert (bf16_ulp_diff(c2.cpu(), ref2.cpu()) > 1).float().mean() < 1e-3
+
+
+@pytest.mark.parametrize("M", [1, 16, 64, 300])
+def test_gemm_swiglu(lib, M):
+    torch.manual_seed(M)
+    I, K = 512, 1024
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    g = (torch.randn(I, K, device=DEV) * 0.03).to(torch.bfloat16)
+    u = (torch.randn(I, K, device=DEV) * 0.03).to(torch.bfloat16)
+    c = _gemm(lib, a, torch.cat([g, u], 0).contiguous(), lib.EPI_SILU)
+    # reference rounding points: F.silu(gate(x)) * up(x) in bf16
+    gr = (a.float() @ g.float().t()).to(torch.bfloat16)
+    ur = (a.float() @ u.float().t()).to(torch.bfloat16)
+    ref = torch.nn.functional.silu(gr) * ur
+    assert (bf16_ulp_diff(c.cpu(), ref.cpu()) > 2).float().mean() < 2e-3
+
+
+def test_qk_norm_rope_golden_and_cache(lib):
+    """QK-norm + RoPE vs the reference's own output (units.npz), K/V written to the cache."""
+    from golden_io import load, tensor
+    from kv_layout import read_kv
+    L = lib.load()
+    u = load("units.npz")
+    d = R.CONFIGS["qwen3-0.6b"]
+    W = R.gen_layer_weights(d, SEED, 3)
+    q, k = tensor(u["qkr_q"]), tensor(u["qkr_k"])  # (1,T,H,d), (1,T,KV,d)
+    T = q.shape[1]
+    v = torch.randn(1, T, d.kv_heads, 128).to(torch.bfloat16)
+    qkv = torch.cat([q.reshape(T, -1), k.reshape(T, -1), v.reshape(T, -1)], 1).contiguous().to(DEV)
+    pos = torch.from_numpy(u["qkr_pos"]).reshape(-1).to(torch.int32).to(DEV)
+    cos_t = torch.empty(40960, 64, dtype=torch.bfloat16, device=DEV)
+    sin_t = torch.empty_like(cos_t)
+    lib.check(L.inferd_rope_table(d.rope_theta, 128, 40960, cos_t.data_ptr(), sin_t.data_ptr(), lib.stream_ptr()))
+    pages = [3, 1, 5]
+    slots = torch.tensor([pages[(100 + i) // 64] * 64 + (100 + i) % 64 for i in range(T)], dtype=torch.int32, device=DEV)
+    kv = torch.zeros(8 * 2 * d.kv_heads * 64 * 128, dtype=torch.bfloat16, device=DEV)
+    q_out = torch.empty(T, d.heads, 128, dtype=torch.bfloat16, device=DEV)
+    qn_d, kn_d = W["q_norm"].to(DEV), W["k_norm"].to(DEV)
+    lib.check(L.inferd_qk_norm_rope_kv(qkv.data_ptr(), pos.data_ptr(), slots.data_ptr(), qn_d.data_ptr(),
+                                       kn_d.data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(),
+                                       q_out.data_ptr(), kv.data_ptr(), T, d.heads, d.kv_heads, d.eps,
+                                       lib.stream_ptr()))
+    qe = tensor(u["qkr_q_out"])[0].transpose(0, 1)  # (T,H,d)
+    ke = tensor(u["qkr_k_out"])[0]                  # (KV,T,d)
+    ulp = bf16_ulp_diff(q_out.cpu(), qe)
+    assert ulp.max() <= 1 and (ulp > 0).float().mean() < 5e-3
+    K, V = read_kv(kv, d.kv_heads, pages, 100 + T)
+    ulp = bf16_ulp_diff(K[:, 100:], ke)
+    assert ulp.max() <= 1 and (ulp > 0).float().mean() < 5e-3
+    assert torch.equal(V[:, 100:], v[0].transpose(0, 1))
+
+
+def test_rope_table_matches_hf(lib):
+    from golden_io import load, tensor
+    L = lib.load()
+    u = load("units.npz")
+    d = R.CONFIGS["qwen3-0.6b"]
+    cos_t = torch.empty(40960, 64, dtype=torch.bfloat16, device=DEV)
+    sin_t = torch.empty_like(cos_t)
+    lib.check(L.inferd_rope_table(d.rope_theta, 128, 40960, cos_t.data_ptr(), sin_t.data_ptr(), lib.stream_ptr()))
+    pos = torch.from_numpy(u["rope_pos"]).reshape(-1).long()
+    c_ref = tensor(u["rope_bf16_cos"])[0][:, :64]
+    s_ref = tensor(u["rope_bf16_sin"])[0][:, :64]
+    assert bf16_ulp_diff(cos_t.cpu()[pos], c_ref).max() <= 1
+    assert bf16_ulp_diff(sin_t.cpu()[pos], s_ref).max() <= 1
+    # dense check against the oracle table for the first 4096 positions
+    c, s = R.rope_cos_sin(d, torch.arange(4096)[None], torch.bfloat16)
+    ulp_c = bf16_ulp_diff(cos_t.cpu()[:4096], c[0, :, :64])
+    ulp_s = bf16_ulp_diff(sin_t.cpu()[:4096], s[0, :, :64])
+    assert ulp_c.max() <= 1 and (ulp_c > 0).float().mean() < 1e-3
+    assert ulp_s.max() <= 1 and (ulp_s > 0).float().mean() < 1e-3
+
+
+def _attn_case(lib, H, KV, q_lens, past_lens, seed=0):
+    """Random bf16 q/K/V; K/V written into shuffled pages; compare with fp32 SDPA."""
+    from inferd_amd.runtime import PagePool, SeqState, build_batch
+    from kv_layout import K_IDX, V_IDX
+    torch.manual_seed(seed)
+    L = lib.load()
+    pool = PagePool(256)
+    pool._free = list(np.random.default_rng(seed).permutation(256))
+    kv = torch.zeros(256 * 2 * KV * 64 * 128, dtype=torch.bfloat16)
+    blocks = kv.view(256, 2, KV, 64 * 128)
+    seqs, Ks, Vs, Qs = [], [], [], []
+    for T, P in zip(q_lens, past_lens):
+        st = SeqState()
+        n = T + P
+        st.pages = pool.alloc((n + 63) // 64)
+        st.length = P
+        K = (torch.randn(KV, n, 128) * 1.0).to(torch.bfloat16)
+        V = torch.randn(KV, n, 128).to(torch.bfloat16)
+        for pi, p in enumerate(st.pages):
+            kk = torch.zeros(KV, 64, 128, dtype=torch.bfloat16)
+            vv = torch.zeros(KV, 64, 128, dtype=torch.bfloat16)
+            m = min(64, n - pi * 64)
+            kk[:, :m] = K[:, pi * 64: pi * 64 + m]
+            vv[:, :m] = V[:, pi * 64: pi * 64 + m]
+            blocks[p, 0][:, K_IDX.reshape(-1)] = kk.reshape(KV, -1)
+            blocks[p, 1][:, V_IDX.reshape(-1)] = vv.reshape(KV, -1)
+        seqs.append((st, T))
+        Ks.append(K)
+        Vs.append(V)
+        Qs.append((torch.randn(T, H, 128) * 1.5).to(torch.bfloat16))
+    batch, keep = build_batch(seqs, DEV)
+    q = torch.cat(Qs, 0).contiguous().to(DEV)
+    out = torch.empty(q.shape[0], H * 128, dtype=torch.bfloat16, device=DEV)
+    ws_bytes = L.inferd_attention_workspace_bytes(len(seqs), H, max(t + p for t, p in zip(q_lens, past_lens)))
+    ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=DEV)
+    kv_d = kv.to(DEV)
+    lib.check(L.inferd_attention(q.data_ptr(), kv_d.data_ptr(), batch, H, KV, out.data_ptr(), ws.data_ptr(),
+                                 ws_bytes, lib.stream_ptr()))
+    torch.cuda.synchronize()
+    refs = []
+    for Q, K, V, (st, T) in zip(Qs, Ks, Vs, seqs):
+        o = R.attention(Q.float().transpose(0, 1)[None], K.float()[None], V.float()[None], st.length,
+                        128 ** -0.5, "sdpa")
+        refs.append(o[0].reshape(T, H * 128))
+    ref = torch.cat(refs, 0)
+    err = (out.cpu().float() - ref).abs()
+    return err, ref
+
+
+@pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (64, 8), (4, 2)])
+def test_attention_decode(lib, H, KV):
+    err, ref = _attn_case(lib, H, KV, [1] * 5, [0, 63, 64, 700, 2100], seed=H)
+    assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
+
+
+@pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2)])
+def test_attention_prefill(lib, H, KV):
+    err, ref = _attn_case(lib, H, KV, [1, 17, 64, 130], [0, 5, 0, 200], seed=H + 1)
+    assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()

@@ -1,0 +1,126 @@
+"""Span-level parity of the HIP path against the oracle and the reference's golden vectors.
+
+Tolerance (stated once, used everywhere below): a bf16 hidden state H_gpu matches the
+reference H_ref when  max|H_gpu - H_ref| <= TOL_REL * max|H_ref|  (per tensor), with
+TOL_REL = 2e-2 against the oracle run with the same attention semantics (sdpa) and
+3e-2 against the gRPC golden (eager attention rounds scores to bf16, the kernel keeps
+them in fp32).  Greedy tokens must be identical wherever the reference's top-1 margin
+exceeds MARGIN_FLOOR (in logit units); steps below it are reported, not silently passed.
+"""
+import pytest
+import torch
+
+from golden_io import load, tensor
+from oracle import qwen3_ref as R
+
+pytestmark = pytest.mark.gpu
+
+SEED = 1234
+DEV = "cuda"
+TOL_REL = 2e-2
+TOL_REL_EAGER = 3e-2
+MARGIN_FLOOR = 0.05
+
+
+def rel_err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def span(cfg, first, n, embed, lm, **kw):
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS[cfg]
+    s = SpanRuntime(d, first, n, has_embed=embed, has_lm_head=lm, device=DEV,
+                    max_positions=kw.pop("max_positions", 8192), **kw)
+    s.init_synthetic(SEED)
+    return s
+
+
+def test_tiny_two_spans_vs_golden():
+    g = load("tiny_petals.npz")
+    prompt = torch.from_numpy(g["prompt"])
+    s0 = span("tiny", 0, 2, True, False)
+    s1 = span("tiny", 2, 2, False, True)
+    o0 = s0.forward([(None, 16)], ids=prompt, want_layers=True)
+    o1 = s1.forward([(None, 16)], x=o0["hidden"], want_layers=True, want_next_ids=True, want_logits=True)
+    layers = torch.cat([o0["layers"], o1["layers"]], 0)
+    for i in range(4):
+        e = rel_err(layers[i], tensor(g[f"bf16_layer{i}"])[0])
+        print(f"tiny layer {i}: rel err {e:.2e}")
+        assert e < TOL_REL, (i, e)
+    lg = tensor(g["bf16_logits"])[0, -1]
+    e = rel_err(o1["logits"][0], lg)
+    print(f"tiny last-row logits rel err {e:.2e}")
+    assert e < TOL_REL
+    # greedy full-recompute loop (send_message.py:46-60 semantics): 8 steps
+    ids = prompt.tolist()
+    ref_ids = g["bf16_greedy_ids"].tolist()
+    b0 = R.RefSpan(R.CONFIGS["tiny"], SEED, 0, 1, True, False)
+    b1 = R.RefSpan(R.CONFIGS["tiny"], SEED, 2, 3, False, True)
+    for step in range(8):
+        x = torch.tensor(ids)
+        h = s0.forward([(None, len(ids))], ids=x)["hidden"]
+        nid = int(s1.forward([(None, len(ids))], x=h, want_next_ids=True, want_hidden=False)["next_ids"][0])
+        ref_logits = b1.forward(b0.forward(x[None]))[0, -1]
+        margin = R.top2_margin(ref_logits)
+        print(f"step {step}: gpu {nid} ref {ref_ids[step]} margin {margin:.4f}")
+        if margin > MARGIN_FLOOR:
+            assert nid == ref_ids[step], step
+        ids.append(ref_ids[step])  # teacher-forced: every step compares the same prefix
+
+
+def test_q06_layer_cached_vs_golden():
+    g = load("q06_layer.npz")
+    s = span("qwen3-0.6b", int(g["start"]), 1, False, False)
+    oracle = R.RefSpan(R.CONFIGS["qwen3-0.6b"], SEED, int(g["start"]), int(g["end"]), False, False,
+                       torch.bfloat16, "sdpa")
+    ins = [tensor(g["bf16_in_prefill"])] + [tensor(g[f"bf16_in_dec{i}"]) for i in range(4)]
+    for i, x in enumerate(ins):
+        T = x.shape[1]
+        out = s.forward([("sess", T)], x=x[0])["hidden"]
+        ref_o = oracle.forward_cached("sess", x)[0]
+        e_or = rel_err(out, ref_o)
+        e_gold = rel_err(out, tensor(g[f"bf16_out{i}"])[0])
+        print(f"q06 call {i}: vs oracle(sdpa) {e_or:.2e}  vs golden(eager) {e_gold:.2e}")
+        assert e_or < TOL_REL and e_gold < TOL_REL_EAGER
+
+
+def test_q8b_layer_batched_cached_vs_golden():
+    g = load("q8b_layer.npz")
+    s = span("qwen3-8b", int(g["start"]), 1, False, False, max_tokens=64)
+    ins = [tensor(g["bf16_in_prefill"])] + [tensor(g[f"bf16_in_dec{i}"]) for i in range(2)]
+    for i, x in enumerate(ins):
+        B, T = x.shape[0], x.shape[1]
+        out = s.forward([(f"s{b}", T) for b in range(B)], x=x.reshape(B * T, -1))["hidden"]
+        e = rel_err(out, tensor(g[f"bf16_out{i}"]).reshape(B * T, -1))
+        print(f"q8b call {i}: vs golden(eager) {e:.2e}")
+        assert e < TOL_REL_EAGER
+
+
+def test_q06_full_model_greedy_cached():
+    """Config 2: Qwen3-0.6B single full span, prefill 32 + cached greedy decode."""
+    d = R.CONFIGS["qwen3-0.6b"]
+    s = span("qwen3-0.6b", 0, d.layers, True, True)
+    oracle = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa")
+    prompt = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(5))
+    ids = prompt.tolist()
+    gpu_tokens, ref_tokens, margins = [], [], []
+    lg_ref = oracle.forward_cached("s", prompt[None])[0, -1]
+    out = s.forward([("s", 32)], ids=prompt, want_next_ids=True, want_logits=True, want_hidden=False)
+    for step in range(12):
+        gid = int(out["next_ids"][0])
+        rid = int(torch.argmax(lg_ref))
+        m = R.top2_margin(lg_ref)
+        e = rel_err(out["logits"][0], lg_ref)
+        gpu_tokens.append(gid)
+        ref_tokens.append(rid)
+        margins.append(m)
+        print(f"step {step}: gpu {gid} ref {rid} margin {m:.4f} logits rel err {e:.2e}")
+        assert e < 5e-2
+        if m > MARGIN_FLOOR:
+            assert gid == rid, step
+        nxt = torch.tensor([rid])
+        lg_ref = oracle.forward_cached("s", nxt[None])[0, -1]
+        out = s.forward([("s", 1)], ids=nxt, want_next_ids=True, want_logits=True, want_hidden=False)
+    agree = sum(a == b for a, b in zip(gpu_tokens, ref_tokens))
+    print(f"greedy agreement {agree}/{len(gpu_tokens)}")
