@@ -1,0 +1,256 @@
+"""Headline benchmark: decode tokens/s of the Qwen3-8B layer-span pipeline (BASELINE.json).
+
+Workload (BASELINE.json configs[2], the metric's config): Qwen3-8B, batch 16 decode at
+2k context.  Synthetic token ids, synthetic weights from the counter-based generator
+(no checkpoint is reachable offline).  One "step" = one decode step of every in-flight
+microbatch of 16 sequences through all 36 layers + final norm + lm_head + greedy argmax.
+
+  N = 1 : the whole model is one span on one GPU.
+  N > 1 : the 36 layers are split into N even spans, one per GPU/rank ([5,5,5,5,4,4,4,4]
+          at N = 8); N microbatches of 16 sequences are in flight; hidden states move
+          stage -> stage with RCCL send/recv over xGMI, greedy ids return last -> first.
+          Per-GPU work is fixed as N grows ("scaling": "weak").
+
+Before timing: every sequence is prefilled with 2048 tokens through the real prefill
+path (untimed; its rate is reported as `prefill`), so the KV cache holds real K/V.
+Timed region: K decode steps bracketed by barrier + synchronize; value = tokens of all
+ranks / max-over-ranks time.  Roofline: per-kernel HIP events recorded inside the timed
+region (inferd_span_profile_*); the dominant kernel class's algorithmic bytes per
+launch / its mean launch time, against 8 TB/s HBM.  cpu_baseline: the oracle
+(oracle/qwen3_ref.py, `port`) on the host cores, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFLOPS = 2500.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=32)
+    p.add_argument("--warmup", type=int, default=4)
+    p.add_argument("--model", default="qwen3-8b")
+    p.add_argument("--batch", type=int, default=16)
+    p.add_argument("--ctx", type=int, default=2048)
+    p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-layers", type=int, default=2, help="layers timed by the CPU baseline sample")
+    p.add_argument("--cpu-steps", type=int, default=3)
+    p.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
+    return p.parse_args()
+
+
+def even_split(n_layers: int, n: int):
+    base, extra = divmod(n_layers, n)
+    sizes = [base + (1 if i < extra else 0) for i in range(n)]
+    starts = [sum(sizes[:i]) for i in range(n)]
+    return list(zip(starts, sizes))
+
+
+# ------------------------------------------------------------------ algorithmic traffic
+def kernel_bytes(d, B: int, ctx_mean: float) -> dict:
+    """Algorithmic HBM bytes per launch of each kernel class for one decode step of B
+    sequences at mean context ctx_mean (weights read once, activations read/written once,
+    KV read once per layer)."""
+    h, I, H, KV, hd = d.hidden, d.intermediate, d.heads, d.kv_heads, d.head_dim
+    qkvN = (H + 2 * KV) * hd
+    return {
+        "rmsnorm": 2 * B * h * 2 + h * 2,
+        "qkv_gemm": qkvN * h * 2 + B * h * 2 + B * qkvN * 2,
+        "qk_norm_rope_kv": B * qkvN * 2 + B * H * hd * 2 + B * 2 * KV * hd * 2 + 2 * B * 64 * 2 * 2,
+        "attention": B * ctx_mean * 2 * KV * hd * 2 + B * H * hd * 2 * 2,
+        "o_gemm": h * H * hd * 2 + B * H * hd * 2 + 2 * B * h * 2,
+        "gateup_gemm": 2 * I * h * 2 + B * h * 2 + B * I * 2,
+        "down_gemm": h * I * 2 + B * I * 2 + 2 * B * h * 2,
+        "lm_head_argmax": d.vocab * h * 2 + B * h * 2,
+    }
+
+
+def step_bytes(d, n_layers: int, B: int, ctx_mean: float, lm_head: bool) -> float:
+    kb = kernel_bytes(d, B, ctx_mean)
+    per_layer = sum(kb[k] for k in ("qkv_gemm", "qk_norm_rope_kv", "attention", "o_gemm", "gateup_gemm",
+                                    "down_gemm")) + 2 * kb["rmsnorm"]
+    return n_layers * per_layer + (kb["lm_head_argmax"] if lm_head else 0)
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_baseline(d_name: str, B: int, ctx: int, seed: int, n_layers_sample: int, n_steps: int) -> dict:
+    """Oracle (`port`) decode on the host cores: a bounded sample of `n_layers_sample`
+    Qwen3-8B layers x `n_steps` decode steps at B x ctx (KV cache pre-filled with random
+    bf16 K/V: the decode-step cost does not depend on the cached values), plus the
+    lm_head once; tokens/s extrapolated to the full 36-layer model."""
+    from oracle import qwen3_ref as R
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    d = R.CONFIGS[d_name]
+    sp = R.RefSpan(d, seed, 0, n_layers_sample - 1, False, False, torch.bfloat16, "sdpa")
+    g = torch.Generator().manual_seed(0)
+    caches = []
+    for _ in range(n_layers_sample):
+        c = R.LayerCache()
+        c.k = torch.randn((B, d.kv_heads, ctx, d.head_dim), generator=g).to(torch.bfloat16)
+        c.v = torch.randn((B, d.kv_heads, ctx, d.head_dim), generator=g).to(torch.bfloat16)
+        caches.append(c)
+    sp.sessions["bench"] = caches
+    x = torch.randn((B, 1, d.hidden), generator=g).to(torch.bfloat16)
+    sp.forward_cached("bench", x)   # warm-up (1 step)
+    t0 = time.perf_counter()
+    for _ in range(n_steps):
+        sp.forward_cached("bench", x)
+    t_layers = (time.perf_counter() - t0) / n_steps / n_layers_sample
+    gw = R.gen_global_weights(d, seed)
+    hn = R.rms_norm(x[:, -1], gw["norm"], d.eps)
+    torch.nn.functional.linear(hn, gw["lm_head"])
+    t0 = time.perf_counter()
+    torch.argmax(torch.nn.functional.linear(R.rms_norm(x[:, -1], gw["norm"], d.eps), gw["lm_head"]), -1)
+    t_head = time.perf_counter() - t0
+    t_step = t_layers * d.layers + t_head
+    return {"value": round(B / t_step, 3), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/qwen3_ref.py bf16 on {threads} host threads: {n_layers_sample} Qwen3-8B layers x "
+                      f"{n_steps} decode steps at B={B}, ctx={ctx} (random KV) + lm_head once; "
+                      f"{t_layers * 1e3:.1f} ms/layer-step extrapolated to {d.layers} layers "
+                      f"({t_step:.2f} s/step)"}
+
+
+# ------------------------------------------------------------------ main
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from inferd_amd import pipeline as P
+    from inferd_amd.runtime import MODELS
+
+    d = MODELS[args.model]
+    B, ctx, K, W = args.batch, args.ctx, args.steps, args.warmup
+    spans = even_split(d.layers, world)
+    first, n_layers = spans[rank]
+    n_mb = world                                   # microbatches in flight
+    st = P.PipelineStage(d, rank, world, first, n_layers, device=dev, seed=args.seed,
+                         n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + 64,
+                         prefill_chunk=args.prefill_chunk)
+    # ---- prefill (untimed): every microbatch's sequences get `ctx` real tokens
+    g = torch.Generator().manual_seed(args.seed + 17)
+    prompts = [torch.randint(0, d.vocab, (B, ctx), generator=g) for _ in range(n_mb)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    st.prefill(prompts)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t_prefill = time.perf_counter() - t0
+    # ---- decode: warmup + timed
+    st.prepare_decode(W + K)
+    st.decode(W)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    if not args.no_profile:
+        st.span.profile_start(1 << 17)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st.decode(K)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = None if args.no_profile else st.span.profile_stop()
+    t = torch.tensor([elapsed, t_prefill], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, t_prefill = float(t[0]), float(t[1])
+
+    tokens = K * n_mb * B
+    value = tokens / elapsed
+    ms_per_step = elapsed / K * 1e3
+    ctx_mean = ctx + W + (K + 1) / 2.0
+    kb = kernel_bytes(d, B, ctx_mean)
+
+    # dominant kernel class of this rank (by total event time) -> roofline
+    roof, kernels = None, None
+    if prof:
+        kernels = {}
+        for name, (ms, n) in prof.items():
+            if n == 0:
+                continue
+            avg_us = ms / n * 1e3
+            gbs = kb[name] / (avg_us * 1e-6) / 1e9
+            kernels[name] = {"launches": n, "avg_us": round(avg_us, 2), "total_ms": round(ms, 3),
+                             "alg_bytes": int(kb[name]), "GB/s": round(gbs, 1),
+                             "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic_r01.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                tr = json.load(f)
+            if tr.get("workload") == f"{args.model}-decode-B{B}-ctx{ctx}" and dom in tr.get("per_launch_bytes", {}):
+                traffic = tr["per_launch_bytes"][dom]
+        roof = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["GB/s"], "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": kernels[dom]["frac"], "traffic": traffic,
+                "alg_bytes_per_launch": kernels[dom]["alg_bytes"]}
+
+    if rank == 0:
+        sb = step_bytes(d, d.layers, B, ctx_mean, True) * n_mb
+        out = {
+            "metric": "decode tokens/sec, Qwen3-8B layer-span pipeline",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic token ids + counter-generated synthetic weights (no checkpoint offline)",
+            "config": {"workload": f"{args.model} greedy decode, batch {B} per microbatch at {ctx} context "
+                                   f"(prefilled), {n_mb} microbatch(es) in flight",
+                       "global_batch": B * n_mb, "seq_len": ctx, "parallelism": f"pp{world}",
+                       "spans": [n for _, n in spans]},
+            "roofline": roof,
+            "roofline_step": {"bound": "hbm", "alg_bytes_per_step": int(sb),
+                              "achieved": round(sb / (ms_per_step * 1e-3) / 1e9 / world, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s per GPU",
+                              "frac": round(sb / (ms_per_step * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4)},
+            "kernels": kernels,
+            "prefill": {"tokens": n_mb * B * ctx, "seconds": round(t_prefill, 3),
+                        "tokens_per_s": round(n_mb * B * ctx / t_prefill, 1)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            st.release()
+            out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers, args.cpu_steps)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -125,6 +125,21 @@ int inferd_span_forward(InferdSpan* span, const InferdBatch* batch, const int32_
                         const void* x_in, void* x_out, int32_t* next_ids, void* logits,
                         void* layer_out, void* stream);
 
+/* Per-kernel-class timing: HIP events recorded on the launch stream around every kernel of
+ * the forward (classes below), up to max_pairs pairs; stop() synchronises on the events
+ * and returns the summed milliseconds and launch counts per class. */
+#define INFERD_PROF_NORM 0
+#define INFERD_PROF_QKV 1
+#define INFERD_PROF_ROPE 2
+#define INFERD_PROF_ATTN 3
+#define INFERD_PROF_O 4
+#define INFERD_PROF_GATEUP 5
+#define INFERD_PROF_DOWN 6
+#define INFERD_PROF_LMHEAD 7
+#define INFERD_PROF_NCLASSES 8
+int inferd_span_profile_start(InferdSpan* span, int32_t max_pairs);
+int inferd_span_profile_stop(InferdSpan* span, double* total_ms, int32_t* counts, int32_t n_classes);
+
 /* Device base pointer of one layer's KV pool ([pages][K|V][kv_heads][64*128] bf16). */
 int inferd_span_kv_layer(InferdSpan* span, int32_t layer, void** out);
 /* Zero the KV pool. */

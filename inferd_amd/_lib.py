@@ -15,6 +15,8 @@ LIB_PATH = os.path.join(_HERE, "libinferd_span.so")
 INFERD_OK = 0
 EPI_NONE, EPI_RESID, EPI_SILU = 0, 1, 2
 KV_PAGE = 64
+PROF_CLASSES = ("rmsnorm", "qkv_gemm", "qk_norm_rope_kv", "attention", "o_gemm", "gateup_gemm", "down_gemm",
+                "lm_head_argmax")
 
 # symbol -> (restype, argtypes); the header is the source of truth
 c_i32, c_i64, c_u64, c_u32, c_f, c_p = C.c_int32, C.c_int64, C.c_uint64, C.c_uint32, C.c_float, C.c_void_p
@@ -40,6 +42,8 @@ SIGNATURES = {
     "inferd_span_init_synthetic": (C.c_int, [c_p, c_u64, c_p]),
     "inferd_span_set_weight": (C.c_int, [c_p, c_i32, C.c_char_p, c_p, c_i64, c_i64, c_p]),
     "inferd_span_forward": (C.c_int, [c_p, C.POINTER(Batch), c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "inferd_span_profile_start": (C.c_int, [c_p, c_i32]),
+    "inferd_span_profile_stop": (C.c_int, [c_p, C.POINTER(C.c_double), C.POINTER(c_i32), c_i32]),
     "inferd_span_kv_layer": (C.c_int, [c_p, c_i32, C.POINTER(c_p)]),
     "inferd_span_kv_clear": (C.c_int, [c_p, c_p]),
     "inferd_weightgen": (C.c_int, [c_p, c_i64, c_u64, c_u32, c_f, c_f, c_p]),

@@ -63,6 +63,9 @@ const uint32_t T_EMBED = 0xFFFF0000u, T_NORM = 0xFFFF0001u, T_LM = 0xFFFF0002u;
 const float LINEAR_SCALE = 0.034641016151377546f;  // float32(0.02 * sqrt(3))
 const float NORM_SCALE = 0.1f;
 
+// kernel classes timed by inferd_span_profile_* (order = INFERD_PROF_* in the header)
+enum { PROF_NORM = 0, PROF_QKV, PROF_ROPE, PROF_ATTN, PROF_O, PROF_GATEUP, PROF_DOWN, PROF_LMHEAD, PROF_NCLS };
+
 uint64_t tensor_key(uint64_t seed, uint32_t tid) {
   return splitmix64(((seed & 0xFFFFFFFFull) << 32) | (uint64_t)tid);
 }
@@ -87,9 +90,27 @@ struct InferdSpan {
   unsigned long long* argmax_partial = nullptr;
   int32_t* err = nullptr;
   std::vector<void*> allocs;
+  // optional per-kernel-class timing with HIP events on the launch stream
+  bool prof_on = false;
+  std::vector<hipEvent_t> prof_events;
+  std::vector<int> prof_class;
+  size_t prof_used = 0;
 
   ~InferdSpan() {
+    for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
+  }
+  // returns the pair index or -1
+  long prof_begin(int cls, hipStream_t st) {
+    if (!prof_on || prof_used + 2 > prof_events.size()) return -1;
+    long i = (long)prof_used;
+    prof_used += 2;
+    prof_class[i / 2] = cls;
+    (void)hipEventRecord(prof_events[i], st);
+    return i;
+  }
+  void prof_end(long i, hipStream_t st) {
+    if (i >= 0) (void)hipEventRecord(prof_events[i + 1], st);
   }
   int alloc(void** p, size_t bytes) {
     hipError_t e = hipMalloc(p, bytes < 256 ? 256 : bytes);
@@ -344,23 +365,40 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   if (c.n_layers == 0 && x_out && x != x_out)
     HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
   const AttnBatch ab = to_attn(b);
+  long pe;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
     u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
+    pe = s->prof_begin(PROF_NORM, st);
     launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
+    s->prof_end(pe, st);
+    pe = s->prof_begin(PROF_QKV, st);
     launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st);
+    s->prof_end(pe, st);
+    pe = s->prof_begin(PROF_ROPE, st);
     launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
                            s->sin_t, s->q, kv_l, M, H, KV, c.rms_eps, st);
+    s->prof_end(pe, st);
+    pe = s->prof_begin(PROF_ATTN, st);
     if (b->decode)
       launch_attn_decode(s->q, kv_l, ab, H, KV, scale, s->attn, s->attn_ws, st);
     else
       launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
+    s->prof_end(pe, st);
     // h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
+    pe = s->prof_begin(PROF_O, st);
     launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);
+    s->prof_end(pe, st);
+    pe = s->prof_begin(PROF_NORM, st);
     launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
+    s->prof_end(pe, st);
+    pe = s->prof_begin(PROF_GATEUP, st);
     launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st);
+    s->prof_end(pe, st);
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
+    pe = s->prof_begin(PROF_DOWN, st);
     launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, st);
+    s->prof_end(pe, st);
     x = out;
     if (layer_out)
       HIP_TRY(hipMemcpyAsync((u16*)layer_out + (size_t)l * M * h, x, (size_t)M * h * 2,
@@ -370,12 +408,48 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   if (c.has_lm_head && (next_ids || logits)) {
     if (B > 64) return fail(INFERD_ERR_ARG, "lm_head argmax supports <= 64 sequences per call");
     // last row of each sequence: seq_start[b+1] - 1
+    pe = s->prof_begin(PROF_LMHEAD, st);
     launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st);
     launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
                 s->argmax_partial, st);
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
+    s->prof_end(pe, st);
   }
   LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_span_profile_start(InferdSpan* s, int32_t max_pairs) {
+  if (!s || max_pairs <= 0) return fail(INFERD_ERR_ARG, "bad profile args");
+  while (s->prof_events.size() < (size_t)max_pairs * 2) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    s->prof_events.push_back(e);
+  }
+  s->prof_class.assign(s->prof_events.size() / 2, -1);
+  s->prof_used = 0;
+  s->prof_on = true;
+  return INFERD_OK;
+}
+
+extern "C" int inferd_span_profile_stop(InferdSpan* s, double* total_ms, int32_t* counts, int32_t n_classes) {
+  if (!s) return fail(INFERD_ERR_ARG, "null span");
+  s->prof_on = false;
+  for (int c = 0; c < n_classes; ++c) {
+    total_ms[c] = 0.0;
+    counts[c] = 0;
+  }
+  for (size_t i = 0; i + 1 < s->prof_used; i += 2) {
+    HIP_TRY(hipEventSynchronize(s->prof_events[i + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->prof_events[i], s->prof_events[i + 1]));
+    const int c = s->prof_class[i / 2];
+    if (c >= 0 && c < n_classes) {
+      total_ms[c] += ms;
+      counts[c] += 1;
+    }
+  }
+  s->prof_used = 0;
   return INFERD_OK;
 }
 

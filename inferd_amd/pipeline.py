@@ -1,0 +1,225 @@
+"""Multi-GPU layer-span pipeline: one process per GPU, one span per process, hidden states
+handed stage -> stage with RCCL send/recv over xGMI, greedy ids returned last -> first.
+
+This replaces, inside one node, the reference's chain of HTTP hops between span nodes
+(node.py:102-130 `send_to_next_node` POSTing base64 fp32 hidden states,
+partitioned_models.py:11-26) with device-to-device p2p transfers of bf16 hidden
+states.  Routing across nodes (DHT / path_finder / balancer) is untouched.
+
+Schedule (lockstep ring).  Work items are (decode step k, microbatch m), linearised as
+i = k * S + m for S stages and S microbatches in flight.  Stage s processes item i at
+tick i + s.  At the start of every tick each stage runs ONE grouped exchange
+(batch_isend_irecv): it sends the output it produced in the previous tick to its
+successor and receives the input for this tick from its predecessor; the last stage's
+successor is stage 0, which receives the greedy ids of item i - S (same microbatch, one
+step earlier) exactly when it needs them.  Every transfer is produced one tick before it
+is consumed, so in steady state all S stages compute every tick; grouping the send and
+the recv of a tick into one exchange keeps two-rank rings (where both directions share
+a communicator) deadlock-free.
+
+The compute of one item is delegated to an executor (SpanExecutor: the HIP span engine on
+this rank's GPU).  Tests drive the same schedule on CPU ranks (gloo) with an oracle
+executor.
+"""
+from __future__ import annotations
+
+import torch
+
+from .runtime import KV_PAGE, ModelDims, SeqState, SpanRuntime, build_batch
+
+
+class SpanExecutor:
+    """Runs one span's compute for pipeline items on this rank's GPU."""
+
+    def __init__(self, span: SpanRuntime):
+        self.span = span
+        self.device = span.device
+        self.dims = span.dims
+        self.has_embed, self.has_lm_head = span.has_embed, span.has_lm_head
+        self._decode = {}
+
+    # prefill: `sessions` get n_tokens new tokens each (ids on the first span, x otherwise)
+    def prefill(self, sessions, n_tokens, ids=None, x=None, want_ids=False):
+        out = self.span.forward([(sid, n_tokens) for sid in sessions], ids=ids, x=x,
+                                want_hidden=not want_ids, want_next_ids=want_ids)
+        return out["next_ids"] if want_ids else out["hidden"]
+
+    def prepare_decode(self, microbatches, n_steps):
+        """Prebuild the decode batch descriptor of every (step, microbatch) so the timed
+        loop does no host work beyond launching."""
+        self._decode = {}
+        for m, sessions in enumerate(microbatches):
+            states = [self.span.reserve(sid, n_steps) for sid in sessions]
+            for k in range(n_steps):
+                seqs = [(SeqState(pages=st.pages, length=st.length + k), 1) for st in states]
+                self._decode[(k, m)] = build_batch(seqs, self.device)
+            for st in states:
+                st.length += n_steps   # the cache will hold these tokens once the steps ran
+        self._step0 = 0
+
+    def decode(self, k, m, ids=None, x=None, hidden_out=None, ids_out=None):
+        batch, _ = self._decode[(self._step0 + k, m)]
+        self.span.run(batch, ids=ids, x=x, hidden=hidden_out, next_ids=ids_out)
+
+    def advance(self, n_steps):
+        self._step0 += n_steps
+
+
+class PipelineStage:
+    """One rank of the span pipeline (rank 0 = FirstStage, rank S-1 = LastStage)."""
+
+    def __init__(self, dims: ModelDims, rank: int, world: int, first_layer: int, n_layers: int, *,
+                 device, seed: int, n_microbatches: int, batch: int, max_ctx: int, prefill_chunk: int = 2,
+                 executor=None, group=None):
+        self.dims, self.rank, self.world = dims, rank, world
+        self.S = world
+        self.n_mb, self.B = n_microbatches, batch
+        self.device = torch.device(device)
+        self.group = group
+        self.prefill_chunk = prefill_chunk
+        if executor is None:
+            pages_per_seq = (max_ctx + KV_PAGE - 1) // KV_PAGE + 1
+            span = SpanRuntime(dims, first_layer, n_layers, has_embed=(rank == 0), has_lm_head=(rank == world - 1),
+                               kv_pages=n_microbatches * batch * pages_per_seq + 4,
+                               max_tokens=max(prefill_chunk * max_ctx, batch), max_seqs=max(batch, prefill_chunk),
+                               max_positions=max_ctx, device=self.device)
+            span.init_synthetic(seed)
+            executor = SpanExecutor(span)
+        self.ex = executor
+        self.span = getattr(executor, "span", None)
+        self.sessions = [[("mb", m, b) for b in range(batch)] for m in range(n_microbatches)]
+        h = dims.hidden
+        dev = self.device
+        self.ids = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in range(n_microbatches)]
+        self.h_in = [torch.empty(batch, h, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        self.h_out = [torch.empty(batch, h, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        self.ids_out = [torch.empty(batch, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.step_base = 0   # decode steps already run (absolute step of the next decode call)
+
+    # ------------------------------------------------------------------ comm
+    @property
+    def first(self):
+        return self.rank == 0
+
+    @property
+    def last(self):
+        return self.rank == self.S - 1
+
+    def _exchange(self, send=None, send_to=None, recv=None, recv_from=None):
+        import torch.distributed as dist
+        ops = []
+        if send is not None:
+            ops.append(dist.P2POp(dist.isend, send, send_to, self.group))
+        if recv is not None:
+            ops.append(dist.P2POp(dist.irecv, recv, recv_from, self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+
+    # ------------------------------------------------------------------ prefill
+    @torch.no_grad()
+    def prefill(self, prompts):
+        """prompts: per microbatch an int tensor [B, T] (read on the first stage only).
+        Runs every microbatch's prompt through the pipeline in chunks of prefill_chunk
+        sequences; leaves the first decode ids of every microbatch on stage 0."""
+        S, T = self.S, prompts[0].shape[1]
+        items = [(m, c) for m in range(self.n_mb) for c in range(0, self.B, self.prefill_chunk)]
+        h = self.dims.hidden
+        first_ids = [None] * self.n_mb
+        ids_parts = {}
+        bufs_in, bufs_out = {}, {}
+        n_ticks = len(items) + S  # +1 trailing tick for the last send
+        for t in range(n_ticks):
+            i_send = t - 1 - self.rank          # item produced last tick
+            i_cur = t - self.rank               # item computed this tick
+            send = recv = None
+            if not self.last and 0 <= i_send < len(items):
+                send = bufs_out.pop(i_send)
+            if not self.first and 0 <= i_cur < len(items):
+                m, c = items[i_cur]
+                nseq = min(self.prefill_chunk, self.B - c)
+                recv = torch.empty(nseq * T, h, dtype=torch.bfloat16, device=self.device)
+                bufs_in[i_cur] = recv
+            if S > 1:
+                self._exchange(send, (self.rank + 1) % S, recv, (self.rank - 1) % S)
+            if 0 <= i_cur < len(items):
+                m, c = items[i_cur]
+                sess = self.sessions[m][c:c + self.prefill_chunk]
+                if self.first:
+                    ids = prompts[m][c:c + len(sess)].reshape(-1).to(self.device, torch.int32)
+                    out = self.ex.prefill(sess, T, ids=ids, want_ids=self.last)
+                else:
+                    out = self.ex.prefill(sess, T, x=bufs_in.pop(i_cur), want_ids=self.last)
+                if self.last:
+                    ids_parts[(m, c)] = out
+                else:
+                    bufs_out[i_cur] = out
+        if self.last:
+            for m in range(self.n_mb):
+                first_ids[m] = torch.cat([ids_parts[(m, c)] for c in range(0, self.B, self.prefill_chunk)])
+        # hand the first decode ids to stage 0
+        if S == 1:
+            for m in range(self.n_mb):
+                self.ids[m].copy_(first_ids[m])
+        else:
+            flat = torch.empty(self.n_mb * self.B, dtype=torch.int32, device=self.device)
+            if self.last:
+                flat.copy_(torch.cat(first_ids))
+                self._exchange(send=flat, send_to=0)
+            elif self.first:
+                self._exchange(recv=flat, recv_from=S - 1)
+                for m in range(self.n_mb):
+                    self.ids[m].copy_(flat[m * self.B:(m + 1) * self.B])
+
+    # ------------------------------------------------------------------ decode
+    def prepare_decode(self, n_steps: int):
+        self.ex.prepare_decode(self.sessions, n_steps)
+
+    @torch.no_grad()
+    def decode(self, n_steps: int, record=None):
+        """Run n_steps decode steps of every microbatch.  `record` (stage 0 only): list that
+        receives (absolute step, microbatch, ids tensor copy) of every input fed to the first span."""
+        S = self.S
+        assert self.n_mb == S, "the ring schedule keeps exactly one microbatch per stage in flight"
+        n_items = n_steps * self.n_mb
+        if S == 1:
+            for i in range(n_items):
+                k, m = divmod(i, self.n_mb)
+                if record is not None:
+                    record.append((self.step_base + k, m, self.ids[m].clone()))
+                self.ex.decode(k, m, ids=self.ids[m], ids_out=self.ids_out[0])
+                self.ids[m].copy_(self.ids_out[0])
+            self.ex.advance(n_steps)
+            self.step_base += n_steps
+            return
+        for t in range(n_items + S):
+            i_cur = t - self.rank
+            i_prev = t - 1 - self.rank
+            send = recv = None
+            send_to = (self.rank + 1) % S
+            recv_from = (self.rank - 1) % S
+            if 0 <= i_prev < n_items:                      # output of last tick
+                send = self.ids_out[i_prev % 2] if self.last else self.h_out[i_prev % 2]
+            if self.first:
+                j = t - S                                  # ids of item j feed item j + S
+                if 0 <= j < n_items:
+                    recv = self.ids[j % self.n_mb]
+            elif 0 <= i_cur < n_items:
+                recv = self.h_in[i_cur % 2]
+            self._exchange(send, send_to, recv, recv_from)
+            if 0 <= i_cur < n_items:
+                k, m = divmod(i_cur, self.n_mb)
+                if self.first:
+                    if record is not None:
+                        record.append((self.step_base + k, m, self.ids[m].clone()))
+                    self.ex.decode(k, m, ids=self.ids[m], hidden_out=self.h_out[i_cur % 2])
+                elif self.last:
+                    self.ex.decode(k, m, x=self.h_in[i_cur % 2], ids_out=self.ids_out[i_cur % 2])
+                else:
+                    self.ex.decode(k, m, x=self.h_in[i_cur % 2], hidden_out=self.h_out[i_cur % 2])
+        self.ex.advance(n_steps)
+        self.step_base += n_steps
+
+    def release(self):
+        if self.span is not None:
+            self.span.release_all()

@@ -173,6 +173,32 @@ class SpanRuntime:
     def build_batch(self, seqs):
         return build_batch(seqs, self.device)
 
+    # ----------------------------------------------------------------- fast path
+    def run(self, batch, ids=None, x=None, hidden=None, next_ids=None, logits=None, layers=None, stream=None):
+        """Launch one span forward on a prebuilt Batch with caller-owned device tensors
+        (no host sync, no allocation).  Used by the pipeline runtime and the bench."""
+        _lib.check(self.lib.inferd_span_forward(self.handle, batch, _lib.ptr(ids), _lib.ptr(x), _lib.ptr(hidden),
+                                                _lib.ptr(next_ids), _lib.ptr(logits), _lib.ptr(layers),
+                                                _lib.stream_ptr(stream)))
+
+    def profile_start(self, max_pairs: int = 1 << 16):
+        _lib.check(self.lib.inferd_span_profile_start(self.handle, max_pairs))
+
+    def profile_stop(self) -> dict:
+        """{class: (total_ms, launches)} from the HIP events recorded since profile_start."""
+        import ctypes as C
+        n = len(_lib.PROF_CLASSES)
+        ms = (C.c_double * n)()
+        cnt = (C.c_int32 * n)()
+        _lib.check(self.lib.inferd_span_profile_stop(self.handle, ms, cnt, n))
+        return {name: (ms[i], cnt[i]) for i, name in enumerate(_lib.PROF_CLASSES)}
+
+    def reserve(self, session_id, n_tokens: int) -> SeqState:
+        """Make sure `session_id` has pages for n_tokens more tokens (no forward)."""
+        st = self.sessions.setdefault(session_id, SeqState())
+        self._reserve(st, n_tokens)
+        return st
+
     # ----------------------------------------------------------------- forward
     @torch.no_grad()
     def forward(self, requests, ids: torch.Tensor | None = None, x: torch.Tensor | None = None, *,

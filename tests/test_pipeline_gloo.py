@@ -1,0 +1,139 @@
+"""The pipeline schedule (inferd_amd/pipeline.py) on CPU ranks over gloo.
+
+Each rank runs its span with an oracle executor (tiny Qwen3, fp32, cached decode), so the
+test checks the multi-rank schedule itself: prefill chunking, the lockstep ring exchange,
+microbatch bookkeeping and the ids ring last -> first.  The greedy ids that reach stage 0
+must equal a single-process oracle run of the same model.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import qwen3_ref as R
+
+SEED = 1234
+
+
+class OracleExecutor:
+    """CPU stand-in for SpanExecutor: same interface, oracle compute (bf16)."""
+
+    def __init__(self, d, first, n_layers, first_span, last_span):
+        self.sp = R.RefSpan(d, SEED, first, first + n_layers - 1, first_span, last_span, torch.bfloat16, "sdpa")
+        self.device = torch.device("cpu")
+        self.has_embed, self.has_lm_head = first_span, last_span
+        self.dims = d
+
+    def _run(self, sessions, n, ids=None, x=None, want_ids=False):
+        outs = []
+        for i, sid in enumerate(sessions):
+            if ids is not None:
+                inp = ids.reshape(len(sessions), n)[i:i + 1].long()
+                o = self.sp.forward_cached(sid, inp)
+            else:
+                o = self.sp.forward_cached(sid, x.reshape(len(sessions), n, -1)[i:i + 1])
+            outs.append(o)
+        if self.sp.last:
+            return torch.stack([torch.argmax(o[0, -1]) for o in outs]).to(torch.int32)
+        return torch.cat([o[0] for o in outs]).to(torch.bfloat16)
+
+    def prefill(self, sessions, n_tokens, ids=None, x=None, want_ids=False):
+        return self._run(sessions, n_tokens, ids=ids, x=x)
+
+    def prepare_decode(self, microbatches, n_steps):
+        self.mbs = microbatches
+
+    def decode(self, k, m, ids=None, x=None, hidden_out=None, ids_out=None):
+        out = self._run(self.mbs[m], 1, ids=ids, x=x)
+        (ids_out if self.sp.last else hidden_out).copy_(out.reshape((ids_out if self.sp.last else hidden_out).shape))
+
+    def advance(self, n):
+        pass
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_steps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from inferd_amd.pipeline import PipelineStage
+    from bench import even_split
+    d = R.CONFIGS["tiny"]
+    first, n = even_split(d.layers, world)[rank]
+    ex = OracleExecutor(d, first, n, rank == 0, rank == world - 1)
+    B = 3
+    st = PipelineStage(d, rank, world, first, n, device="cpu", seed=SEED, n_microbatches=world, batch=B,
+                       max_ctx=64, prefill_chunk=2, executor=ex)
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(0, d.vocab, (B, 9), generator=g) for _ in range(world)]
+    st.prefill(prompts)
+    st.prepare_decode(n_steps)
+    rec = []
+    st.decode(2, record=rec)
+    st.decode(n_steps - 2, record=rec)
+    if rank == 0:
+        q.put([(k, m, t.tolist()) for k, m, t in rec] + [("final", m, st.ids[m].tolist()) for m in range(world)])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _reference(world, n_steps):
+    """Single process: the same spans chained directly (bf16 hand-off, like the pipeline)."""
+    from bench import even_split
+    d = R.CONFIGS["tiny"]
+    split = even_split(d.layers, world)
+    spans = [R.RefSpan(d, SEED, f, f + n - 1, i == 0, i == world - 1, torch.bfloat16, "sdpa")
+             for i, (f, n) in enumerate(split)]
+
+    class Chain:
+        def forward_cached(self, sid, x):
+            for s in spans:
+                x = s.forward_cached(sid, x)
+            return x
+    sp = Chain()
+    B = 3
+    g = torch.Generator().manual_seed(3)
+    prompts = [torch.randint(0, d.vocab, (B, 9), generator=g) for _ in range(world)]
+    feeds = {}
+    for m in range(world):
+        for b in range(B):
+            nxt = int(torch.argmax(sp.forward_cached((m, b), prompts[m][b:b + 1])[0, -1]))
+            for k in range(n_steps + 1):
+                feeds[(k, m, b)] = nxt
+                nxt = int(torch.argmax(sp.forward_cached((m, b), torch.tensor([[nxt]]))[0, -1]))
+    return feeds
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipeline_matches_single_process(world):
+    n_steps = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rec = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = _reference(world, n_steps)
+    seen = 0
+    for k, m, ids in rec:
+        if k == "final":
+            assert ids == [ref[(n_steps, m, b)] for b in range(3)]
+            continue
+        assert ids == [ref[(k, m, b)] for b in range(3)], (k, m)
+        seen += 1
+    assert seen == n_steps * world
