@@ -13,10 +13,12 @@ microbatch of 16 sequences through all 36 layers + final norm + lm_head + greedy
 
 Before timing: every sequence is prefilled with 2048 tokens through the real prefill
 path (untimed; its rate is reported as `prefill`), so the KV cache holds real K/V.
-Timed region: K decode steps bracketed by barrier + synchronize; value = tokens of all
-ranks / max-over-ranks time.  Roofline: per-kernel HIP events recorded inside the timed
-region (inferd_span_profile_*); the dominant kernel class's algorithmic bytes per
-launch / its mean launch time, against 8 TB/s HBM.  cpu_baseline: the oracle
+Timed region: K decode steps bracketed by barrier + synchronize; each stage's step of a
+microbatch is one replay of a captured HIP graph; value = tokens of all ranks /
+max-over-ranks time.  Roofline: per-kernel HIP events (inferd_span_profile_*) on the
+launch stream over `--profile-steps` eager decode steps of the same workload run right
+after the timed region (events cannot be recorded inside a replayed graph); the dominant
+kernel class's algorithmic bytes per launch / its mean launch time, against 8 TB/s HBM.  cpu_baseline: the oracle
 (oracle/qwen3_ref.py, `port`) on the host cores, rank 0 at N = 1 only.
 """
 from __future__ import annotations
@@ -48,7 +50,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-layers", type=int, default=2, help="layers timed by the CPU baseline sample")
     p.add_argument("--cpu-steps", type=int, default=3)
-    p.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    p.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing pass")
+    p.add_argument("--profile-steps", type=int, default=8, help="eager event-instrumented decode steps")
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
     return p.parse_args()
 
@@ -149,7 +152,7 @@ def main():
     first, n_layers = spans[rank]
     n_mb = world                                   # microbatches in flight
     st = P.PipelineStage(d, rank, world, first, n_layers, device=dev, seed=args.seed,
-                         n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + 64,
+                         n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + args.profile_steps + 64,
                          prefill_chunk=args.prefill_chunk)
     # ---- prefill (untimed): every microbatch's sequences get `ctx` real tokens
     g = torch.Generator().manual_seed(args.seed + 17)
@@ -163,14 +166,12 @@ def main():
     if dist:
         dist.barrier()
     t_prefill = time.perf_counter() - t0
-    # ---- decode: warmup + timed
+    # ---- decode: warmup + timed (one captured HIP graph replay per stage per microbatch step)
     st.prepare_decode(W + K)
     st.decode(W)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    if not args.no_profile:
-        st.span.profile_start(1 << 17)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     st.decode(K)
@@ -178,7 +179,9 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    prof = None if args.no_profile else st.span.profile_stop()
+    # ---- per-kernel HIP-event timings: the same decode kernels launched eagerly (events
+    # cannot live inside a replayed graph); right after the timed region, same cache state
+    prof = None if args.no_profile else st.profile_decode(args.profile_steps)
     t = torch.tensor([elapsed, t_prefill], dtype=torch.float64, device=dev)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -187,7 +190,7 @@ def main():
     tokens = K * n_mb * B
     value = tokens / elapsed
     ms_per_step = elapsed / K * 1e3
-    ctx_mean = ctx + W + (K + 1) / 2.0
+    ctx_mean = ctx + W + K + (args.profile_steps + 1) / 2.0   # context during the profiled steps
     kb = kernel_bytes(d, B, ctx_mean)
 
     # dominant kernel class of this rank (by total event time) -> roofline

@@ -125,6 +125,24 @@ int inferd_span_forward(InferdSpan* span, const InferdBatch* batch, const int32_
                         const void* x_in, void* x_out, int32_t* next_ids, void* logits,
                         void* layer_out, void* stream);
 
+/* Decode graphs.  Captures one span forward of `batch` (same arguments as
+ * inferd_span_forward) into a HIP graph.  With advance = 1 the graph starts with a
+ * device-side scheduler step: for every sequence b the new token goes to position
+ * ctx_lens[b], its slot comes from the block table, and ctx_lens[b] grows by one -- the
+ * batch arrays are mutated in place, so repeated launches walk the sequences forward one
+ * token per launch with no host work (the caller reserves the pages beforehand and sets
+ * max_ctx_len to the capacity; sequences running out of pages set error flag bit 2).
+ * `ids` and `next_ids` may be the same buffer (the step reads ids first).  Replaces the
+ * per-token client loop over the chain (client.py:244-266, send_message.py:46-60). */
+typedef struct InferdGraph InferdGraph;
+int inferd_span_graph_capture(InferdSpan* span, const InferdBatch* batch, int32_t advance,
+                              const int32_t* ids, const void* x_in, void* x_out, int32_t* next_ids,
+                              void* stream, InferdGraph** out);
+int inferd_graph_launch(InferdGraph* graph, void* stream);
+void inferd_graph_destroy(InferdGraph* graph);
+/* Sticky device error flags (bit 0: token id out of range, bit 1: decode slot overflow). */
+int inferd_span_error_flags(InferdSpan* span, int32_t* flags);
+
 /* Per-kernel-class timing: HIP events recorded on the launch stream around every kernel of
  * the forward (classes below), up to max_pairs pairs; stop() synchronises on the events
  * and returns the summed milliseconds and launch counts per class. */

@@ -266,6 +266,34 @@ void launch_embed(const int32_t* ids, const u16* table, int M, int N, int vocab,
   hipLaunchKernelGGL(embed_kernel, dim3(M), dim3(256), 0, s, ids, table, N, vocab, out, err);
 }
 
+// ------------------------------------------------------------------ decode-step advance
+// Device-side scheduler step for a captured decode graph: the new token of sequence b sits
+// at position ctx_lens[b] (the cached length), writes its K/V to the slot the block table
+// gives for that position, and the cached length grows by one.  Runs as the first node of
+// the graph, so a replay needs no host work.  A sequence whose block table is full gets
+// slot -1 (no cache write) and sets err bit 2.
+__global__ void decode_advance_kernel(int32_t* __restrict__ positions, int32_t* __restrict__ slots,
+                                      int32_t* __restrict__ ctx_lens, const int32_t* __restrict__ block_table,
+                                      int max_pages, int B, int32_t* __restrict__ err) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int p = ctx_lens[b];
+  positions[b] = p;
+  if (p / KV_PAGE < max_pages) {
+    slots[b] = block_table[(int64_t)b * max_pages + p / KV_PAGE] * KV_PAGE + p % KV_PAGE;
+    ctx_lens[b] = p + 1;
+  } else {
+    slots[b] = -1;
+    atomicOr(err, 2);
+  }
+}
+
+void launch_decode_advance(int32_t* positions, int32_t* slots, int32_t* ctx_lens, const int32_t* block_table,
+                           int max_pages, int B, int32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(decode_advance_kernel, dim3((B + 63) / 64), dim3(64), 0, s, positions, slots, ctx_lens,
+                     block_table, max_pages, B, err);
+}
+
 // ------------------------------------------------------------------ argmax key decode
 // key = (float_key(bf16 logit) << 32) | (0xFFFFFFFF - index): max key = max logit, lowest index
 __global__ void argmax_decode_kernel(const unsigned long long* __restrict__ keys, int B,

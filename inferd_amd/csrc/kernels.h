@@ -27,6 +27,8 @@ void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positi
 void launch_embed(const int32_t* ids, const u16* table, int M, int N, int vocab, u16* out,
                   int32_t* err, hipStream_t s);
 void launch_argmax_decode(const unsigned long long* keys, int B, int32_t* ids, hipStream_t s);
+void launch_decode_advance(int32_t* positions, int32_t* slots, int32_t* ctx_lens, const int32_t* block_table,
+                           int max_pages, int B, int32_t* err, hipStream_t s);
 
 // gemm.hip.  Wp is fragment-packed (common.h).  N counts OUTPUT columns: for EPI_SILU the
 // packed weight holds 2N rows ([gate; up]).  For EPI_ARGMAX `partial` receives

@@ -419,6 +419,62 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   return INFERD_OK;
 }
 
+// ------------------------------------------------------------------ decode graphs
+struct InferdGraph {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  ~InferdGraph() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+  }
+};
+
+extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, int32_t advance, const int32_t* ids,
+                                         const void* x_in, void* x_out, int32_t* next_ids, void* stream,
+                                         InferdGraph** out) {
+  if (!s || !b || !out) return fail(INFERD_ERR_ARG, "null argument");
+  if (!stream) return fail(INFERD_ERR_ARG, "graph capture needs a non-null stream");
+  if (advance && !b->decode) return fail(INFERD_ERR_ARG, "advance needs a decode batch");
+  hipStream_t st = (hipStream_t)stream;
+  s->prof_on = false;  // events are not captured
+  HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  int rc = INFERD_OK;
+  if (advance)
+    launch_decode_advance((int32_t*)b->positions, (int32_t*)b->slots, (int32_t*)b->ctx_lens, b->block_table,
+                          b->max_pages, b->n_seqs, s->err, st);
+  rc = inferd_span_forward(s, b, ids, x_in, x_out, next_ids, nullptr, nullptr, stream);
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(st, &g);
+  if (rc) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) return fail(INFERD_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  InferdGraph* G = new InferdGraph();
+  G->graph = g;
+  e = hipGraphInstantiate(&G->exec, g, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    delete G;
+    return fail(INFERD_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+  }
+  *out = G;
+  return INFERD_OK;
+}
+
+extern "C" int inferd_graph_launch(InferdGraph* g, void* stream) {
+  if (!g) return fail(INFERD_ERR_ARG, "null graph");
+  HIP_TRY(hipGraphLaunch(g->exec, (hipStream_t)stream));
+  return INFERD_OK;
+}
+
+extern "C" void inferd_graph_destroy(InferdGraph* g) { delete g; }
+
+extern "C" int inferd_span_error_flags(InferdSpan* s, int32_t* flags) {
+  if (!s || !flags) return fail(INFERD_ERR_ARG, "null argument");
+  HIP_TRY(hipMemcpy(flags, s->err, 4, hipMemcpyDeviceToHost));
+  return INFERD_OK;
+}
+
 extern "C" int inferd_span_profile_start(InferdSpan* s, int32_t max_pairs) {
   if (!s || max_pairs <= 0) return fail(INFERD_ERR_ARG, "bad profile args");
   while (s->prof_events.size() < (size_t)max_pairs * 2) {

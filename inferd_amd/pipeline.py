@@ -17,15 +17,18 @@ is consumed, so in steady state all S stages compute every tick; grouping the se
 the recv of a tick into one exchange keeps two-rank rings (where both directions share
 a communicator) deadlock-free.
 
-The compute of one item is delegated to an executor (SpanExecutor: the HIP span engine on
-this rank's GPU).  Tests drive the same schedule on CPU ranks (gloo) with an oracle
+Every microbatch owns fixed device buffers (ids / hidden in / hidden out / ids out), so
+the decode compute of (stage, microbatch) is one replay of a captured HIP graph whose
+first node advances that microbatch's positions on the device (runtime.DecodeGraph).
+The compute of one item is delegated to an executor (SpanExecutor: the HIP span engine
+on this rank's GPU); tests drive the same schedule on CPU ranks (gloo) with an oracle
 executor.
 """
 from __future__ import annotations
 
 import torch
 
-from .runtime import KV_PAGE, ModelDims, SeqState, SpanRuntime, build_batch
+from .runtime import KV_PAGE, DecodeGraph, ModelDims, SeqState, SpanRuntime, build_batch
 
 
 class SpanExecutor:
@@ -36,33 +39,39 @@ class SpanExecutor:
         self.device = span.device
         self.dims = span.dims
         self.has_embed, self.has_lm_head = span.has_embed, span.has_lm_head
-        self._decode = {}
+        self.graphs = []
 
-    # prefill: `sessions` get n_tokens new tokens each (ids on the first span, x otherwise)
     def prefill(self, sessions, n_tokens, ids=None, x=None, want_ids=False):
+        """`sessions` each get n_tokens new tokens (ids on the first span, x otherwise)."""
         out = self.span.forward([(sid, n_tokens) for sid in sessions], ids=ids, x=x,
                                 want_hidden=not want_ids, want_next_ids=want_ids)
         return out["next_ids"] if want_ids else out["hidden"]
 
-    def prepare_decode(self, microbatches, n_steps):
-        """Prebuild the decode batch descriptor of every (step, microbatch) so the timed
-        loop does no host work beyond launching."""
-        self._decode = {}
-        for m, sessions in enumerate(microbatches):
-            states = [self.span.reserve(sid, n_steps) for sid in sessions]
-            for k in range(n_steps):
-                seqs = [(SeqState(pages=st.pages, length=st.length + k), 1) for st in states]
-                self._decode[(k, m)] = build_batch(seqs, self.device)
-            for st in states:
-                st.length += n_steps   # the cache will hold these tokens once the steps ran
-        self._step0 = 0
+    def prepare_decode(self, microbatches, n_steps, bufs):
+        """Capture one decode graph per microbatch over its fixed buffers
+        (bufs[m]: dict with ids / x / hidden_out / next_ids device tensors or None)."""
+        self.graphs = [DecodeGraph(self.span, sessions, n_steps, **bufs[m])
+                       for m, sessions in enumerate(microbatches)]
 
-    def decode(self, k, m, ids=None, x=None, hidden_out=None, ids_out=None):
-        batch, _ = self._decode[(self._step0 + k, m)]
-        self.span.run(batch, ids=ids, x=x, hidden=hidden_out, next_ids=ids_out)
+    def decode(self, m):
+        self.graphs[m].launch()
 
-    def advance(self, n_steps):
-        self._step0 += n_steps
+    def profile_decode(self, microbatches, bufs, n_steps):
+        """Eager (non-graph) decode steps with per-kernel HIP events, for kernel timings.
+        Returns {kernel class: (total ms, launches)}."""
+        self.span.profile_start(1 << 17)
+        for _ in range(n_steps):
+            for m, sessions in enumerate(microbatches):
+                states = [self.span.reserve(sid, 1) for sid in sessions]
+                batch, keep = build_batch([(st, 1) for st in states], self.device)
+                b = bufs[m]
+                self.span.run(batch, ids=b.get("ids"), x=b.get("x"), hidden=b.get("hidden_out"),
+                              next_ids=b.get("next_ids"))
+                for st in states:
+                    st.length += 1
+                del keep
+        torch.cuda.synchronize(self.device)
+        return self.span.profile_stop()
 
 
 class PipelineStage:
@@ -71,6 +80,7 @@ class PipelineStage:
     def __init__(self, dims: ModelDims, rank: int, world: int, first_layer: int, n_layers: int, *,
                  device, seed: int, n_microbatches: int, batch: int, max_ctx: int, prefill_chunk: int = 2,
                  executor=None, group=None):
+        assert n_microbatches == world, "the ring schedule keeps exactly one microbatch per stage in flight"
         self.dims, self.rank, self.world = dims, rank, world
         self.S = world
         self.n_mb, self.B = n_microbatches, batch
@@ -90,13 +100,13 @@ class PipelineStage:
         self.sessions = [[("mb", m, b) for b in range(batch)] for m in range(n_microbatches)]
         h = dims.hidden
         dev = self.device
-        self.ids = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in range(n_microbatches)]
-        self.h_in = [torch.empty(batch, h, dtype=torch.bfloat16, device=dev) for _ in range(2)]
-        self.h_out = [torch.empty(batch, h, dtype=torch.bfloat16, device=dev) for _ in range(2)]
-        self.ids_out = [torch.empty(batch, dtype=torch.int32, device=dev) for _ in range(2)]
+        mb = range(n_microbatches)
+        self.ids = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
+        self.h_in = [torch.zeros(batch, h, dtype=torch.bfloat16, device=dev) for _ in mb]
+        self.h_out = [torch.zeros(batch, h, dtype=torch.bfloat16, device=dev) for _ in mb]
+        self.ids_out = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
         self.step_base = 0   # decode steps already run (absolute step of the next decode call)
 
-    # ------------------------------------------------------------------ comm
     @property
     def first(self):
         return self.rank == 0
@@ -104,6 +114,16 @@ class PipelineStage:
     @property
     def last(self):
         return self.rank == self.S - 1
+
+    def _bufs(self, m):
+        """Fixed buffers of microbatch m for this stage's role."""
+        if self.S == 1:
+            return {"ids": self.ids[m], "x": None, "hidden_out": None, "next_ids": self.ids[m]}
+        if self.first:
+            return {"ids": self.ids[m], "x": None, "hidden_out": self.h_out[m], "next_ids": None}
+        if self.last:
+            return {"ids": None, "x": self.h_in[m], "hidden_out": None, "next_ids": self.ids_out[m]}
+        return {"ids": None, "x": self.h_in[m], "hidden_out": self.h_out[m], "next_ids": None}
 
     def _exchange(self, send=None, send_to=None, recv=None, recv_from=None):
         import torch.distributed as dist
@@ -128,8 +148,7 @@ class PipelineStage:
         first_ids = [None] * self.n_mb
         ids_parts = {}
         bufs_in, bufs_out = {}, {}
-        n_ticks = len(items) + S  # +1 trailing tick for the last send
-        for t in range(n_ticks):
+        for t in range(len(items) + S):
             i_send = t - 1 - self.rank          # item produced last tick
             i_cur = t - self.rank               # item computed this tick
             send = recv = None
@@ -173,53 +192,50 @@ class PipelineStage:
 
     # ------------------------------------------------------------------ decode
     def prepare_decode(self, n_steps: int):
-        self.ex.prepare_decode(self.sessions, n_steps)
+        """Reserve cache pages for n_steps tokens per sequence and capture the decode graphs."""
+        self.ex.prepare_decode(self.sessions, n_steps, [self._bufs(m) for m in range(self.n_mb)])
 
     @torch.no_grad()
     def decode(self, n_steps: int, record=None):
         """Run n_steps decode steps of every microbatch.  `record` (stage 0 only): list that
         receives (absolute step, microbatch, ids tensor copy) of every input fed to the first span."""
         S = self.S
-        assert self.n_mb == S, "the ring schedule keeps exactly one microbatch per stage in flight"
         n_items = n_steps * self.n_mb
         if S == 1:
             for i in range(n_items):
                 k, m = divmod(i, self.n_mb)
                 if record is not None:
                     record.append((self.step_base + k, m, self.ids[m].clone()))
-                self.ex.decode(k, m, ids=self.ids[m], ids_out=self.ids_out[0])
-                self.ids[m].copy_(self.ids_out[0])
-            self.ex.advance(n_steps)
+                self.ex.decode(m)
             self.step_base += n_steps
             return
         for t in range(n_items + S):
             i_cur = t - self.rank
             i_prev = t - 1 - self.rank
             send = recv = None
-            send_to = (self.rank + 1) % S
-            recv_from = (self.rank - 1) % S
             if 0 <= i_prev < n_items:                      # output of last tick
-                send = self.ids_out[i_prev % 2] if self.last else self.h_out[i_prev % 2]
+                mp = i_prev % self.n_mb
+                send = self.ids_out[mp] if self.last else self.h_out[mp]
             if self.first:
                 j = t - S                                  # ids of item j feed item j + S
                 if 0 <= j < n_items:
                     recv = self.ids[j % self.n_mb]
             elif 0 <= i_cur < n_items:
-                recv = self.h_in[i_cur % 2]
-            self._exchange(send, send_to, recv, recv_from)
+                recv = self.h_in[i_cur % self.n_mb]
+            self._exchange(send, (self.rank + 1) % S, recv, (self.rank - 1) % S)
             if 0 <= i_cur < n_items:
                 k, m = divmod(i_cur, self.n_mb)
-                if self.first:
-                    if record is not None:
-                        record.append((self.step_base + k, m, self.ids[m].clone()))
-                    self.ex.decode(k, m, ids=self.ids[m], hidden_out=self.h_out[i_cur % 2])
-                elif self.last:
-                    self.ex.decode(k, m, x=self.h_in[i_cur % 2], ids_out=self.ids_out[i_cur % 2])
-                else:
-                    self.ex.decode(k, m, x=self.h_in[i_cur % 2], hidden_out=self.h_out[i_cur % 2])
-        self.ex.advance(n_steps)
+                if self.first and record is not None:
+                    record.append((self.step_base + k, m, self.ids[m].clone()))
+                self.ex.decode(m)
         self.step_base += n_steps
+
+    def profile_decode(self, n_steps: int):
+        """Per-kernel timings from eager (event-instrumented) decode steps on this stage,
+        without exchanges (kernel durations do not depend on where inputs came from)."""
+        return self.ex.profile_decode(self.sessions, [self._bufs(m) for m in range(self.n_mb)], n_steps)
 
     def release(self):
         if self.span is not None:
+            self.ex.graphs = []
             self.span.release_all()

@@ -104,6 +104,59 @@ def build_batch(seqs, device):
     return b, dev
 
 
+class DecodeGraph:
+    """One decode step of a fixed set of sessions captured as a HIP graph
+    (inferd_span_graph_capture with advance=1): every launch decodes one more token of
+    each session, reading `ids` (first span) or `x`, writing `hidden_out` and/or
+    `next_ids` -- fixed device buffers chosen at capture.  `ids` and `next_ids` may alias
+    (greedy feedback on a single-span model).  Pages for `n_steps` tokens are reserved
+    up front; launching more than n_steps times raises."""
+
+    def __init__(self, span: "SpanRuntime", sessions, n_steps: int, ids=None, x=None, hidden_out=None,
+                 next_ids=None):
+        self.span, self.n_steps, self.launched = span, n_steps, 0
+        self.states = [span.reserve(sid, n_steps) for sid in sessions]
+        B = len(self.states)
+        max_pages = max(len(st.pages) for st in self.states)
+        table = []
+        for st in self.states:
+            table.extend(st.pages + [0] * (max_pages - len(st.pages)))
+        lengths = [st.length for st in self.states]
+        host = torch.tensor(list(range(B + 1)) + [0] * B + [0] * B + lengths + table, dtype=torch.int32)
+        self.buf = host.to(span.device)
+        base = self.buf.data_ptr()
+        o = [0, B + 1, 2 * B + 1, 3 * B + 1, 4 * B + 1]
+        self.batch = _lib.Batch(n_seqs=B, n_tokens=B, max_q_len=1, max_ctx_len=max(lengths) + n_steps,
+                                max_pages=max_pages, decode=1, seq_start=base + 4 * o[0],
+                                positions=base + 4 * o[1], slots=base + 4 * o[2], ctx_lens=base + 4 * o[3],
+                                block_table=base + 4 * o[4])
+        self._keep = (ids, x, hidden_out, next_ids)
+        cur = torch.cuda.current_stream(span.device)
+        cs = torch.cuda.Stream(span.device)
+        cs.wait_stream(cur)
+        g = _lib.c_p()
+        with torch.cuda.device(span.device):
+            _lib.check(span.lib.inferd_span_graph_capture(span.handle, self.batch, 1, _lib.ptr(ids), _lib.ptr(x),
+                                                          _lib.ptr(hidden_out), _lib.ptr(next_ids),
+                                                          cs.cuda_stream, g))
+        cur.wait_stream(cs)
+        self.graph = g
+
+    def launch(self, stream=None):
+        if self.launched >= self.n_steps:
+            raise RuntimeError("decode graph ran out of reserved steps")
+        _lib.check(self.span.lib.inferd_graph_launch(self.graph, _lib.stream_ptr(stream)))
+        self.launched += 1
+        for st in self.states:
+            st.length += 1
+
+    def __del__(self):
+        g = getattr(self, "graph", None)
+        if g is not None and g.value:
+            self.span.lib.inferd_graph_destroy(g)
+            self.graph = None
+
+
 class SpanRuntime:
     """One layer span on one GPU (FirstStage / StageInner / LastStage compute)."""
 

@@ -97,6 +97,32 @@ def test_q8b_layer_batched_cached_vs_golden():
         assert e < TOL_REL_EAGER
 
 
+def test_decode_graph_matches_eager():
+    """A captured decode step (device-side position advance + whole span) replayed n times
+    gives bit-identical ids/logit-argmax to n eager cached decode calls."""
+    from inferd_amd.runtime import DecodeGraph
+    d = R.CONFIGS["tiny"]
+    prompts = torch.randint(0, d.vocab, (3, 70), generator=torch.Generator().manual_seed(9))
+    runs = []
+    for use_graph in (False, True):
+        s = span("tiny", 0, d.layers, True, True)
+        sess = [f"g{b}" for b in range(3)]
+        out = s.forward([(sid, 70) for sid in sess], ids=prompts.reshape(-1), want_next_ids=True, want_hidden=False)
+        ids = out["next_ids"].clone()
+        seq = [ids.cpu().clone()]
+        if use_graph:
+            g = DecodeGraph(s, sess, 6, ids=ids, next_ids=ids)
+            for _ in range(6):
+                g.launch()
+                seq.append(ids.cpu().clone())
+        else:
+            for _ in range(6):
+                ids = s.forward([(sid, 1) for sid in sess], ids=ids, want_next_ids=True, want_hidden=False)["next_ids"]
+                seq.append(ids.cpu().clone())
+        runs.append(torch.stack(seq))
+    assert torch.equal(runs[0], runs[1]), (runs[0], runs[1])
+
+
 def test_q06_full_model_greedy_cached():
     """Config 2: Qwen3-0.6B single full span, prefill 32 + cached greedy decode."""
     d = R.CONFIGS["qwen3-0.6b"]

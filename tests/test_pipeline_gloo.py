@@ -43,15 +43,14 @@ class OracleExecutor:
     def prefill(self, sessions, n_tokens, ids=None, x=None, want_ids=False):
         return self._run(sessions, n_tokens, ids=ids, x=x)
 
-    def prepare_decode(self, microbatches, n_steps):
-        self.mbs = microbatches
+    def prepare_decode(self, microbatches, n_steps, bufs):
+        self.mbs, self.bufs = microbatches, bufs
 
-    def decode(self, k, m, ids=None, x=None, hidden_out=None, ids_out=None):
-        out = self._run(self.mbs[m], 1, ids=ids, x=x)
-        (ids_out if self.sp.last else hidden_out).copy_(out.reshape((ids_out if self.sp.last else hidden_out).shape))
-
-    def advance(self, n):
-        pass
+    def decode(self, m):
+        b = self.bufs[m]
+        out = self._run(self.mbs[m], 1, ids=b["ids"], x=b["x"])
+        dst = b["next_ids"] if self.sp.last else b["hidden_out"]
+        dst.copy_(out.reshape(dst.shape))
 
 
 def _free_port():
