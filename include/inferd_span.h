@@ -186,7 +186,9 @@ int inferd_qk_norm_rope_kv(const void* qkv, const int32_t* positions, const int3
                            const void* q_norm_w, const void* k_norm_w, const void* cos_t,
                            const void* sin_t, void* q_out, void* kv_layer, int32_t m,
                            int32_t heads, int32_t kv_heads, float eps, void* stream);
-/* causal GQA attention of q [M][H][128] over the paged cache -> out [M][H*128] */
+/* causal GQA attention of q [M][H][128] over the paged cache -> out [M][H*128].
+ * Decode batches use `workspace` (inferd_attention_workspace_bytes); it must be
+ * zero-filled before its first use, and every call leaves its counter block zero. */
 int inferd_attention(const void* q, const void* kv_layer, const InferdBatch* batch,
                      int32_t heads, int32_t kv_heads, void* out, void* workspace,
                      int64_t workspace_bytes, void* stream);

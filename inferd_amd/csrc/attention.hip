@@ -15,11 +15,12 @@
 #include "common.h"
 #include "kernels.h"
 
+#include <stdlib.h>
+
 #define LOG2E 1.4426950408889634f
 
 // One 64-token page of online-softmax attention for one wave.
-// qf: Q^T fragments (4 k-steps of 32 dims); pos_lim: keys t with t <= pos_lim[col] are
-// visible (lane-local column limit).
+// qf: Q^T fragments (4 k-steps of 32 dims); keys t <= lim are visible (lane-local limit).
 __device__ __forceinline__ void attend_page(const u16* __restrict__ kblk, const u16* __restrict__ vblk,
                                             const bf16x8 (&qf)[4], int page_tok0, int lim,
                                             float scale_log2, float& m_i, float& l_i,
@@ -81,22 +82,40 @@ __device__ __forceinline__ void attend_page(const u16* __restrict__ kblk, const 
 }
 
 // ------------------------------------------------------------------ decode (1 token/seq)
-// grid (n_chunks, KV, B), 4 waves; wave w handles pages [chunk*4*ppw + w*ppw, +ppw).
-// Writes unnormalised partial O and (m, l) per (seq, kv head, chunk, head-in-group).
+// Workgroup (chunk, g, b) = 4 waves; wave w attends pages [chunk*4*ppw + w*ppw, +ppw) of
+// sequence b for the n_rep query heads of kv head g; the 4 waves merge through LDS.  A
+// sequence with a single chunk writes its output directly.  Otherwise every chunk stores
+// its unnormalised partial (O, m, l) and the LAST chunk to arrive merges all chunks
+// (fixed chunk order -> deterministic) and resets the counter.  Hand-off per
+// cdna_hip_programming.md §6 Guideline 16 (write-through form): sc1 partial stores -> every
+// wave s_waitcnt vmcnt(0) -> barrier -> lane 0 relaxed agent fetch_add; the last arriver:
+// agent acquire fence + vmcnt(0) + barrier -> plain loads.
+// The merge is parallel: per-chunk scale factors first (LDS), then independent loads.
+// Workspace: [DECODE_COUNTER_BYTES of u32 counters | partials, PART_STRIDE f32 per head].
+#define PART_STRIDE (HEAD_DIM + 4)
+#define DECODE_COUNTER_BYTES 65536   // B * KV <= 16384; zero before first use, left zero
+#define MAX_DECODE_CHUNKS 64
+
 __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict__ q,
-                                                          const u16* __restrict__ kv,
-                                                          AttnBatch b, int H, int KV, int ppw,
-                                                          float scale_log2, int n_chunks,
-                                                          float* __restrict__ ws) {
+                                                          const u16* __restrict__ kv, AttnBatch b,
+                                                          int H, int KV, int ppw, float scale_log2,
+                                                          int n_chunks_max,
+                                                          unsigned* __restrict__ counters,
+                                                          float* __restrict__ part,
+                                                          u16* __restrict__ out) {
   __shared__ float sm_m[4][16], sm_l[4][16];
   __shared__ float sm_o[4][16][HEAD_DIM + 4];
+  __shared__ float sm_f[MAX_DECODE_CHUNKS][16];
+  __shared__ float sm_L[16];
+  __shared__ int sm_last;
   const int chunk = blockIdx.x, g = blockIdx.y, bseq = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_rep = H / KV;
   const int ctx = b.ctx_lens[bseq];
   const int n_pages = (ctx + KV_PAGE - 1) / KV_PAGE;
-  const int p_begin = chunk * 4 * ppw;
-  if (p_begin >= n_pages) return;  // uniform over the workgroup
+  const int cp = 4 * ppw;
+  const int nc = (n_pages + cp - 1) / cp;
+  if (chunk >= nc) return;  // uniform over the workgroup
   const int tok = b.seq_start[bseq + 1] - 1;
   const int hn = lane & 15;
   bf16x8 qf[4];
@@ -113,15 +132,15 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict_
 #pragma unroll
   for (int db = 0; db < 8; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
-  for (int pp = 0; pp < ppw; ++pp) {
-    const int pi = p_begin + wave * ppw + pp;
-    if (pi >= n_pages) break;
+  const int p0 = chunk * cp + wave * ppw;
+  const int p1 = min(n_pages, p0 + ppw);
+  for (int pi = p0; pi < p1; ++pi) {
     const int phys = bt[pi];
     const u16* kblk = kv + ((int64_t)(phys * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
     const u16* vblk = kv + ((int64_t)(phys * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
     attend_page(kblk, vblk, qf, pi * KV_PAGE, ctx - 1, scale_log2, m_i, l_i, o, lane);
   }
-  // combine the 4 waves of this chunk through LDS
+  // merge the 4 waves of this chunk through LDS
   if (lane < 16) {
     sm_m[wave][lane] = m_i;
     sm_l[wave][lane] = l_i;
@@ -131,10 +150,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict_
 #pragma unroll
     for (int r = 0; r < 4; ++r) sm_o[wave][hn][db * 16 + 4 * (lane >> 4) + r] = o[db][r];
   __syncthreads();
-  float* wsb = ws + (((int64_t)bseq * KV + g) * n_chunks + chunk) * 16 * (HEAD_DIM + 2);
+  u16* op = out + (int64_t)tok * H * HEAD_DIM + (int64_t)g * n_rep * HEAD_DIM;
+  const int stride = n_rep * PART_STRIDE;
+  float* base = part + ((int64_t)bseq * KV + g) * n_chunks_max * stride;
   for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += 256) {
     const int n = idx / HEAD_DIM, d = idx % HEAD_DIM;
-    float M = fmaxf(fmaxf(sm_m[0][n], sm_m[1][n]), fmaxf(sm_m[2][n], sm_m[3][n]));
+    const float M = fmaxf(fmaxf(sm_m[0][n], sm_m[1][n]), fmaxf(sm_m[2][n], sm_m[3][n]));
     float acc = 0.f, L = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -142,52 +163,82 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict_
       acc += sm_o[w][n][d] * f;
       L += sm_l[w][n] * f;
     }
-    wsb[n * (HEAD_DIM + 2) + d] = acc;
-    if (d == 0) {
-      wsb[n * (HEAD_DIM + 2) + HEAD_DIM] = M;
-      wsb[n * (HEAD_DIM + 2) + HEAD_DIM + 1] = L;
+    if (nc == 1) {
+      op[n * HEAD_DIM + d] = f2bf(acc / L);
+    } else {
+      // write-through (sc1) partial stores: visible chip-wide once drained, no release fence
+      float* pc = base + (int64_t)chunk * stride + n * PART_STRIDE;
+      __hip_atomic_store(pc + d, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == 0) {
+        __hip_atomic_store(pc + HEAD_DIM, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(pc + HEAD_DIM + 1, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
-}
-
-// grid (H, B), 128 threads: merge the chunks of one (seq, head) and normalise.
-__global__ __launch_bounds__(128) void attn_decode_combine_kernel(AttnBatch b, int H, int KV,
-                                                                  int ppw, int n_chunks,
-                                                                  const float* __restrict__ ws,
-                                                                  u16* __restrict__ out) {
-  const int h = blockIdx.x, bseq = blockIdx.y, d = threadIdx.x;
-  const int n_rep = H / KV, g = h / n_rep, n = h % n_rep;
-  const int ctx = b.ctx_lens[bseq];
-  const int n_pages = (ctx + KV_PAGE - 1) / KV_PAGE;
-  const int nc = (n_pages + 4 * ppw - 1) / (4 * ppw);
-  const float* base = ws + ((int64_t)bseq * KV + g) * n_chunks * 16 * (HEAD_DIM + 2) + n * (HEAD_DIM + 2);
-  float M = -INFINITY;
-  for (int c = 0; c < nc; ++c) M = fmaxf(M, base[(int64_t)c * 16 * (HEAD_DIM + 2) + HEAD_DIM]);
-  float acc = 0.f, L = 0.f;
-  for (int c = 0; c < nc; ++c) {
-    const float* p = base + (int64_t)c * 16 * (HEAD_DIM + 2);
-    const float f = exp2f(p[HEAD_DIM] - M);
-    acc += p[d] * f;
-    L += p[HEAD_DIM + 1] * f;
+  if (nc == 1) return;
+  // publish the partial (every storing wave drains, then one ticket); the last chunk merges
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev =
+        __hip_atomic_fetch_add(&counters[bseq * KV + g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm_last = (prev == (unsigned)(nc - 1));
+    if (sm_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&counters[bseq * KV + g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
-  const int tok = b.seq_start[bseq + 1] - 1;
-  out[(int64_t)tok * H * HEAD_DIM + h * HEAD_DIM + d] = f2bf(acc / L);
+  __syncthreads();
+  if (!sm_last) return;
+  // per-chunk scale factors f[c][n] = 2^(m_c - M_n) and the normaliser L_n
+  for (int idx = threadIdx.x; idx < nc * n_rep; idx += 256) {
+    const int c = idx / n_rep, n = idx % n_rep;
+    sm_f[c][n] = base[(int64_t)c * stride + n * PART_STRIDE + HEAD_DIM];
+  }
+  __syncthreads();
+  if (threadIdx.x < n_rep) {
+    const int n = threadIdx.x;
+    float M = -INFINITY;
+    for (int c = 0; c < nc; ++c) M = fmaxf(M, sm_f[c][n]);
+    float L = 0.f;
+    for (int c = 0; c < nc; ++c) {
+      const float f = exp2f(sm_f[c][n] - M);
+      sm_f[c][n] = f;
+      L += base[(int64_t)c * stride + n * PART_STRIDE + HEAD_DIM + 1] * f;
+    }
+    sm_L[n] = L;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += 256) {
+    const int n = idx / HEAD_DIM, d = idx % HEAD_DIM;
+    const float* pc = base + n * PART_STRIDE + d;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int c = 0; c < nc; ++c) acc += pc[(int64_t)c * stride] * sm_f[c][n];
+    op[n * HEAD_DIM + d] = f2bf(acc / sm_L[n]);
+  }
 }
 
 static int decode_ppw(int B, int KV, int max_ctx) {
+  static int env = -2;
+  if (env == -2) {
+    const char* e = getenv("INFERD_DECODE_PPW");
+    env = e ? atoi(e) : -1;
+  }
   const int n_pages = (max_ctx + KV_PAGE - 1) / KV_PAGE;
-  // aim for >= ~4096 waves in flight over the chip
-  int ppw = (B * KV * n_pages + 4095) / 4096;
+  // ~2 four-wave workgroups per CU (512) over the (seq, kv-head, page) stream: measured on
+  // B=16 x 2.1k ctx x 8 kv heads, 1 page/wave 31.8 us, 2: 29.9, 4: 28.2, 8: 33.7
+  int ppw = env > 0 ? env : (B * KV * n_pages + 4 * 512 - 1) / (4 * 512);
   if (ppw < 1) ppw = 1;
-  if (ppw > 16) ppw = 16;
-  return ppw;
+  // chunks of 4*ppw pages; at most MAX_DECODE_CHUNKS chunks per sequence
+  const int min_ppw = (n_pages + 4 * MAX_DECODE_CHUNKS - 1) / (4 * MAX_DECODE_CHUNKS);
+  return ppw < min_ppw ? min_ppw : ppw;
 }
 
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx) {
-  // upper bound over kv-head counts: chunks computed with ppw = 1
-  const int n_pages = (max_ctx + KV_PAGE - 1) / KV_PAGE;
-  const int n_chunks = (n_pages + 3) / 4;
-  return (size_t)B * H * n_chunks * 16 * (HEAD_DIM + 2) * sizeof(float);
+  // worst case over kv-head counts (KV <= H): MAX_DECODE_CHUNKS chunks of n_rep heads
+  return DECODE_COUNTER_BYTES + (size_t)B * H * MAX_DECODE_CHUNKS * PART_STRIDE * sizeof(float);
 }
 
 void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
@@ -195,10 +246,10 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
   const int ppw = decode_ppw(b.B, KV, b.max_ctx);
   const int n_pages = (b.max_ctx + KV_PAGE - 1) / KV_PAGE;
   const int n_chunks = (n_pages + 4 * ppw - 1) / (4 * ppw);
-  hipLaunchKernelGGL(attn_decode_kernel, dim3(n_chunks, KV, b.B), dim3(256), 0, s, q, kv_layer, b,
-                     H, KV, ppw, scale * LOG2E, n_chunks, ws);
-  hipLaunchKernelGGL(attn_decode_combine_kernel, dim3(H, b.B), dim3(HEAD_DIM), 0, s, b, H, KV, ppw,
-                     n_chunks, (const float*)ws, out);
+  unsigned* counters = (unsigned*)ws;
+  float* part = (float*)((char*)ws + DECODE_COUNTER_BYTES);
+  hipLaunchKernelGGL(attn_decode_kernel, dim3(n_chunks, KV, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, ppw,
+                     scale * LOG2E, n_chunks, counters, part, out);
 }
 
 // ------------------------------------------------------------------ prefill (causal)

@@ -6,10 +6,14 @@
 //
 // Two kernels, both on v_mfma_f32_16x16x32_bf16 with weights in the fragment-packed
 // layout of common.h:
-//  * gemm_skinny: M <= 64 rows (decode).  HBM-bound weight stream: one workgroup per
-//    16-column tile, the K range split across its waves, every weight tile fetched
-//    exactly once straight into VGPRs (1 KiB dwordx4 per wave-instruction), partial
-//    sums reduced through LDS, epilogue fused.
+//  * gemm_decode: M <= 64 rows.  HBM-bound weight stream.  Workgroup = 4 waves = one
+//    16-column output tile x one K slice of 4*TW k-tiles; every wave issues ALL of its
+//    TW weight-tile loads (1 KiB dwordx4 each) and activation fragments up front, then
+//    its MFMAs; the 4 waves reduce through LDS.  K slices (KS per tile) spread the stream
+//    over >= ~2 workgroups per CU; slices combine deterministically: each stores its fp32
+//    partial write-through (sc1, 16 B per lane), takes a ticket on the tile's counter, and
+//    the last arriver sums the KS partials in slice order and runs the fused epilogue
+//    (cdna_hip_programming.md §5 "In-launch split-K reduction", sc1 form).
 //  * gemm_tiled: M > 64 rows (prefill).  128x128x64 block tile, 4 waves (2x2, 64x64
 //    each), A and B staged through double-buffered LDS with global_load_lds (A
 //    XOR-swizzled on the source address, B already fragment-ordered), 32 MFMA per
@@ -17,19 +21,26 @@
 #include "common.h"
 #include "kernels.h"
 
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g)); }
 
-// ============================================================ skinny (decode) kernel
-template <int MT, int NW, int EPI>
-__global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(
-    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles,
+// ============================================================ decode (M <= 64) kernel
+template <int MT, int S, int TW, int EPI>
+__global__ __launch_bounds__(256) void gemm_decode_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles, int KS,
     u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    unsigned long long* __restrict__ partial) {
-  constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
-  __shared__ float red[NW * S * MT * 256];
-  const int nt = blockIdx.x;
+    unsigned long long* __restrict__ keys, float* __restrict__ slab, unsigned slab_bytes,
+    unsigned* __restrict__ counters) {
+  constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
+  __shared__ f32x4 red[4][NV];
+  __shared__ int sm_last;
+  const int nt = blockIdx.x / KS, ks = blockIdx.x - (blockIdx.x / KS) * KS;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int kt0 = (wave * KT) / NW, kt1 = ((wave + 1) * KT) / NW;
+  // slice [k0, k1) of the K tiles; processed in rounds of 4*TW tiles (one round when the
+  // dispatcher could choose KS = ceil(KT / (4*TW))), wave w taking TW consecutive tiles
+  const int SL = (KT + KS - 1) / KS;
+  const int k0 = ks * SL, k1 = min(KT, k0 + SL);
   const bf16x8* w0 = (const bf16x8*)(Wp + (int64_t)nt * KT * 512) + lane;
   const bf16x8* w1 = (const bf16x8*)(Wp + (int64_t)(nt + n_tiles) * KT * 512) + lane;
   const u16* a[MT];
@@ -39,112 +50,163 @@ __global__ __launch_bounds__(NW * 64) void gemm_skinny_kernel(
     row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
     a[mt] = A + (int64_t)row * lda + 8 * (lane >> 4);
   }
+  const bf16x8 zero = as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   f32x4 acc[S][MT];
 #pragma unroll
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[s][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  constexpr int U = (MT <= 2) ? 8 : 4;
-  int kt = kt0;
-  for (; kt + U <= kt1; kt += U) {
-    bf16x8 wv[S][U];
-    bf16x8 av[U][MT];
+  for (int kr = k0 + wave * TW; kr < k1; kr += 4 * TW) {
+    bf16x8 wv[S][TW];
+    bf16x8 av[TW][MT];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      wv[0][u] = w0[(kt + u) * 64];
-      if constexpr (S == 2) wv[1][u] = w1[(kt + u) * 64];
+    for (int u = 0; u < TW; ++u) {
+      const int kt = kr + u;
+      const bool ok = kt < k1;
+      wv[0][u] = ok ? w0[kt * 64] : zero;
+      if constexpr (S == 2) wv[1][u] = ok ? w1[kt * 64] : zero;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < TW; ++u) {
+      const int kt = kr + u;
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) av[u][mt] = *(const bf16x8*)(a[mt] + (kt + u) * 32);
+      for (int mt = 0; mt < MT; ++mt) av[u][mt] = (kt < k1) ? *(const bf16x8*)(a[mt] + kt * 32) : zero;
+    }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < TW; ++u)
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[u][mt], wv[s][u], acc[s][mt]);
   }
-  for (; kt < kt1; ++kt) {
-    bf16x8 wv0 = w0[kt * 64];
-    bf16x8 wv1;
-    if constexpr (S == 2) wv1 = w1[kt * 64];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      bf16x8 av = *(const bf16x8*)(a[mt] + kt * 32);
-      acc[0][mt] = mfma16(av, wv0, acc[0][mt]);
-      if constexpr (S == 2) acc[1][mt] = mfma16(av, wv1, acc[1][mt]);
-    }
-  }
-  // cross-wave reduction: red[wave][s][mt][r][lane]
 #pragma unroll
   for (int s = 0; s < S; ++s)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[(((wave * S + s) * MT + mt) * 4 + r) * 64 + lane] = acc[s][mt][r];
+    for (int mt = 0; mt < MT; ++mt) red[wave][(s * MT + mt) * 64 + lane] = acc[s][mt];
   __syncthreads();
-  for (int idx = threadIdx.x; idx < MT * 256; idx += NW * 64) {
-    const int mt = idx >> 8, r = (idx >> 6) & 3, ln = idx & 63;
-    float v[S];
+  // thread p < MT*64 owns (mt, lane ln) of every stream s: rows mt*16 + 4*(ln>>4) + r, col ln&15
+  const int p = threadIdx.x;
+  const bool own = p < MT * 64;
+  f32x4 v[S];
+  if (own) {
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) t += red[(((w * S + s) * MT + mt) * 4 + r) * 64 + ln];
-      v[s] = t;
+      const int q = s * MT * 64 + p;
+      v[s] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
     }
+  }
+  if (KS > 1) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, slab_bytes, 0x00020000);
+    if (own) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const unsigned off = (unsigned)((((int64_t)nt * KS + ks) * NV + s * MT * 64 + p) * 16);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v[s]), rs, off, 0, 16);  // sc1
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(&counters[nt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sm_last = prev == (unsigned)(KS - 1);
+      if (sm_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&counters[nt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __syncthreads();
+    if (!sm_last) return;
+    if (own) {
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < KS; ++k)
+          t += *(const f32x4*)(slab + ((((int64_t)nt * KS + k) * NV + s * MT * 64 + p) * 4));
+        v[s] = t;
+      }
+    }
+  }
+  if (!own) return;
+  const int mt = p >> 6, ln = p & 63;
+  const int col = nt * 16 + (ln & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
     const int row = mt * 16 + 4 * (ln >> 4) + r;
-    const int col = nt * 16 + (ln & 15);
     if constexpr (EPI == EPI_ARGMAX) {
-      float lv = rbf(v[0]);
+      const float lv = rbf(v[0][r]);
       unsigned long long key = ((unsigned long long)float_key(lv) << 32) | (0xFFFFFFFFu - (uint32_t)col);
-      // max over the 16 columns held by lanes with the same (ln >> 4)
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) {
-        unsigned long long other = __shfl_xor(key, o, 16);
+        const unsigned long long other = __shfl_xor(key, o, 16);
         key = other > key ? other : key;
       }
       if (row < M) {
-        if ((ln & 15) == 0) partial[(int64_t)nt * M + row] = key;
+        if ((ln & 15) == 0) keys[(int64_t)nt * M + row] = key;
         if (C) C[(int64_t)row * ldc + col] = f2bf(lv);
       }
     } else if (row < M) {
       float o;
       if constexpr (EPI == EPI_NONE) {
-        o = v[0];
+        o = v[0][r];
       } else if constexpr (EPI == EPI_RESID) {
-        o = rbf(v[0]) + bf2f(R[(int64_t)row * ldr + col]);
+        o = rbf(v[0][r]) + bf2f(R[(int64_t)row * ldr + col]);
       } else {  // EPI_SILU
-        o = rbf(silu_f(rbf(v[0]))) * rbf(v[1]);
+        o = rbf(silu_f(rbf(v[0][r]))) * rbf(v[1][r]);
       }
       C[(int64_t)row * ldc + col] = f2bf(o);
     }
   }
 }
 
+// weight tiles per wave and round: ~16-32 loads (weights + activation fragments) in flight
+__host__ __device__ constexpr int decode_tw(int MT, int S) {
+  return S == 1 ? (MT == 1 ? 16 : (MT == 2 ? 8 : 4)) : (MT == 1 ? 8 : 4);
+}
+
+static int decode_ks(int KT, int MT, int S) {
+  const int tw = decode_tw(MT, S);
+  return (KT + 4 * tw - 1) / (4 * tw);
+}
+
+size_t gemm_decode_ws_bytes(int N, int K, int epi, int M) {
+  const int S = (epi == EPI_SILU) ? 2 : 1;
+  const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 48 ? 3 : 4));
+  const int KS = decode_ks(K / 32, MT, S);
+  return KS > 1 ? (size_t)(N / 16) * KS * S * MT * 1024 : 0;
+}
+
 template <int MT, int EPI>
-static void skinny_dispatch(const u16* A, int64_t lda, const u16* Wp, int KT, int n_tiles, u16* C,
-                            int64_t ldc, const u16* R, int64_t ldr, int M,
-                            unsigned long long* partial, hipStream_t s) {
-  constexpr int NW = 8;
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NW, EPI>), dim3(n_tiles), dim3(NW * 64), 0, s, A, lda,
-                     Wp, KT, n_tiles, C, ldc, R, ldr, M, partial);
+static void decode_dispatch(const u16* A, int64_t lda, const u16* Wp, int KT, int n_tiles, u16* C, int64_t ldc,
+                            const u16* R, int64_t ldr, int M, unsigned long long* keys, const GemmWs* ws,
+                            hipStream_t s) {
+  constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
+  constexpr int TW = decode_tw(MT, S);
+  // one round of 4*TW tiles per workgroup when the workspace can hold the KS partials
+  int KS = decode_ks(KT, MT, S);
+  constexpr size_t part_bytes = (size_t)S * MT * 64 * 16;
+  if (!ws || !ws->slab || (size_t)n_tiles * KS * part_bytes > ws->slab_bytes || n_tiles > ws->n_counters)
+    KS = 1;
+  float* slab = ws ? ws->slab : nullptr;
+  unsigned sb = ws ? (unsigned)(ws->slab_bytes < 0xFFFFFFF0ull ? ws->slab_bytes : 0xFFFFFFF0ull) : 0;
+  unsigned* cnt = ws ? ws->counters : nullptr;
+  dim3 grid(n_tiles * KS), block(256);
+  hipLaunchKernelGGL((gemm_decode_kernel<MT, S, TW, EPI>), grid, block, 0, s, A, lda, Wp, KT, n_tiles, KS, C, ldc, R,
+                     ldr, M, keys, slab, sb, cnt);
 }
 
 template <int EPI>
-static void skinny_mt(const u16* A, int64_t lda, const u16* Wp, int KT, int n_tiles, u16* C,
-                      int64_t ldc, const u16* R, int64_t ldr, int M, unsigned long long* partial,
+static void decode_mt(const u16* A, int64_t lda, const u16* Wp, int KT, int n_tiles, u16* C, int64_t ldc,
+                      const u16* R, int64_t ldr, int M, unsigned long long* keys, const GemmWs* ws,
                       hipStream_t s) {
   if (M <= 16)
-    skinny_dispatch<1, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, partial, s);
+    decode_dispatch<1, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, keys, ws, s);
   else if (M <= 32)
-    skinny_dispatch<2, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, partial, s);
+    decode_dispatch<2, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, keys, ws, s);
   else if (M <= 48)
-    skinny_dispatch<3, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, partial, s);
+    decode_dispatch<3, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, keys, ws, s);
   else
-    skinny_dispatch<4, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, partial, s);
+    decode_dispatch<4, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, keys, ws, s);
 }
 
 // ============================================================ tiled (prefill) kernel
@@ -278,8 +340,8 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(
 }
 
 // ============================================================ dispatch
-void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C,
-                 int64_t ldc, const u16* R, int64_t ldr, int epi, unsigned long long* partial,
+void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
+                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, const GemmWs* ws,
                  hipStream_t s) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
@@ -302,17 +364,17 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     }
     return;
   }
-  // skinny path, 64-row slabs (M > 64 only when the tiled shape constraints fail)
+  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail)
   for (int m0 = 0; m0 < M; m0 += 64) {
     const int mm = (M - m0) < 64 ? (M - m0) : 64;
     const u16* Am = A + (int64_t)m0 * lda;
     u16* Cm = C ? C + (int64_t)m0 * ldc : nullptr;
     const u16* Rm = R ? R + (int64_t)m0 * ldr : nullptr;
     switch (epi) {
-      case EPI_NONE: skinny_mt<EPI_NONE>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, partial, s); break;
-      case EPI_RESID: skinny_mt<EPI_RESID>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, partial, s); break;
-      case EPI_SILU: skinny_mt<EPI_SILU>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, partial, s); break;
-      default: skinny_mt<EPI_ARGMAX>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, partial, s); break;
+      case EPI_NONE: decode_mt<EPI_NONE>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, keys, ws, s); break;
+      case EPI_RESID: decode_mt<EPI_RESID>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, keys, ws, s); break;
+      case EPI_SILU: decode_mt<EPI_SILU>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, keys, ws, s); break;
+      default: decode_mt<EPI_ARGMAX>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, keys, ws, s); break;
     }
     if (epi == EPI_ARGMAX) break;  // argmax requires M <= 64 (checked by the caller)
   }

@@ -88,6 +88,7 @@ struct InferdSpan {
   float* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
   unsigned long long* argmax_partial = nullptr;
+  GemmWs gws = {nullptr, 0, nullptr, 0};
   int32_t* err = nullptr;
   std::vector<void*> allocs;
   // optional per-kernel-class timing with HIP events on the launch stream
@@ -134,6 +135,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   if (!cfg || !out) return fail(INFERD_ERR_ARG, "null argument");
   const InferdSpanConfig& c = *cfg;
   if (c.head_dim != HEAD_DIM) return fail(INFERD_ERR_ARG, "head_dim must be 128");
+  if ((int64_t)c.max_seqs * c.heads > 16384) return fail(INFERD_ERR_ARG, "max_seqs * heads must be <= 16384");
   if (c.kv_heads <= 0 || c.heads % c.kv_heads != 0 || c.heads / c.kv_heads > 16)
     return fail(INFERD_ERR_ARG, "heads must be a multiple of kv_heads with group size <= 16");
   if (c.hidden % 128 || c.intermediate % 64 || c.vocab % 16)
@@ -203,7 +205,32 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->last, (size_t)c.max_seqs * h * 2);
   s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
   SALLOC(s->attn_ws, s->attn_ws_bytes);
+  if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
+  {
+    // split-K workspace of the decode GEMMs (M <= 64), sized for the span's largest need
+    const int Md = c.max_tokens < 64 ? c.max_tokens : 64;
+    const int Mh = c.max_seqs < 64 ? c.max_seqs : 64;
+    size_t need = 0;
+    auto upd = [&](size_t b) { need = b > need ? b : need; };
+    upd(gemm_decode_ws_bytes(s->qkv_rows(), h, EPI_NONE, Md));
+    upd(gemm_decode_ws_bytes(h, H * HEAD_DIM, EPI_RESID, Md));
+    upd(gemm_decode_ws_bytes(I, h, EPI_SILU, Md));
+    upd(gemm_decode_ws_bytes(h, I, EPI_RESID, Md));
+    int max_nt = s->qkv_rows() / 16;
+    if (h / 16 > max_nt) max_nt = h / 16;
+    if (I / 16 > max_nt) max_nt = I / 16;
+    if (c.has_lm_head) {
+      upd(gemm_decode_ws_bytes(c.vocab, h, EPI_ARGMAX, Mh));
+      if (c.vocab / 16 > max_nt) max_nt = c.vocab / 16;
+    }
+    s->gws.n_counters = max_nt;
+    s->gws.slab_bytes = need;
+    SALLOC(s->gws.slab, s->gws.slab_bytes);
+    SALLOC(s->gws.counters, (size_t)max_nt * 4);
+    if (hipMemset(s->gws.counters, 0, (size_t)max_nt * 4) != hipSuccess)
+      return bail(fail(INFERD_ERR_HIP, "memset failed"));
+  }
   SALLOC(s->err, 256);
   if (hipMemset(s->err, 0, 4) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(INFERD_ERR_HIP, "init sync failed"));
@@ -373,7 +400,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_QKV, st);
-    launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st);
+    launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, &s->gws, st);
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_ROPE, st);
     launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
@@ -387,17 +414,17 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     s->prof_end(pe, st);
     // h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
     pe = s->prof_begin(PROF_O, st);
-    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);
+    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, &s->gws, st);
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_NORM, st);
     launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_GATEUP, st);
-    launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st);
+    launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, &s->gws, st);
     s->prof_end(pe, st);
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
     pe = s->prof_begin(PROF_DOWN, st);
-    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, st);
+    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, &s->gws, st);
     s->prof_end(pe, st);
     x = out;
     if (layer_out)
@@ -411,7 +438,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pe = s->prof_begin(PROF_LMHEAD, st);
     launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st);
     launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
-                s->argmax_partial, st);
+                s->argmax_partial, &s->gws, st);
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
     s->prof_end(pe, st);
   }
@@ -560,7 +587,17 @@ extern "C" int inferd_gemm(const void* a, const void* w, void* c, const void* r,
   if (!a || !w || !c || m <= 0 || n % 16 || k % 32) return fail(INFERD_ERR_ARG, "gemm needs n%16==0, k%32==0");
   if (epi < 0 || epi > 2) return fail(INFERD_ERR_ARG, "bad epilogue");
   if (epi == INFERD_EPI_RESID && !r) return fail(INFERD_ERR_ARG, "resid epilogue needs R");
-  launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr,
+  // process-wide split-K workspace of the single-op entry point (allocated once, outside
+  // any capture; the span owns its own)
+  static GemmWs ws = {nullptr, 0, nullptr, 0};
+  if (!ws.slab) {
+    ws.n_counters = 1 << 16;
+    ws.slab_bytes = (size_t)256 << 20;
+    HIP_TRY(hipMalloc((void**)&ws.slab, ws.slab_bytes));
+    HIP_TRY(hipMalloc((void**)&ws.counters, ws.n_counters * 4));
+    HIP_TRY(hipMemset(ws.counters, 0, ws.n_counters * 4));
+  }
+  launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr, &ws,
               (hipStream_t)stream);
   LAUNCH_CHECK();
   return INFERD_OK;

@@ -300,8 +300,20 @@ def gen_units():
     np.savez_compressed(os.path.join(OUT, "units.npz"), **res)
 
 
+def gen_codec():
+    """The reference's wire codec and mask builder on fixed inputs (partitioned_models.py:11-35)."""
+    import json
+    t = (torch.arange(24, dtype=torch.float32).reshape(1, 4, 6) - 7.5) / 3.0
+    meta = PM.tensor_to_base64(t)
+    mask = PM.build_decoder_attention_mask(torch.tensor([[1, 1, 1, 0, 1]]))
+    with open(os.path.join(OUT, "codec.json"), "w") as f:
+        json.dump({"input": t.reshape(-1).tolist(), "shape": list(t.shape), "meta": meta,
+                   "mask": mask.to(torch.int32).reshape(-1).tolist(), "mask_shape": list(mask.shape)}, f)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
+    gen_codec()
     gen_units()
     gen_tiny_petals()
     gen_server("tiny_server", "tiny", 0, 3, 1, 8, 4, ((torch.float32, "fp32"), (torch.bfloat16, "bf16")), 21)

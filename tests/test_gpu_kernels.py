@@ -120,10 +120,11 @@ def test_gemm_plain_and_resid(lib, M, N, K):
     assert (bf16_ulp_diff(c2.cpu(), ref2.cpu()) > 1).float().mean() < 1e-3
 
 
-@pytest.mark.parametrize("M", [1, 16, 64, 300])
-def test_gemm_swiglu(lib, M):
+@pytest.mark.parametrize("M,K", [(1, 1024), (16, 1024), (64, 1024), (300, 1024), (16, 4096), (40, 4096)])
+def test_gemm_swiglu(lib, M, K):
+    """Also covers the decode GEMM's split-K reduction (K = 4096 -> 4 slices at M <= 16)."""
     torch.manual_seed(M)
-    I, K = 512, 1024
+    I = 512
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     g = (torch.randn(I, K, device=DEV) * 0.03).to(torch.bfloat16)
     u = (torch.randn(I, K, device=DEV) * 0.03).to(torch.bfloat16)
@@ -225,7 +226,7 @@ def _attn_case(lib, H, KV, q_lens, past_lens, seed=0):
     q = torch.cat(Qs, 0).contiguous().to(DEV)
     out = torch.empty(q.shape[0], H * 128, dtype=torch.bfloat16, device=DEV)
     ws_bytes = L.inferd_attention_workspace_bytes(len(seqs), H, max(t + p for t, p in zip(q_lens, past_lens)))
-    ws = torch.empty(max(ws_bytes, 256), dtype=torch.uint8, device=DEV)
+    ws = torch.zeros(max(ws_bytes, 256), dtype=torch.uint8, device=DEV)
     kv_d = kv.to(DEV)
     lib.check(L.inferd_attention(q.data_ptr(), kv_d.data_ptr(), batch, H, KV, out.data_ptr(), ws.data_ptr(),
                                  ws_bytes, lib.stream_ptr()))

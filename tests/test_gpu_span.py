@@ -97,6 +97,48 @@ def test_q8b_layer_batched_cached_vs_golden():
         assert e < TOL_REL_EAGER
 
 
+def test_partitioned_qwen2_dict_protocol(tmp_path):
+    """The node-facing API end to end: stage files written by the offline splitter, two
+    PartitionedQwen2 stages chained through the reference's dict protocol (generated_ids ->
+    hidden_meta (bf16 wire codec) -> next_token_id), 8 greedy steps of full recompute as in
+    send_message.py:46-60, against the golden ids of the reference's own chain."""
+    from inferd_amd.partitioned_models import PartitionedQwen2
+    from inferd_amd.runtime import MODELS
+    from inferd_amd.split_model import split
+    g = load("tiny_petals.npz")
+    d = R.CONFIGS["tiny"]
+    cfg = {"model_name": "tiny", "parts_dir": str(tmp_path), "stages_count": 2,
+           "stages": [{"name": "node0", "stage": 0, "start_layer": 0, "end_layer": 1},
+                      {"name": "node1", "stage": 1, "start_layer": 2, "end_layer": 3}]}
+    glob = R.gen_global_weights(d, SEED)
+    attn = ("q_proj", "k_proj", "v_proj", "o_proj", "q_norm", "k_norm")
+
+    def get_layer(i):
+        return {("self_attn." if k in attn else "mlp." if k.endswith("_proj") else "") + k + ".weight": v
+                for k, v in R.gen_layer_weights(d, SEED, i).items()}
+    p0, p1 = split(cfg, MODELS["tiny"], get_layer, lambda n: glob[n])
+    n0 = PartitionedQwen2("tiny", 2, 0, p0)
+    n1 = PartitionedQwen2("tiny", 2, 1, p1)
+    ids = g["prompt"].tolist()
+    ref_ids = g["bf16_greedy_ids"].tolist()
+    b0 = R.RefSpan(d, SEED, 0, 1, True, False)
+    b1 = R.RefSpan(d, SEED, 2, 3, False, True)
+    for step in range(8):
+        o0 = n0.forward({"generated_ids": ids})
+        assert o0["hidden_meta"]["dtype"] == "bfloat16" and o0["generated_ids"] == ids
+        o1 = n1.forward(o0)
+        margin = R.top2_margin(b1.forward(b0.forward(torch.tensor([ids])))[0, -1])
+        if margin > MARGIN_FLOOR:
+            assert o1["next_token_id"] == ref_ids[step], step
+        assert o1["generated_ids"] == ids + [o1["next_token_id"]]
+        ids = ids + [ref_ids[step]]
+    # synthetic stage spec gives the same model without files
+    s0 = PartitionedQwen2("tiny", 2, 0, f"synthetic:{SEED}:tiny:0:1")
+    h_file = n0.forward({"generated_ids": ids})["hidden_meta"]
+    h_syn = s0.forward({"generated_ids": ids})["hidden_meta"]
+    assert h_file == h_syn
+
+
 def test_decode_graph_matches_eager():
     """A captured decode step (device-side position advance + whole span) replayed n times
     gives bit-identical ids/logit-argmax to n eager cached decode calls."""
