@@ -14,6 +14,11 @@
 //    partial write-through (sc1, 16 B per lane), takes a ticket on the tile's counter, and
 //    the last arriver sums the KS partials in slice order and runs the fused epilogue
 //    (cdna_hip_programming.md §5 "In-launch split-K reduction", sc1 form).
+//    Fused RMSNorm (Qwen3RMSNorm, qwen3_server_module.py:19-25): with `ss_in` the A operand
+//    is normalised on load, A' = bf16(w * bf16(x * rsqrt(sum(x^2)/K + eps))), from per-row
+//    partial sums of squares that the PRODUCER of x wrote (`ss_out` of an EPI_RESID GEMM:
+//    per 16-column tile, deterministic fixed-order sum in the consumer) -- so the two
+//    per-layer RMSNorm kernels disappear from the decode step.
 //  * gemm_tiled: M > 64 rows (prefill).  128x128x64 block tile, 4 waves (2x2, 64x64
 //    each), A and B staged through double-buffered LDS with global_load_lds (A
 //    XOR-swizzled on the source address, B already fragment-ordered), 32 MFMA per
@@ -26,29 +31,50 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g)); }
 
 // ============================================================ decode (M <= 64) kernel
-template <int MT, int S, int TW, int EPI>
-__global__ __launch_bounds__(256) void gemm_decode_kernel(
-    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles, int KS,
-    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    unsigned long long* __restrict__ keys, float* __restrict__ slab, unsigned slab_bytes,
-    unsigned* __restrict__ counters) {
+struct DecodeArgs {
+  const u16* A;
+  int64_t lda;
+  const u16* Wp;
+  int KT, n_tiles, KS, M;
+  u16* C;
+  int64_t ldc;
+  const u16* R;
+  int64_t ldr;
+  unsigned long long* keys;  // EPI_ARGMAX partial keys [n_tiles][M]
+  float* slab;               // split-K partials
+  unsigned slab_bytes;
+  unsigned* counters;
+  const float* ss_in;        // fused norm: [n_ss_in][64] partial sums of squares of A rows
+  int n_ss_in;
+  const u16* norm_w;         // fused norm weight [K]
+  float eps;
+  float* ss_out;             // EPI_RESID: [n_tiles][64] sums of squares of the bf16 outputs
+};
+
+template <int MT, int S, int TW, int EPI, bool NORM>
+__global__ __launch_bounds__(256) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[4][NV];
+  __shared__ float sm_ss[16][64];
+  __shared__ float sm_inv[64];
   __shared__ int sm_last;
+  const int KT = g.KT, KS = g.KS, M = g.M;
   const int nt = blockIdx.x / KS, ks = blockIdx.x - (blockIdx.x / KS) * KS;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // slice [k0, k1) of the K tiles; processed in rounds of 4*TW tiles (one round when the
   // dispatcher could choose KS = ceil(KT / (4*TW))), wave w taking TW consecutive tiles
   const int SL = (KT + KS - 1) / KS;
   const int k0 = ks * SL, k1 = min(KT, k0 + SL);
-  const bf16x8* w0 = (const bf16x8*)(Wp + (int64_t)nt * KT * 512) + lane;
-  const bf16x8* w1 = (const bf16x8*)(Wp + (int64_t)(nt + n_tiles) * KT * 512) + lane;
+  const bf16x8* w0 = (const bf16x8*)(g.Wp + (int64_t)nt * KT * 512) + lane;
+  const bf16x8* w1 = (const bf16x8*)(g.Wp + (int64_t)(nt + g.n_tiles) * KT * 512) + lane;
   const u16* a[MT];
+  int arow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int row = mt * 16 + (lane & 15);
     row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
-    a[mt] = A + (int64_t)row * lda + 8 * (lane >> 4);
+    arow[mt] = row;
+    a[mt] = g.A + (int64_t)row * g.lda + 8 * (lane >> 4);
   }
   const bf16x8 zero = as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   f32x4 acc[S][MT];
@@ -56,6 +82,7 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[s][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool inv_ready = false;
   for (int kr = k0 + wave * TW; kr < k1; kr += 4 * TW) {
     bf16x8 wv[S][TW];
     bf16x8 av[TW][MT];
@@ -72,12 +99,58 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) av[u][mt] = (kt < k1) ? *(const bf16x8*)(a[mt] + kt * 32) : zero;
     }
+    if constexpr (NORM) {
+      if (!inv_ready) {
+        // per-row 1/rms from the producer's partial sums (weight loads already in flight);
+        // rows r < 16*MT, partial groups gr of the n_ss_in tiles, fixed summation order
+        constexpr int RR = MT * 16, G = 256 / RR;
+        const int r = threadIdx.x % RR, gr = threadIdx.x / RR;
+        if (gr < G) {
+          float t = 0.f;
+          for (int i = gr; i < g.n_ss_in; i += G) t += g.ss_in[i * 64 + r];
+          sm_ss[gr][r] = t;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (threadIdx.x < RR) {
+          float t = 0.f;
+          for (int i = 0; i < G; ++i) t += sm_ss[i][threadIdx.x];
+          sm_inv[threadIdx.x] = 1.0f / sqrtf(t / (float)(KT * 32) + g.eps);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        inv_ready = true;
+      }
+      float inv[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) inv[mt] = sm_inv[arow[mt]];
+#pragma unroll
+      for (int u = 0; u < TW; ++u) {
+        const int kt = kr + u;
+        const u16x8 wn = (kt < k1) ? *(const u16x8*)(g.norm_w + kt * 32 + 8 * (lane >> 4)) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const u16x8 xv = __builtin_bit_cast(u16x8, av[u][mt]);
+          u16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(wn[j]) * rbf(bf2f(xv[j]) * inv[mt]));
+          av[u][mt] = as_bf16x8(o);
+        }
+      }
+    }
 #pragma unroll
     for (int u = 0; u < TW; ++u)
 #pragma unroll
       for (int s = 0; s < S; ++s)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[u][mt], wv[s][u], acc[s][mt]);
+  }
+  if constexpr (NORM) {
+    // waves without a round must still join the two barriers of the norm prologue
+    if (!inv_ready) {
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
+    }
   }
 #pragma unroll
   for (int s = 0; s < S; ++s)
@@ -96,7 +169,7 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(
     }
   }
   if (KS > 1) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, slab_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(g.slab, 0, g.slab_bytes, 0x00020000);
     if (own) {
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -107,12 +180,12 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(&counters[nt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned prev = __hip_atomic_fetch_add(&g.counters[nt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sm_last = prev == (unsigned)(KS - 1);
       if (sm_last) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&counters[nt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&g.counters[nt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     __syncthreads();
@@ -122,7 +195,7 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(
       for (int s = 0; s < S; ++s) {
         f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int k = 0; k < KS; ++k)
-          t += *(const f32x4*)(slab + ((((int64_t)nt * KS + k) * NV + s * MT * 64 + p) * 4));
+          t += *(const f32x4*)(g.slab + ((((int64_t)nt * KS + k) * NV + s * MT * 64 + p) * 4));
         v[s] = t;
       }
     }
@@ -142,19 +215,28 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(
         key = other > key ? other : key;
       }
       if (row < M) {
-        if ((ln & 15) == 0) keys[(int64_t)nt * M + row] = key;
-        if (C) C[(int64_t)row * ldc + col] = f2bf(lv);
+        if ((ln & 15) == 0) g.keys[(int64_t)nt * M + row] = key;
+        if (g.C) g.C[(int64_t)row * g.ldc + col] = f2bf(lv);
       }
-    } else if (row < M) {
+    } else {
       float o;
       if constexpr (EPI == EPI_NONE) {
         o = v[0][r];
       } else if constexpr (EPI == EPI_RESID) {
-        o = rbf(v[0][r]) + bf2f(R[(int64_t)row * ldr + col]);
+        o = rbf(v[0][r]) + bf2f(g.R[(int64_t)(row < M ? row : M - 1) * g.ldr + col]);
       } else {  // EPI_SILU
         o = rbf(silu_f(rbf(v[0][r]))) * rbf(v[1][r]);
       }
-      C[(int64_t)row * ldc + col] = f2bf(o);
+      const u16 ob = f2bf(o);
+      if (row < M) g.C[(int64_t)row * g.ldc + col] = ob;
+      if constexpr (EPI == EPI_RESID) {
+        if (g.ss_out) {  // this tile's share of the next RMSNorm's sum of squares
+          float sq = bf2f(ob) * bf2f(ob);
+#pragma unroll
+          for (int off = 8; off > 0; off >>= 1) sq += __shfl_xor(sq, off, 16);
+          if ((ln & 15) == 0 && row < M) g.ss_out[nt * 64 + row] = sq;
+        }
+      }
     }
   }
 }
@@ -176,37 +258,39 @@ size_t gemm_decode_ws_bytes(int N, int K, int epi, int M) {
   return KS > 1 ? (size_t)(N / 16) * KS * S * MT * 1024 : 0;
 }
 
-template <int MT, int EPI>
-static void decode_dispatch(const u16* A, int64_t lda, const u16* Wp, int KT, int n_tiles, u16* C, int64_t ldc,
-                            const u16* R, int64_t ldr, int M, unsigned long long* keys, const GemmWs* ws,
-                            hipStream_t s) {
+template <int MT, int EPI, bool NORM>
+static void decode_launch(DecodeArgs a, const GemmWs* ws, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   constexpr int TW = decode_tw(MT, S);
   // one round of 4*TW tiles per workgroup when the workspace can hold the KS partials
-  int KS = decode_ks(KT, MT, S);
+  a.KS = decode_ks(a.KT, MT, S);
   constexpr size_t part_bytes = (size_t)S * MT * 64 * 16;
-  if (!ws || !ws->slab || (size_t)n_tiles * KS * part_bytes > ws->slab_bytes || n_tiles > ws->n_counters)
-    KS = 1;
-  float* slab = ws ? ws->slab : nullptr;
-  unsigned sb = ws ? (unsigned)(ws->slab_bytes < 0xFFFFFFF0ull ? ws->slab_bytes : 0xFFFFFFF0ull) : 0;
-  unsigned* cnt = ws ? ws->counters : nullptr;
-  dim3 grid(n_tiles * KS), block(256);
-  hipLaunchKernelGGL((gemm_decode_kernel<MT, S, TW, EPI>), grid, block, 0, s, A, lda, Wp, KT, n_tiles, KS, C, ldc, R,
-                     ldr, M, keys, slab, sb, cnt);
+  if (!ws || !ws->slab || (size_t)a.n_tiles * a.KS * part_bytes > ws->slab_bytes || a.n_tiles > ws->n_counters)
+    a.KS = 1;
+  a.slab = ws ? ws->slab : nullptr;
+  a.slab_bytes = ws ? (unsigned)(ws->slab_bytes < 0xFFFFFFF0ull ? ws->slab_bytes : 0xFFFFFFF0ull) : 0;
+  a.counters = ws ? ws->counters : nullptr;
+  hipLaunchKernelGGL((gemm_decode_kernel<MT, S, TW, EPI, NORM>), dim3(a.n_tiles * a.KS), dim3(256), 0, s, a);
+}
+
+template <int EPI, bool NORM>
+static void decode_mt(const DecodeArgs& a, const GemmWs* ws, hipStream_t s) {
+  if (a.M <= 16)
+    decode_launch<1, EPI, NORM>(a, ws, s);
+  else if (a.M <= 32)
+    decode_launch<2, EPI, NORM>(a, ws, s);
+  else if (a.M <= 48)
+    decode_launch<3, EPI, NORM>(a, ws, s);
+  else
+    decode_launch<4, EPI, NORM>(a, ws, s);
 }
 
 template <int EPI>
-static void decode_mt(const u16* A, int64_t lda, const u16* Wp, int KT, int n_tiles, u16* C, int64_t ldc,
-                      const u16* R, int64_t ldr, int M, unsigned long long* keys, const GemmWs* ws,
-                      hipStream_t s) {
-  if (M <= 16)
-    decode_dispatch<1, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, keys, ws, s);
-  else if (M <= 32)
-    decode_dispatch<2, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, keys, ws, s);
-  else if (M <= 48)
-    decode_dispatch<3, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, keys, ws, s);
+static void decode_norm(const DecodeArgs& a, const GemmWs* ws, hipStream_t s) {
+  if (a.ss_in)
+    decode_mt<EPI, true>(a, ws, s);
   else
-    decode_dispatch<4, EPI>(A, lda, Wp, KT, n_tiles, C, ldc, R, ldr, M, keys, ws, s);
+    decode_mt<EPI, false>(a, ws, s);
 }
 
 // ============================================================ tiled (prefill) kernel
@@ -340,14 +424,17 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(
 }
 
 // ============================================================ dispatch
+bool gemm_uses_tiled(int M, int N, int K, int epi) {
+  return (M > 64) && (K % TBK == 0) && ((epi == EPI_SILU) ? (N % 64 == 0) : (N % TBN == 0)) &&
+         epi != EPI_ARGMAX;
+}
+
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, const GemmWs* ws,
-                 hipStream_t s) {
+                 hipStream_t s, const GemmNorm* norm) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
-  const bool tiled_ok = (M > 64) && (K % TBK == 0) &&
-                        ((epi == EPI_SILU) ? (N % 64 == 0) : (N % TBN == 0)) && epi != EPI_ARGMAX;
-  if (tiled_ok) {
+  if (gemm_uses_tiled(M, N, K, epi)) {
     const int ncols = (epi == EPI_SILU) ? 64 : 128;
     dim3 g(N / ncols, (M + TBM - 1) / TBM);
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
@@ -364,17 +451,33 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     }
     return;
   }
-  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail)
+  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail; the
+  // fused norm and the sum-of-squares output are only used with M <= 64)
   for (int m0 = 0; m0 < M; m0 += 64) {
-    const int mm = (M - m0) < 64 ? (M - m0) : 64;
-    const u16* Am = A + (int64_t)m0 * lda;
-    u16* Cm = C ? C + (int64_t)m0 * ldc : nullptr;
-    const u16* Rm = R ? R + (int64_t)m0 * ldr : nullptr;
+    DecodeArgs a = {};
+    a.M = (M - m0) < 64 ? (M - m0) : 64;
+    a.A = A + (int64_t)m0 * lda;
+    a.lda = lda;
+    a.Wp = Wp;
+    a.KT = KT;
+    a.n_tiles = n_tiles;
+    a.C = C ? C + (int64_t)m0 * ldc : nullptr;
+    a.ldc = ldc;
+    a.R = R ? R + (int64_t)m0 * ldr : nullptr;
+    a.ldr = ldr;
+    a.keys = keys;
+    if (norm && M <= 64) {
+      a.ss_in = norm->ss_in;
+      a.n_ss_in = norm->n_ss_in;
+      a.norm_w = norm->w;
+      a.eps = norm->eps;
+      a.ss_out = norm->ss_out;
+    }
     switch (epi) {
-      case EPI_NONE: decode_mt<EPI_NONE>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, keys, ws, s); break;
-      case EPI_RESID: decode_mt<EPI_RESID>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, keys, ws, s); break;
-      case EPI_SILU: decode_mt<EPI_SILU>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, keys, ws, s); break;
-      default: decode_mt<EPI_ARGMAX>(Am, lda, Wp, KT, n_tiles, Cm, ldc, Rm, ldr, mm, keys, ws, s); break;
+      case EPI_NONE: decode_norm<EPI_NONE>(a, ws, s); break;
+      case EPI_RESID: decode_norm<EPI_RESID>(a, ws, s); break;
+      case EPI_SILU: decode_norm<EPI_SILU>(a, ws, s); break;
+      default: decode_norm<EPI_ARGMAX>(a, ws, s); break;
     }
     if (epi == EPI_ARGMAX) break;  // argmax requires M <= 64 (checked by the caller)
   }

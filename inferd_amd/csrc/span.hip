@@ -89,6 +89,8 @@ struct InferdSpan {
   size_t attn_ws_bytes = 0;
   unsigned long long* argmax_partial = nullptr;
   GemmWs gws = {nullptr, 0, nullptr, 0};
+  float* ss_a = nullptr;  // fused-norm row statistics: [hidden/16][64] partial sums of squares
+  float* ss_b = nullptr;
   int32_t* err = nullptr;
   std::vector<void*> allocs;
   // optional per-kernel-class timing with HIP events on the launch stream
@@ -207,6 +209,8 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
+  SALLOC(s->ss_a, (size_t)(h / 16) * 64 * 4);
+  SALLOC(s->ss_b, (size_t)(h / 16) * 64 * 4);
   {
     // split-K workspace of the decode GEMMs (M <= 64), sized for the span's largest need
     const int Md = c.max_tokens < 64 ? c.max_tokens : 64;
@@ -392,15 +396,33 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   if (c.n_layers == 0 && x_out && x != x_out)
     HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
   const AttnBatch ab = to_attn(b);
-  long pe;
+  // Decode-sized batches (M <= 64, the decode GEMM path) fold both RMSNorms into the GEMMs:
+  // the residual-producing GEMMs emit per-tile sums of squares (ss_b after o_proj, ss_a
+  // after down_proj) that the next qkv / gate-up GEMM consumes while loading its A operand;
+  // the span input gets its row statistics from one row_ss launch.
+  const bool fuse = M <= 64;
+  int n_ss_a = 1;
+  long pe = -1;
+  if (fuse && c.n_layers > 0) {
+    pe = s->prof_begin(PROF_NORM, st);
+    launch_row_ss(x, h, M, h, s->ss_a, st);
+    s->prof_end(pe, st);
+  }
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
     u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
-    pe = s->prof_begin(PROF_NORM, st);
-    launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
-    s->prof_end(pe, st);
+    if (!fuse) {
+      pe = s->prof_begin(PROF_NORM, st);
+      launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
+      s->prof_end(pe, st);
+    }
     pe = s->prof_begin(PROF_QKV, st);
-    launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, &s->gws, st);
+    if (fuse) {
+      const GemmNorm nq = {s->ss_a, n_ss_a, W.in_ln, c.rms_eps, nullptr};
+      launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, &s->gws, st, &nq);
+    } else {
+      launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, &s->gws, st);
+    }
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_ROPE, st);
     launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
@@ -414,18 +436,25 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     s->prof_end(pe, st);
     // h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
     pe = s->prof_begin(PROF_O, st);
-    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, &s->gws, st);
-    s->prof_end(pe, st);
-    pe = s->prof_begin(PROF_NORM, st);
-    launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
+    const GemmNorm no = {nullptr, 0, nullptr, 0.f, s->ss_b};
+    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, &s->gws, st,
+                fuse ? &no : nullptr);
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_GATEUP, st);
-    launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, &s->gws, st);
+    if (fuse) {
+      const GemmNorm ng = {s->ss_b, h / 16, W.post_ln, c.rms_eps, nullptr};
+      launch_gemm(s->h, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, &s->gws, st, &ng);
+    } else {
+      launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
+      launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, &s->gws, st);
+    }
     s->prof_end(pe, st);
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
     pe = s->prof_begin(PROF_DOWN, st);
-    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, &s->gws, st);
+    const GemmNorm nd = {nullptr, 0, nullptr, 0.f, s->ss_a};
+    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, &s->gws, st, fuse ? &nd : nullptr);
     s->prof_end(pe, st);
+    n_ss_a = h / 16;
     x = out;
     if (layer_out)
       HIP_TRY(hipMemcpyAsync((u16*)layer_out + (size_t)l * M * h, x, (size_t)M * h * 2,

@@ -1,0 +1,85 @@
+"""Drop-in for `models/qwen3/server/qwen3_server_module.py::Qwen3Server` on the gfx950 engine.
+
+Same constructor `Qwen3Server(start_layer, end_layer)` and the same
+`send(session_id, hidden_states, attention_mask, cache_position, position_embeddings)`
+(qwen3_server_module.py:209-255).  The per-session `DynamicCache`
+(`session_caches = defaultdict(DynamicCache)`, :220) becomes the span's paged KV pool:
+prefill appends T tokens, each decode call appends one, positions continue from the
+cached length (client.py:244-266).
+
+Arguments the GPU path derives itself:
+  * attention_mask -- the client's additive causal mask (client.py:221-224 for prefill,
+    the all-zero (1,1,1,1) mask for decode, :249-250); causality over the cached prefix is
+    implicit in the attention kernels;
+  * position_embeddings -- (cos, sin) of the HF default rope at cache_position
+    (client.py:56-71); the engine keeps the same table (bf16) on the device.
+`cache_position` must continue the session's cached length; anything else raises
+(the reference would silently concatenate onto the cache).
+
+Unlike the reference, sessions can be released (`release(session_id)`), and
+`max_sessions` evicts the least recently used one when the pool would overflow.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+
+from .runtime import MODELS, ModelDims, SpanRuntime
+
+
+class Qwen3Server:
+    def __init__(self, start_layer: int, end_layer: int, *, model: str | ModelDims = "qwen3-0.6b",
+                 weights: str = "synthetic:1234", kv_pages: int = 1024, max_tokens: int = 8192,
+                 max_sessions: int | None = None, device="cuda"):
+        dims = MODELS[model] if isinstance(model, str) else model
+        self.dims = dims
+        self.start_layer, self.end_layer = start_layer, end_layer
+        self.device = torch.device(device)
+        self.span = SpanRuntime(dims, start_layer, end_layer - start_layer + 1, has_embed=False,
+                                has_lm_head=False, kv_pages=kv_pages, max_tokens=max_tokens, max_seqs=64,
+                                device=self.device)
+        self.max_sessions = max_sessions
+        self._lru = OrderedDict()
+        if weights.startswith("synthetic:"):
+            self.span.init_synthetic(int(weights.split(":")[1]))
+        else:
+            self.load_layer_files(weights)
+
+    def load_layer_files(self, pattern: str):
+        """Per-layer state dicts `layer_XX.pt` (qwen3_server_module.py:227-235), loaded with
+        weights_only=True; `pattern` contains `{idx:02d}`."""
+        for j, i in enumerate(range(self.start_layer, self.end_layer + 1)):
+            sd = torch.load(pattern.format(idx=i), map_location="cpu", weights_only=True)
+            self.span.load_layer_state_dict(j, sd)
+
+    @property
+    def session_caches(self):
+        return self.span.sessions
+
+    def release(self, session_id):
+        for key in [k for k in self.span.sessions
+                    if k == session_id or (isinstance(k, tuple) and len(k) == 2 and k[0] == session_id)]:
+            self.span.release(key)
+        self._lru.pop(session_id, None)
+
+    def send(self, session_id, hidden_states, attention_mask=None, cache_position=None,
+             position_embeddings=None, input_start_layer=None, input_end_layer=None):
+        """qwen3_server_module.py:237-255: hidden (B,T,h) -> hidden (B,T,h) through the span,
+        appending T tokens to each of the B rows' caches of `session_id`."""
+        B, T, h = hidden_states.shape
+        sids = [session_id] if B == 1 else [(session_id, b) for b in range(B)]
+        st = self.span.sessions.get(sids[0])
+        past = 0 if st is None else st.length
+        if cache_position is not None:
+            cp = torch.as_tensor(cache_position).reshape(-1).tolist()
+            if cp != list(range(past, past + T)):
+                raise ValueError(f"cache_position {cp[:3]}... does not continue session {session_id!r} "
+                                 f"(cached length {past})")
+        if self.max_sessions is not None and session_id not in self._lru and len(self._lru) >= self.max_sessions:
+            old, _ = self._lru.popitem(last=False)
+            self.release(old)
+        self._lru[session_id] = True
+        self._lru.move_to_end(session_id)
+        out = self.span.forward([(sid, T) for sid in sids], x=hidden_states.reshape(B * T, h))
+        return out["hidden"].reshape(B, T, h)
