@@ -53,7 +53,61 @@ def parse():
     p.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing pass")
     p.add_argument("--profile-steps", type=int, default=8, help="eager event-instrumented decode steps")
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
+    p.add_argument("--mode", choices=("decode", "prefill"), default="decode",
+                   help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline)")
+    p.add_argument("--prefill-layers", type=int, default=8)
+    p.add_argument("--prefill-batch", type=int, default=1)
+    p.add_argument("--prefill-len", type=int, default=8192)
     return p.parse_args()
+
+
+def prefill_flops(d, n_layers: int, B: int, T: int) -> float:
+    """Algorithmic flops of a span prefill: 2*params*tokens for the projections plus causal
+    attention 2*2*H*d*T(T+1)/2 per sequence and layer."""
+    h, I, H, KV, hd = d.hidden, d.intermediate, d.heads, d.kv_heads, d.head_dim
+    lin = h * (H + 2 * KV) * hd + H * hd * h + 3 * h * I
+    return n_layers * B * (2.0 * lin * T + 4.0 * H * hd * T * (T + 1) / 2)
+
+
+def run_prefill(args):
+    """Config 5: one pipeline stage of Qwen3-32B (8 of 64 layers) prefilling B x 8k tokens.
+    Per-GPU work of the 8-stage pipeline; the hand-off is one 8k x 5120 bf16 tensor."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["qwen3-32b" if args.model == "qwen3-8b" else args.model]
+    B, T, L = args.prefill_batch, args.prefill_len, args.prefill_layers
+    dev = torch.device("cuda", 0)
+    span = SpanRuntime(d, 8, L, has_embed=False, has_lm_head=False, kv_pages=B * (T // 64 + 2) + 4,
+                       max_tokens=B * T, max_seqs=max(B, 1), max_positions=T + 64, device=dev)
+    span.init_synthetic(args.seed)
+    x = (torch.randn(B * T, d.hidden, device=dev) * 0.5).to(torch.bfloat16)
+    times = []
+    for it in range(args.warmup + args.steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        span.forward([(None, T)] * B, x=x, want_hidden=True)
+        torch.cuda.synchronize()
+        if it >= args.warmup:
+            times.append(time.perf_counter() - t0)
+    t = sorted(times)[len(times) // 2]
+    fl = prefill_flops(d, L, B, T)
+    span.profile_start(1 << 12)
+    span.forward([(None, T)] * B, x=x, want_hidden=True)
+    torch.cuda.synchronize()
+    prof = span.profile_stop()
+    kernels = {k: {"launches": n, "avg_ms": round(ms / max(n, 1), 3)} for k, (ms, n) in prof.items() if n}
+    tf = fl / t / 1e12
+    print(json.dumps({
+        "metric": "prefill tokens/sec, Qwen3-32B 8-layer span (one of 8 pipeline stages)",
+        "value": round(B * T / t, 1), "unit": "tokens/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic hidden states + counter-generated synthetic weights",
+        "config": {"workload": f"qwen3-32b layers 8-{8 + L - 1}, prefill {B} x {T} tokens",
+                   "global_batch": B, "seq_len": T, "parallelism": "pp-stage"},
+        "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "alg_flops_per_step": fl},
+        "kernels": kernels}), flush=True)
 
 
 def even_split(n_layers: int, n: int):
@@ -132,6 +186,8 @@ def cpu_baseline(d_name: str, B: int, ctx: int, seed: int, n_layers_sample: int,
 # ------------------------------------------------------------------ main
 def main():
     args = parse()
+    if args.mode == "prefill":
+        return run_prefill(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

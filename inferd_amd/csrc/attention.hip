@@ -253,58 +253,157 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 }
 
 // ------------------------------------------------------------------ prefill (causal)
-// grid (ceil(max_q_len/64), H, B), 4 waves; wave w owns query rows [64*bx + 16*w, +16)
-// of one head; walks every page up to the block's largest position.
-__global__ __launch_bounds__(256) void attn_prefill_kernel(const u16* __restrict__ q,
+// grid (ceil(max_q_len/128), H, B), 4 waves.  The workgroup owns 128 query rows of one head;
+// wave w owns rows [32w, 32w+32) as two 16-row MFMA column blocks.  Every K/V page (K 16 KiB
+// + V 16 KiB of this kv head) is staged ONCE per workgroup into double-buffered LDS with
+// global_load_lds_dwordx4 (32 x 1 KiB pieces, 8 per wave) while the previous page is being
+// consumed; the page layout is already fragment-ordered, so every fragment read is
+// lds[tile * 1 KiB + lane * 16] (contiguous, bank-conflict free), and each K/V fragment feeds
+// the MFMAs of both column blocks.  Waves whose rows all precede a page skip its compute but
+// keep the barriers.
+__device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, const bf16x8 (&qf)[2][4],
+                                                 int page_tok0, const int (&lim)[2], float scale_log2,
+                                                 float (&m_i)[2], float (&l_i)[2], f32x4 (&o)[2][8], int lane) {
+  f32x4 sc[2][4];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb) sc[nb][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 kf = *(const bf16x8*)(lds + (tb * 4 + ks) * 1024 + lane * 16);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) sc[nb][tb] = mfma16(kf, qf[nb][ks], sc[nb][tb]);
+    }
+  bf16x8 pf[2][2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    float pmax = -INFINITY;
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
+        const float s = (t <= lim[nb]) ? sc[nb][tb][r] * scale_log2 : -INFINITY;
+        sc[nb][tb][r] = s;
+        pmax = fmaxf(pmax, s);
+      }
+    pmax = fmaxf(pmax, __shfl_xor(pmax, 16));
+    pmax = fmaxf(pmax, __shfl_xor(pmax, 32));
+    const float m_new = fmaxf(m_i[nb], pmax);
+    const float alpha = exp2f(m_i[nb] - m_new);
+    float psum = 0.f;
+#pragma unroll
+    for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(sc[nb][tb][r] - m_new);
+        sc[nb][tb][r] = p;
+        psum += p;
+      }
+    psum += __shfl_xor(psum, 16);
+    psum += __shfl_xor(psum, 32);
+    l_i[nb] = l_i[nb] * alpha + psum;
+    m_i[nb] = m_new;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[nb][kt][j] = (__bf16)sc[nb][2 * kt][j];
+        pf[nb][kt][4 + j] = (__bf16)sc[nb][2 * kt + 1][j];
+      }
+  }
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      const bf16x8 vf = *(const bf16x8*)(lds + 16384 + (kt * 8 + db) * 1024 + lane * 16);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) o[nb][db] = mfma16(vf, pf[nb][kt], o[nb][db]);
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restrict__ q,
                                                            const u16* __restrict__ kv,
                                                            AttnBatch b, int H, int KV,
                                                            float scale_log2,
                                                            u16* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 32768];
   const int bseq = blockIdx.z, h = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_rep = H / KV, g = h / n_rep;
   const int t0 = b.seq_start[bseq];
   const int T = b.seq_start[bseq + 1] - t0;
-  const int r0 = blockIdx.x * 64 + wave * 16;
-  if (r0 >= T) return;  // no barriers in this kernel
-  const int row = r0 + (lane & 15);
-  const bool valid = row < T;
-  const int tokrow = t0 + (valid ? row : T - 1);
-  const int qpos = b.positions[tokrow];
-  int maxpos = qpos;
+  const int qb0 = blockIdx.x * 128;
+  if (qb0 >= T) return;  // uniform over the workgroup
+  bf16x8 qf[2][4];
+  int lim[2], tokrow[2];
+  bool valid[2];
 #pragma unroll
-  for (int o = 8; o > 0; o >>= 1) maxpos = max(maxpos, __shfl_xor(maxpos, o, 16));
-  bf16x8 qf[4];
-  const u16* qp = q + ((int64_t)tokrow * H + h) * HEAD_DIM + 8 * (lane >> 4);
+  for (int nb = 0; nb < 2; ++nb) {
+    const int row = qb0 + wave * 32 + nb * 16 + (lane & 15);
+    valid[nb] = row < T;
+    tokrow[nb] = t0 + (valid[nb] ? row : T - 1);
+    lim[nb] = b.positions[tokrow[nb]];
+    const u16* qp = q + ((int64_t)tokrow[nb] * H + h) * HEAD_DIM + 8 * (lane >> 4);
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const bf16x8*)(qp + ks * 32);
-  float m_i = -INFINITY, l_i = 0.f;
-  f32x4 o[8];
-#pragma unroll
-  for (int db = 0; db < 8; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
+  }
+  // pages: up to the workgroup's last row; a wave computes up to its own last row
+  const int wg_last = b.positions[t0 + min(qb0 + 127, T - 1)];
+  const int wave_first_row = qb0 + wave * 32;
+  const int wave_last = wave_first_row < T ? b.positions[t0 + min(wave_first_row + 31, T - 1)] : -1;
+  const int n_pages = wg_last / KV_PAGE + 1;
   const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
-  const int n_pages = maxpos / KV_PAGE + 1;
-  for (int pi = 0; pi < n_pages; ++pi) {
+  auto stage = [&](int buf, int pi) {
     const int phys = bt[pi];
     const u16* kblk = kv + ((int64_t)(phys * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
     const u16* vblk = kv + ((int64_t)(phys * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
-    attend_page(kblk, vblk, qf, pi * KV_PAGE, qpos, scale_log2, m_i, l_i, o, lane);
+    char* base = lds + buf * 32768;
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc) {
+      const int piece = wave * 8 + pc;  // 0..15 K tiles, 16..31 V tiles
+      const u16* src = (piece < 16 ? kblk + piece * 512 : vblk + (piece - 16) * 512) + lane * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + piece * 1024), 16, 0, 0);
+    }
+  };
+  float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
+  f32x4 o[2][8];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+    for (int db = 0; db < 8; ++db) o[nb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  stage(0, 0);
+  __syncthreads();
+  for (int pi = 0; pi < n_pages; ++pi) {
+    const int cur = pi & 1;
+    if (pi + 1 < n_pages) stage(cur ^ 1, pi + 1);
+    if (pi * KV_PAGE <= wave_last)
+      prefill_page_lds(lds + cur * 32768, qf, pi * KV_PAGE, lim, scale_log2, m_i, l_i, o, lane);
+    __syncthreads();  // next page landed (vmcnt(0)) and everyone is done with this buffer
   }
-  if (!valid) return;
-  const float inv = 1.0f / l_i;
-  u16* op = out + (int64_t)tokrow * H * HEAD_DIM + h * HEAD_DIM;
 #pragma unroll
-  for (int db = 0; db < 8; ++db) {
-    u16x4 v;
+  for (int nb = 0; nb < 2; ++nb) {
+    if (!valid[nb]) continue;
+    const float inv = 1.0f / l_i[nb];
+    u16* op = out + (int64_t)tokrow[nb] * H * HEAD_DIM + h * HEAD_DIM;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = f2bf(o[db][r] * inv);
-    *(u16x4*)(op + db * 16 + 4 * (lane >> 4)) = v;
+    for (int db = 0; db < 8; ++db) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[nb][db][r] * inv);
+      *(u16x4*)(op + db * 16 + 4 * (lane >> 4)) = v;
+    }
   }
 }
 
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
                          float scale, u16* out, hipStream_t s) {
-  dim3 g((b.max_q_len + 63) / 64, H, b.B);
+  dim3 g((b.max_q_len + 127) / 128, H, b.B);
   hipLaunchKernelGGL(attn_prefill_kernel, g, dim3(256), 0, s, q, kv_layer, b, H, KV,
                      scale * LOG2E, out);
 }

@@ -23,6 +23,8 @@
 //    each), A and B staged through double-buffered LDS with global_load_lds (A
 //    XOR-swizzled on the source address, B already fragment-ordered), 32 MFMA per
 //    wave per K-step.
+#include <stdlib.h>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -423,6 +425,127 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(
   }
 }
 
+// ============================================================ 256x256 tiled (large prefill)
+// 256x256x64 block tile, 8 waves as 2 (M) x 4 (N), each wave 128x64 = 8x4 MFMA tiles
+// (128 fp32 accumulator registers).  Per K-step the workgroup stages A (256 rows x 64 k,
+// 32 KiB, source-swizzled) and B (16 n-tiles x 2 k-tiles = 32 packed 1 KiB tiles) into one
+// of two 64 KiB LDS buffers with global_load_lds_dwordx4 (8 pieces per wave), overlapping
+// the next step's transfer with this step's 64 MFMAs per wave.  EPI_SILU: the B tile holds
+// 128 gate + 128 up columns of the same 128 outputs.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_tiled256_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 65536];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int m0 = blockIdx.y * 256;
+  const int ncols = (EPI == EPI_SILU) ? 128 : 256;
+  const int n0 = blockIdx.x * ncols;
+  const int nsteps = KT / 2;
+  // A pieces q = 0..31: rows 8q..8q+7; B pieces q = 0..31: local n-tile q/2, k-tile q%2
+  const u16* a_src[4];
+  const u16* b_src[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int q = wave * 4 + p;
+    const int r = 8 * q + (lane >> 3);
+    int grow = m0 + r;
+    grow = grow < M ? grow : M - 1;
+    const int chunk = (lane & 7) ^ ((r >> 1) & 7);
+    a_src[p] = A + (int64_t)grow * lda + chunk * 8;
+    const int j = q >> 1, kk = q & 1;
+    int gnt;
+    if (EPI == EPI_SILU)
+      gnt = (j < 8) ? (n0 / 16 + j) : (n_tiles_w / 2 + n0 / 16 + (j - 8));
+    else
+      gnt = n0 / 16 + j;
+    b_src[p] = Wp + ((int64_t)gnt * KT + kk) * 512 + lane * 8;
+  }
+  auto stage = [&](int buf, int step) {
+    char* base = lds + buf * 65536;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[p] + step * 64), (void*)(base + (wave * 4 + p) * 1024),
+                                       16, 0, 0);
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[p] + (int64_t)step * 1024),
+                                       (void*)(base + 32768 + (wave * 4 + p) * 1024), 16, 0, 0);
+  };
+  // local n-tiles of this wave (4 x 16 columns)
+  int bj[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (EPI == EPI_SILU)
+      bj[t] = (t < 2) ? (wc * 2 + t) : (8 + wc * 2 + (t - 2));
+    else
+      bj[t] = wc * 4 + t;
+  }
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  stage(0, 0);
+  __syncthreads();
+  for (int t = 0; t < nsteps; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nsteps) stage(cur ^ 1, t + 1);
+    const char* base = lds + cur * 65536;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) bfr[nt] = *(const bf16x8*)(base + 32768 + (bj[nt] * 2 + kk) * 1024 + lane * 16);
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const int r = wr * 128 + mt * 16 + (lane & 15);
+        const int c = kk * 4 + (lane >> 4);
+        const bf16x8 af = *(const bf16x8*)(base + r * 128 + 16 * (c ^ ((r >> 1) & 7)));
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16(af, bfr[nt], acc[mt][nt]);
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wr * 128 + mt * 16 + 4 * (lane >> 4) + r;
+      if (row >= M) continue;
+      if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int col = n0 + wc * 32 + nt * 16 + (lane & 15);
+          const float gg = rbf(acc[mt][nt][r]);
+          const float uu = rbf(acc[mt][nt + 2][r]);
+          C[(int64_t)row * ldc + col] = f2bf(rbf(silu_f(gg)) * uu);
+        }
+      } else {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
+          float o = acc[mt][nt][r];
+          if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(R[(int64_t)row * ldr + col]);
+          C[(int64_t)row * ldc + col] = f2bf(o);
+        }
+      }
+    }
+  }
+}
+
+static bool use_tiled256(int M, int N, int epi) {
+  static int env = -1;
+  if (env < 0) {
+    const char* e = getenv("INFERD_GEMM_TILE");
+    env = e ? atoi(e) : 256;
+  }
+  if (env != 256 || M < 512) return false;
+  return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
+}
+
 // ============================================================ dispatch
 bool gemm_uses_tiled(int M, int N, int K, int epi) {
   return (M > 64) && (K % TBK == 0) && ((epi == EPI_SILU) ? (N % 64 == 0) : (N % TBN == 0)) &&
@@ -434,6 +557,23 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
                  hipStream_t s, const GemmNorm* norm) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
+  if (gemm_uses_tiled(M, N, K, epi) && use_tiled256(M, N, epi)) {
+    const int ncols = (epi == EPI_SILU) ? 128 : 256;
+    dim3 g(N / ncols, (M + 255) / 256);
+    const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
+    switch (epi) {
+      case EPI_NONE:
+        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_NONE>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        break;
+      case EPI_RESID:
+        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_RESID>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        break;
+      default:
+        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_SILU>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        break;
+    }
+    return;
+  }
   if (gemm_uses_tiled(M, N, K, epi)) {
     const int ncols = (epi == EPI_SILU) ? 64 : 128;
     dim3 g(N / ncols, (M + TBM - 1) / TBM);

@@ -120,7 +120,8 @@ def test_gemm_plain_and_resid(lib, M, N, K):
     assert (bf16_ulp_diff(c2.cpu(), ref2.cpu()) > 1).float().mean() < 1e-3
 
 
-@pytest.mark.parametrize("M,K", [(1, 1024), (16, 1024), (64, 1024), (300, 1024), (16, 4096), (40, 4096)])
+@pytest.mark.parametrize("M,K", [(1, 1024), (16, 1024), (64, 1024), (300, 1024), (16, 4096), (40, 4096),
+                                 (600, 1024)])
 def test_gemm_swiglu(lib, M, K):
     """Also covers the decode GEMM's split-K reduction (K = 4096 -> 4 slices at M <= 16)."""
     torch.manual_seed(M)
