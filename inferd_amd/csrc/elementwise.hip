@@ -146,29 +146,6 @@ void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row
     hipLaunchKernelGGL(rmsnorm_kernel<8>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps);
 }
 
-// per-row sum of squares (fp32) of bf16 rows: the input statistics of a span's first fused
-// RMSNorm (later norms get theirs from the producing GEMM's epilogue)
-__global__ __launch_bounds__(256) void row_ss_kernel(const u16* __restrict__ x, int64_t ldx, int N,
-                                                     float* __restrict__ ss) {
-  __shared__ float red[4];
-  const u16* xr = x + (int64_t)blockIdx.x * ldx;
-  float t = 0.f;
-  for (int c = threadIdx.x; c < N / 8; c += 256) {
-    u16x8 p = *(const u16x8*)(xr + c * 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t += bf2f(p[j]) * bf2f(p[j]);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) ss[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
-}
-
-void launch_row_ss(const u16* x, int64_t ldx, int M, int N, float* ss, hipStream_t s) {
-  hipLaunchKernelGGL(row_ss_kernel, dim3(M), dim3(256), 0, s, x, ldx, N, ss);
-}
-
 // ------------------------------------------------------------------ rope table
 // cos/sin[pos][i] for i < 64, HF default rope: freq = pos * inv_freq[i] in fp32
 // (client.py:56-71); stored as bf16 exactly like `cos.to(dtype=x.dtype)`.

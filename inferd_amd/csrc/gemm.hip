@@ -4,31 +4,26 @@
 // (models/qwen3/server/qwen3_server_module.py:103-120, :33-40) and LastStage.lm_head
 // (petals/partitioned_models.py:96) -- bf16 inputs, fp32 accumulate, one output rounding.
 //
-// Two kernels, both on v_mfma_f32_16x16x32_bf16 with weights in the fragment-packed
-// layout of common.h:
-//  * gemm_decode: M <= 64 rows.  HBM-bound weight stream.  Workgroup = 4 waves = one
-//    16-column output tile x one K slice of 4*TW k-tiles; every wave issues ALL of its
-//    TW weight-tile loads (1 KiB dwordx4 each) and activation fragments up front, then
-//    its MFMAs; the 4 waves reduce through LDS.  K slices (KS per tile) spread the stream
-//    over >= ~2 workgroups per CU; slices combine deterministically: each stores its fp32
-//    partial write-through (sc1, 16 B per lane), takes a ticket on the tile's counter, and
-//    the last arriver sums the KS partials in slice order and runs the fused epilogue
-//    (cdna_hip_programming.md §5 "In-launch split-K reduction", sc1 form).
-//    Fused RMSNorm (Qwen3RMSNorm, qwen3_server_module.py:19-25): with `ss_in` the A operand
-//    is normalised on load, A' = bf16(w * bf16(x * rsqrt(sum(x^2)/K + eps))), from per-row
-//    partial sums of squares that the PRODUCER of x wrote (`ss_out` of an EPI_RESID GEMM:
-//    per 16-column tile, deterministic fixed-order sum in the consumer) -- so the two
-//    per-layer RMSNorm kernels disappear from the decode step.
-//  * gemm_tiled: M > 64 rows (prefill).  128x128x64 block tile, 4 waves (2x2, 64x64
-//    each), A and B staged through double-buffered LDS with global_load_lds (A
-//    XOR-swizzled on the source address, B already fragment-ordered), 32 MFMA per
-//    wave per K-step.
+// Kernels on v_mfma_f32_16x16x32_bf16 with weights in the fragment-packed layout of
+// common.h:
+//  * gemm_decode: M <= 64 rows.  HBM-bound weight stream (GEMV-like).  Workgroup = NW
+//    waves = one 16-column output tile (x S streams: gate and up for the SwiGLU GEMM) over
+//    the whole K range.  The K tiles are cut into batches of TW (1 KiB weight tiles + the
+//    matching activation fragments, straight into VGPRs); wave w takes batches w, w+NW, ...
+//    through a D-stage register ring: batch i+D-1 is issued before batch i is consumed, so
+//    (D-1)*TW weight tiles per wave stay in flight across the MFMAs (weights loaded
+//    non-temporal: each byte is read once per step).  The NW partial accumulators reduce
+//    through LDS; the epilogue (residual add / SwiGLU / argmax keys) is fused.  No split-K:
+//    measured on the box, every in-launch K split cost more than the balance it bought.
+//  * gemm_tiled / gemm_tiled256: M > 64 rows (prefill).  128x128 (4 waves) or 256x256
+//    (8 waves) block tiles, A and B staged through double-buffered LDS with
+//    global_load_lds (A XOR-swizzled on the source address, B already fragment-ordered).
 #include <stdlib.h>
+
+#include <utility>
 
 #include "common.h"
 #include "kernels.h"
-
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g)); }
 
@@ -37,121 +32,79 @@ struct DecodeArgs {
   const u16* A;
   int64_t lda;
   const u16* Wp;
-  int KT, n_tiles, KS, M;
+  int KT, n_tiles, M;
   u16* C;
   int64_t ldc;
   const u16* R;
   int64_t ldr;
   unsigned long long* keys;  // EPI_ARGMAX partial keys [n_tiles][M]
-  float* slab;               // split-K partials
-  unsigned slab_bytes;
-  unsigned* counters;
-  const float* ss_in;        // fused norm: [n_ss_in][64] partial sums of squares of A rows
-  int n_ss_in;
-  const u16* norm_w;         // fused norm weight [K]
-  float eps;
-  float* ss_out;             // EPI_RESID: [n_tiles][64] sums of squares of the bf16 outputs
 };
 
-template <int MT, int S, int TW, int EPI, bool NORM>
-__global__ __launch_bounds__(256) void gemm_decode_kernel(DecodeArgs g) {
+template <int MT, int S, int NW, int TW, int D, int EPI>
+__global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
-  __shared__ f32x4 red[4][NV];
-  __shared__ float sm_ss[16][64];
-  __shared__ float sm_inv[64];
-  __shared__ int sm_last;
-  const int KT = g.KT, KS = g.KS, M = g.M;
-  const int nt = blockIdx.x / KS, ks = blockIdx.x - (blockIdx.x / KS) * KS;
+  __shared__ f32x4 red[NW][NV];
+  const int KT = g.KT, M = g.M;
+  const int nt = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // slice [k0, k1) of the K tiles; processed in rounds of 4*TW tiles (one round when the
-  // dispatcher could choose KS = ceil(KT / (4*TW))), wave w taking TW consecutive tiles
-  const int SL = (KT + KS - 1) / KS;
-  const int k0 = ks * SL, k1 = min(KT, k0 + SL);
   const bf16x8* w0 = (const bf16x8*)(g.Wp + (int64_t)nt * KT * 512) + lane;
   const bf16x8* w1 = (const bf16x8*)(g.Wp + (int64_t)(nt + g.n_tiles) * KT * 512) + lane;
   const u16* a[MT];
-  int arow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int row = mt * 16 + (lane & 15);
     row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
-    arow[mt] = row;
     a[mt] = g.A + (int64_t)row * g.lda + 8 * (lane >> 4);
   }
-  const bf16x8 zero = as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   f32x4 acc[S][MT];
 #pragma unroll
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[s][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bool inv_ready = false;
-  for (int kr = k0 + wave * TW; kr < k1; kr += 4 * TW) {
-    bf16x8 wv[S][TW];
-    bf16x8 av[TW][MT];
+
+  const int nb = KT / TW;  // batches (the dispatcher guarantees KT % TW == 0)
+  int b = wave;
+  bf16x8 wv[D][S][TW], av[D][TW][MT];
+  auto issue = [&](auto stage, int bb) {
+    constexpr int d = decltype(stage)::value;
 #pragma unroll
     for (int u = 0; u < TW; ++u) {
-      const int kt = kr + u;
-      const bool ok = kt < k1;
-      wv[0][u] = ok ? w0[kt * 64] : zero;
-      if constexpr (S == 2) wv[1][u] = ok ? w1[kt * 64] : zero;
-    }
-#pragma unroll
-    for (int u = 0; u < TW; ++u) {
-      const int kt = kr + u;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) av[u][mt] = (kt < k1) ? *(const bf16x8*)(a[mt] + kt * 32) : zero;
-    }
-    if constexpr (NORM) {
-      if (!inv_ready) {
-        // per-row 1/rms from the producer's partial sums (weight loads already in flight);
-        // rows r < 16*MT, partial groups gr of the n_ss_in tiles, fixed summation order
-        constexpr int RR = MT * 16, G = 256 / RR;
-        const int r = threadIdx.x % RR, gr = threadIdx.x / RR;
-        if (gr < G) {
-          float t = 0.f;
-          for (int i = gr; i < g.n_ss_in; i += G) t += g.ss_in[i * 64 + r];
-          sm_ss[gr][r] = t;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (threadIdx.x < RR) {
-          float t = 0.f;
-          for (int i = 0; i < G; ++i) t += sm_ss[i][threadIdx.x];
-          sm_inv[threadIdx.x] = 1.0f / sqrtf(t / (float)(KT * 32) + g.eps);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        inv_ready = true;
-      }
-      float inv[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) inv[mt] = sm_inv[arow[mt]];
-#pragma unroll
-      for (int u = 0; u < TW; ++u) {
-        const int kt = kr + u;
-        const u16x8 wn = (kt < k1) ? *(const u16x8*)(g.norm_w + kt * 32 + 8 * (lane >> 4)) : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const u16x8 xv = __builtin_bit_cast(u16x8, av[u][mt]);
-          u16x8 o;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(wn[j]) * rbf(bf2f(xv[j]) * inv[mt]));
-          av[u][mt] = as_bf16x8(o);
-        }
-      }
+      wv[d][0][u] = __builtin_nontemporal_load(w0 + (bb * TW + u) * 64);
+      if constexpr (S == 2) wv[d][1][u] = __builtin_nontemporal_load(w1 + (bb * TW + u) * 64);
     }
 #pragma unroll
     for (int u = 0; u < TW; ++u)
 #pragma unroll
-      for (int s = 0; s < S; ++s)
+      for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
+  };
+  if (b < nb) {
+    // prologue: stages 0..D-2
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      ((b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
+    }(std::make_integer_sequence<int, D - 1>{});
+    bool fin = false;
+    while (!fin) {
+      [&]<int... I>(std::integer_sequence<int, I...>) {
+        auto step = [&](auto stage) {
+          constexpr int d = decltype(stage)::value;
+          if (fin) return;
+          const int nxt = b + (D - 1) * NW;
+          if (nxt < nb) issue(std::integral_constant<int, (d + D - 1) % D>{}, nxt);
+          // keep the issued loads ahead of the MFMAs (the scheduler would otherwise
+          // interleave them to save registers, leaving few loads in flight)
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[u][mt], wv[s][u], acc[s][mt]);
-  }
-  if constexpr (NORM) {
-    // waves without a round must still join the two barriers of the norm prologue
-    if (!inv_ready) {
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_s_barrier();
+          for (int u = 0; u < TW; ++u)
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+#pragma unroll
+              for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[d][u][mt], wv[d][s][u], acc[s][mt]);
+          __builtin_amdgcn_sched_barrier(0);
+          b += NW;
+          if (b >= nb) fin = true;
+        };
+        (step(std::integral_constant<int, I>{}), ...);
+      }(std::make_integer_sequence<int, D>{});
     }
   }
 #pragma unroll
@@ -161,48 +114,16 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(DecodeArgs g) {
   __syncthreads();
   // thread p < MT*64 owns (mt, lane ln) of every stream s: rows mt*16 + 4*(ln>>4) + r, col ln&15
   const int p = threadIdx.x;
-  const bool own = p < MT * 64;
+  if (p >= MT * 64) return;
   f32x4 v[S];
-  if (own) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const int q = s * MT * 64 + p;
-      v[s] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
-    }
+  for (int s = 0; s < S; ++s) {
+    const int q = s * MT * 64 + p;
+    f32x4 t = red[0][q];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) t += red[w][q];
+    v[s] = t;
   }
-  if (KS > 1) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(g.slab, 0, g.slab_bytes, 0x00020000);
-    if (own) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        const unsigned off = (unsigned)((((int64_t)nt * KS + ks) * NV + s * MT * 64 + p) * 16);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, v[s]), rs, off, 0, 16);  // sc1
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned prev = __hip_atomic_fetch_add(&g.counters[nt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sm_last = prev == (unsigned)(KS - 1);
-      if (sm_last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&g.counters[nt], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
-    if (!sm_last) return;
-    if (own) {
-#pragma unroll
-      for (int s = 0; s < S; ++s) {
-        f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < KS; ++k)
-          t += *(const f32x4*)(g.slab + ((((int64_t)nt * KS + k) * NV + s * MT * 64 + p) * 4));
-        v[s] = t;
-      }
-    }
-  }
-  if (!own) return;
   const int mt = p >> 6, ln = p & 63;
   const int col = nt * 16 + (ln & 15);
 #pragma unroll
@@ -220,79 +141,49 @@ __global__ __launch_bounds__(256) void gemm_decode_kernel(DecodeArgs g) {
         if ((ln & 15) == 0) g.keys[(int64_t)nt * M + row] = key;
         if (g.C) g.C[(int64_t)row * g.ldc + col] = f2bf(lv);
       }
-    } else {
+    } else if (row < M) {
       float o;
       if constexpr (EPI == EPI_NONE) {
         o = v[0][r];
       } else if constexpr (EPI == EPI_RESID) {
-        o = rbf(v[0][r]) + bf2f(g.R[(int64_t)(row < M ? row : M - 1) * g.ldr + col]);
+        o = rbf(v[0][r]) + bf2f(g.R[(int64_t)row * g.ldr + col]);
       } else {  // EPI_SILU
         o = rbf(silu_f(rbf(v[0][r]))) * rbf(v[1][r]);
       }
-      const u16 ob = f2bf(o);
-      if (row < M) g.C[(int64_t)row * g.ldc + col] = ob;
-      if constexpr (EPI == EPI_RESID) {
-        if (g.ss_out) {  // this tile's share of the next RMSNorm's sum of squares
-          float sq = bf2f(ob) * bf2f(ob);
-#pragma unroll
-          for (int off = 8; off > 0; off >>= 1) sq += __shfl_xor(sq, off, 16);
-          if ((ln & 15) == 0 && row < M) g.ss_out[nt * 64 + row] = sq;
-        }
-      }
+      g.C[(int64_t)row * g.ldc + col] = f2bf(o);
     }
   }
 }
 
-// weight tiles per wave and round: ~16-32 loads (weights + activation fragments) in flight
-__host__ __device__ constexpr int decode_tw(int MT, int S) {
-  return S == 1 ? (MT == 1 ? 16 : (MT == 2 ? 8 : 4)) : (MT == 1 ? 8 : 4);
-}
+// ring shape per (row tiles, streams): tuned on the Qwen3-8B decode shapes (tools/gemv_lab.hip)
+template <int MT, int S>
+struct DecodeCfg {
+  static constexpr int NW = S == 1 ? 8 : 4;
+  static constexpr int TW = (MT <= 2) ? 4 : 2;
+  static constexpr int D = (S == 1 && MT == 1) ? 3 : 2;
+};
 
-static int decode_ks(int KT, int MT, int S) {
-  const int tw = decode_tw(MT, S);
-  return (KT + 4 * tw - 1) / (4 * tw);
-}
-
-size_t gemm_decode_ws_bytes(int N, int K, int epi, int M) {
-  const int S = (epi == EPI_SILU) ? 2 : 1;
-  const int MT = M <= 16 ? 1 : (M <= 32 ? 2 : (M <= 48 ? 3 : 4));
-  const int KS = decode_ks(K / 32, MT, S);
-  return KS > 1 ? (size_t)(N / 16) * KS * S * MT * 1024 : 0;
-}
-
-template <int MT, int EPI, bool NORM>
-static void decode_launch(DecodeArgs a, const GemmWs* ws, hipStream_t s) {
+template <int MT, int EPI>
+static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
-  constexpr int TW = decode_tw(MT, S);
-  // one round of 4*TW tiles per workgroup when the workspace can hold the KS partials
-  a.KS = decode_ks(a.KT, MT, S);
-  constexpr size_t part_bytes = (size_t)S * MT * 64 * 16;
-  if (!ws || !ws->slab || (size_t)a.n_tiles * a.KS * part_bytes > ws->slab_bytes || a.n_tiles > ws->n_counters)
-    a.KS = 1;
-  a.slab = ws ? ws->slab : nullptr;
-  a.slab_bytes = ws ? (unsigned)(ws->slab_bytes < 0xFFFFFFF0ull ? ws->slab_bytes : 0xFFFFFFF0ull) : 0;
-  a.counters = ws ? ws->counters : nullptr;
-  hipLaunchKernelGGL((gemm_decode_kernel<MT, S, TW, EPI, NORM>), dim3(a.n_tiles * a.KS), dim3(256), 0, s, a);
-}
-
-template <int EPI, bool NORM>
-static void decode_mt(const DecodeArgs& a, const GemmWs* ws, hipStream_t s) {
-  if (a.M <= 16)
-    decode_launch<1, EPI, NORM>(a, ws, s);
-  else if (a.M <= 32)
-    decode_launch<2, EPI, NORM>(a, ws, s);
-  else if (a.M <= 48)
-    decode_launch<3, EPI, NORM>(a, ws, s);
-  else
-    decode_launch<4, EPI, NORM>(a, ws, s);
+  using C = DecodeCfg<MT, S>;
+  if (a.KT % C::TW == 0)
+    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI>), dim3(a.n_tiles), dim3(C::NW * 64), 0,
+                       s, a);
+  else  // odd K/32 (single-op API only; every Qwen3 projection has K % 128 == 0)
+    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI>), dim3(a.n_tiles), dim3(C::NW * 64), 0, s, a);
 }
 
 template <int EPI>
-static void decode_norm(const DecodeArgs& a, const GemmWs* ws, hipStream_t s) {
-  if (a.ss_in)
-    decode_mt<EPI, true>(a, ws, s);
+static void decode_mt(const DecodeArgs& a, hipStream_t s) {
+  if (a.M <= 16)
+    decode_launch<1, EPI>(a, s);
+  else if (a.M <= 32)
+    decode_launch<2, EPI>(a, s);
+  else if (a.M <= 48)
+    decode_launch<3, EPI>(a, s);
   else
-    decode_mt<EPI, false>(a, ws, s);
+    decode_launch<4, EPI>(a, s);
 }
 
 // ============================================================ tiled (prefill) kernel
@@ -553,8 +444,7 @@ bool gemm_uses_tiled(int M, int N, int K, int epi) {
 }
 
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
-                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, const GemmWs* ws,
-                 hipStream_t s, const GemmNorm* norm) {
+                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
   if (gemm_uses_tiled(M, N, K, epi) && use_tiled256(M, N, epi)) {
@@ -591,8 +481,7 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     }
     return;
   }
-  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail; the
-  // fused norm and the sum-of-squares output are only used with M <= 64)
+  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail)
   for (int m0 = 0; m0 < M; m0 += 64) {
     DecodeArgs a = {};
     a.M = (M - m0) < 64 ? (M - m0) : 64;
@@ -606,18 +495,11 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     a.R = R ? R + (int64_t)m0 * ldr : nullptr;
     a.ldr = ldr;
     a.keys = keys;
-    if (norm && M <= 64) {
-      a.ss_in = norm->ss_in;
-      a.n_ss_in = norm->n_ss_in;
-      a.norm_w = norm->w;
-      a.eps = norm->eps;
-      a.ss_out = norm->ss_out;
-    }
     switch (epi) {
-      case EPI_NONE: decode_norm<EPI_NONE>(a, ws, s); break;
-      case EPI_RESID: decode_norm<EPI_RESID>(a, ws, s); break;
-      case EPI_SILU: decode_norm<EPI_SILU>(a, ws, s); break;
-      default: decode_norm<EPI_ARGMAX>(a, ws, s); break;
+      case EPI_NONE: decode_mt<EPI_NONE>(a, s); break;
+      case EPI_RESID: decode_mt<EPI_RESID>(a, s); break;
+      case EPI_SILU: decode_mt<EPI_SILU>(a, s); break;
+      default: decode_mt<EPI_ARGMAX>(a, s); break;
     }
     if (epi == EPI_ARGMAX) break;  // argmax requires M <= 64 (checked by the caller)
   }

@@ -33,34 +33,9 @@ void launch_decode_advance(int32_t* positions, int32_t* slots, int32_t* ctx_lens
 // gemm.hip.  Wp is fragment-packed (common.h).  N counts OUTPUT columns: for EPI_SILU the
 // packed weight holds 2N rows ([gate; up]).  For EPI_ARGMAX `partial` receives
 // (N/16) x M keys and `amax_keys` the per-row reduction (M <= 64).
-// Split-K workspace of the decode GEMM: fp32 partial slabs + per-16-column-tile counters
-// (zero before first use; every launch leaves them zero).  nullptr -> no K split.
-struct GemmWs {
-  float* slab;
-  size_t slab_bytes;
-  unsigned* counters;
-  int n_counters;
-};
-// split-K partial bytes the decode GEMM wants for C[M][N] = A[M][K] W^T (0: no split)
-size_t gemm_decode_ws_bytes(int N, int K, int epi, int M);
-// Fused RMSNorm of the decode GEMM (M <= 64 only):
-//   ss_in  [n_ss_in][64] partial sums of squares of the A rows (fixed-order sum) -> A is
-//          normalised on load with weight w and eps (Qwen3RMSNorm rounding points);
-//   ss_out EPI_RESID: [N/16][64] per-tile sums of squares of the bf16 output rows, i.e. the
-//          ss_in of the next norm.
-struct GemmNorm {
-  const float* ss_in;
-  int n_ss_in;
-  const u16* w;
-  float eps;
-  float* ss_out;
-};
 bool gemm_uses_tiled(int M, int N, int K, int epi);
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
-                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, const GemmWs* ws,
-                 hipStream_t s, const GemmNorm* norm = nullptr);
-// per-row sum of squares of x[M][N] bf16 -> ss[row] (one partial: n_ss_in = 1)
-void launch_row_ss(const u16* x, int64_t ldx, int M, int N, float* ss, hipStream_t s);
+                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s);
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
                           int32_t* ids, hipStream_t s);
 

@@ -10,6 +10,7 @@
 //     -> rmsnorm -> gate/up gemm (+SwiGLU) -> down gemm (+resid)
 // with no allocation and no host synchronisation on the hot path.
 #include <math.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -88,9 +89,6 @@ struct InferdSpan {
   float* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
   unsigned long long* argmax_partial = nullptr;
-  GemmWs gws = {nullptr, 0, nullptr, 0};
-  float* ss_a = nullptr;  // fused-norm row statistics: [hidden/16][64] partial sums of squares
-  float* ss_b = nullptr;
   int32_t* err = nullptr;
   std::vector<void*> allocs;
   // optional per-kernel-class timing with HIP events on the launch stream
@@ -209,32 +207,6 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
-  SALLOC(s->ss_a, (size_t)(h / 16) * 64 * 4);
-  SALLOC(s->ss_b, (size_t)(h / 16) * 64 * 4);
-  {
-    // split-K workspace of the decode GEMMs (M <= 64), sized for the span's largest need
-    const int Md = c.max_tokens < 64 ? c.max_tokens : 64;
-    const int Mh = c.max_seqs < 64 ? c.max_seqs : 64;
-    size_t need = 0;
-    auto upd = [&](size_t b) { need = b > need ? b : need; };
-    upd(gemm_decode_ws_bytes(s->qkv_rows(), h, EPI_NONE, Md));
-    upd(gemm_decode_ws_bytes(h, H * HEAD_DIM, EPI_RESID, Md));
-    upd(gemm_decode_ws_bytes(I, h, EPI_SILU, Md));
-    upd(gemm_decode_ws_bytes(h, I, EPI_RESID, Md));
-    int max_nt = s->qkv_rows() / 16;
-    if (h / 16 > max_nt) max_nt = h / 16;
-    if (I / 16 > max_nt) max_nt = I / 16;
-    if (c.has_lm_head) {
-      upd(gemm_decode_ws_bytes(c.vocab, h, EPI_ARGMAX, Mh));
-      if (c.vocab / 16 > max_nt) max_nt = c.vocab / 16;
-    }
-    s->gws.n_counters = max_nt;
-    s->gws.slab_bytes = need;
-    SALLOC(s->gws.slab, s->gws.slab_bytes);
-    SALLOC(s->gws.counters, (size_t)max_nt * 4);
-    if (hipMemset(s->gws.counters, 0, (size_t)max_nt * 4) != hipSuccess)
-      return bail(fail(INFERD_ERR_HIP, "memset failed"));
-  }
   SALLOC(s->err, 256);
   if (hipMemset(s->err, 0, 4) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(INFERD_ERR_HIP, "init sync failed"));
@@ -396,33 +368,15 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   if (c.n_layers == 0 && x_out && x != x_out)
     HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
   const AttnBatch ab = to_attn(b);
-  // Decode-sized batches (M <= 64, the decode GEMM path) fold both RMSNorms into the GEMMs:
-  // the residual-producing GEMMs emit per-tile sums of squares (ss_b after o_proj, ss_a
-  // after down_proj) that the next qkv / gate-up GEMM consumes while loading its A operand;
-  // the span input gets its row statistics from one row_ss launch.
-  const bool fuse = M <= 64;
-  int n_ss_a = 1;
   long pe = -1;
-  if (fuse && c.n_layers > 0) {
-    pe = s->prof_begin(PROF_NORM, st);
-    launch_row_ss(x, h, M, h, s->ss_a, st);
-    s->prof_end(pe, st);
-  }
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
     u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
-    if (!fuse) {
-      pe = s->prof_begin(PROF_NORM, st);
-      launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
-      s->prof_end(pe, st);
-    }
+    pe = s->prof_begin(PROF_NORM, st);
+    launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
+    s->prof_end(pe, st);
     pe = s->prof_begin(PROF_QKV, st);
-    if (fuse) {
-      const GemmNorm nq = {s->ss_a, n_ss_a, W.in_ln, c.rms_eps, nullptr};
-      launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, &s->gws, st, &nq);
-    } else {
-      launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, &s->gws, st);
-    }
+    launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st);
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_ROPE, st);
     launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
@@ -436,25 +390,18 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     s->prof_end(pe, st);
     // h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
     pe = s->prof_begin(PROF_O, st);
-    const GemmNorm no = {nullptr, 0, nullptr, 0.f, s->ss_b};
-    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, &s->gws, st,
-                fuse ? &no : nullptr);
+    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);
+    s->prof_end(pe, st);
+    pe = s->prof_begin(PROF_NORM, st);
+    launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_GATEUP, st);
-    if (fuse) {
-      const GemmNorm ng = {s->ss_b, h / 16, W.post_ln, c.rms_eps, nullptr};
-      launch_gemm(s->h, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, &s->gws, st, &ng);
-    } else {
-      launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
-      launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, &s->gws, st);
-    }
+    launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st);
     s->prof_end(pe, st);
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
     pe = s->prof_begin(PROF_DOWN, st);
-    const GemmNorm nd = {nullptr, 0, nullptr, 0.f, s->ss_a};
-    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, &s->gws, st, fuse ? &nd : nullptr);
+    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, st);
     s->prof_end(pe, st);
-    n_ss_a = h / 16;
     x = out;
     if (layer_out)
       HIP_TRY(hipMemcpyAsync((u16*)layer_out + (size_t)l * M * h, x, (size_t)M * h * 2,
@@ -467,7 +414,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pe = s->prof_begin(PROF_LMHEAD, st);
     launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st);
     launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
-                s->argmax_partial, &s->gws, st);
+                s->argmax_partial, st);
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
     s->prof_end(pe, st);
   }
@@ -616,17 +563,7 @@ extern "C" int inferd_gemm(const void* a, const void* w, void* c, const void* r,
   if (!a || !w || !c || m <= 0 || n % 16 || k % 32) return fail(INFERD_ERR_ARG, "gemm needs n%16==0, k%32==0");
   if (epi < 0 || epi > 2) return fail(INFERD_ERR_ARG, "bad epilogue");
   if (epi == INFERD_EPI_RESID && !r) return fail(INFERD_ERR_ARG, "resid epilogue needs R");
-  // process-wide split-K workspace of the single-op entry point (allocated once, outside
-  // any capture; the span owns its own)
-  static GemmWs ws = {nullptr, 0, nullptr, 0};
-  if (!ws.slab) {
-    ws.n_counters = 1 << 16;
-    ws.slab_bytes = (size_t)256 << 20;
-    HIP_TRY(hipMalloc((void**)&ws.slab, ws.slab_bytes));
-    HIP_TRY(hipMalloc((void**)&ws.counters, ws.n_counters * 4));
-    HIP_TRY(hipMemset(ws.counters, 0, ws.n_counters * 4));
-  }
-  launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr, &ws,
+  launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr,
               (hipStream_t)stream);
   LAUNCH_CHECK();
   return INFERD_OK;
