@@ -157,6 +157,13 @@ int inferd_span_error_flags(InferdSpan* span, int32_t* flags);
 #define INFERD_PROF_NCLASSES 8
 int inferd_span_profile_start(InferdSpan* span, int32_t max_pairs);
 int inferd_span_profile_stop(InferdSpan* span, double* total_ms, int32_t* counts, int32_t n_classes);
+// Event pairs recorded so far (a graph captured while profiling holds its pairs as graph
+// nodes: pairs [before, after) of its capture).
+int inferd_span_profile_pairs(InferdSpan* span, int32_t* n_pairs);
+// ADD the elapsed times of pairs [first_pair, first_pair + n_pairs) into total_ms / counts
+// per class (waits for them).  Call after each replay of a profiled graph.
+int inferd_span_profile_collect(InferdSpan* span, int32_t first_pair, int32_t n_pairs, double* total_ms,
+                                int32_t* counts, int32_t n_classes);
 
 /* Device base pointer of one layer's KV pool ([pages][K|V][kv_heads][64*128] bf16). */
 int inferd_span_kv_layer(InferdSpan* span, int32_t layer, void** out);

@@ -439,7 +439,8 @@ extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, in
   if (!stream) return fail(INFERD_ERR_ARG, "graph capture needs a non-null stream");
   if (advance && !b->decode) return fail(INFERD_ERR_ARG, "advance needs a decode batch");
   hipStream_t st = (hipStream_t)stream;
-  s->prof_on = false;  // events are not captured
+  // with profiling on, the per-kernel-class event pairs are captured as graph nodes
+  // (inferd_span_profile_collect reads them after each replay)
   HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
   int rc = INFERD_OK;
   if (advance)
@@ -509,6 +510,29 @@ extern "C" int inferd_span_profile_stop(InferdSpan* s, double* total_ms, int32_t
     }
   }
   s->prof_used = 0;
+  return INFERD_OK;
+}
+
+extern "C" int inferd_span_profile_pairs(InferdSpan* s, int32_t* n_pairs) {
+  if (!s || !n_pairs) return fail(INFERD_ERR_ARG, "null argument");
+  *n_pairs = (int32_t)(s->prof_used / 2);
+  return INFERD_OK;
+}
+
+extern "C" int inferd_span_profile_collect(InferdSpan* s, int32_t first_pair, int32_t n_pairs, double* total_ms,
+                                           int32_t* counts, int32_t n_classes) {
+  if (!s || first_pair < 0 || n_pairs < 0 || (size_t)(first_pair + n_pairs) * 2 > s->prof_used)
+    return fail(INFERD_ERR_ARG, "bad profile pair range");
+  for (int32_t k = first_pair; k < first_pair + n_pairs; ++k) {
+    HIP_TRY(hipEventSynchronize(s->prof_events[2 * k + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->prof_events[2 * k], s->prof_events[2 * k + 1]));
+    const int c = s->prof_class[k];
+    if (c >= 0 && c < n_classes) {
+      total_ms[c] += ms;
+      counts[c] += 1;
+    }
+  }
   return INFERD_OK;
 }
 

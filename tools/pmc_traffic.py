@@ -14,9 +14,9 @@ half the bytes of a wide (16 B/lane) coalesced streaming read, so fetched bytes 
 2 * FETCH_SIZE * 1024 for the 16-B-per-lane streams the decode kernels issue; WRITE_SIZE is
 exact for 16-B stores.  Infinity-Cache hits are counted as fetches.
 
-Kernel classes: dispatch names are mapped to the bench's classes; o_proj and down_proj use
-the same template instance (EPI_RESID, no fused norm), so they are told apart by order
-within a layer (o first, down second).
+Kernel classes: decode-phase dispatches (after the last prefill kernel) are mapped to the
+bench's classes; o_proj and down_proj use the same template instance (EPI_RESID), so they
+are told apart by order within a layer (o first, down second).
 """
 import csv
 import glob
@@ -38,18 +38,31 @@ def rows(d):
     return out
 
 
+PREFILL_KEYS = ("gemm_tiled", "attn_prefill")
+
+
 def classify(name):
+    """Bench kernel class of a decode-phase dispatch name (None: not a decode kernel)."""
     if "gemm_decode_kernel" in name:
-        m = re.search(r"gemm_decode_kernel<(\d+), (\d+), (\d+), (\d+), (true|false)>", name)
+        m = re.search(r"gemm_decode_kernel<([-\d, ]+)>", name)
         if not m:
             return "gemm_decode"
-        epi = int(m.group(4))
+        epi = int(m.group(1).split(",")[-1])
         return {0: "qkv_gemm", 1: "resid_gemm", 2: "gateup_gemm", 3: "lm_head_argmax"}[epi]
     for key, cls in (("attn_decode_kernel", "attention"), ("qk_norm_rope_kv", "qk_norm_rope_kv"),
-                     ("row_ss", "rmsnorm"), ("rmsnorm", "rmsnorm"), ("argmax_reduce", "lm_head_argmax")):
+                     ("rmsnorm", "rmsnorm"), ("argmax_reduce", "lm_head_argmax")):
         if key in name:
             return cls
     return None
+
+
+def decode_phase(seq):
+    """Dispatches after the last prefill kernel (the bench prefills before it decodes)."""
+    last = -1
+    for i, (name, _) in enumerate(seq):
+        if any(k in name for k in PREFILL_KEYS):
+            last = i
+    return seq[last + 1:]
 
 
 def per_dispatch(d, counter):
@@ -67,7 +80,7 @@ def per_dispatch(d, counter):
 def summarize(seq, scale):
     acc = defaultdict(list)
     resid_toggle = 0
-    for name, v in seq:
+    for name, v in decode_phase(seq):
         c = classify(name)
         if c is None:
             continue
