@@ -15,11 +15,11 @@ Before timing: every sequence is prefilled with 2048 tokens through the real pre
 path (untimed; its rate is reported as `prefill`), so the KV cache holds real K/V.
 Timed region: K decode steps bracketed by barrier + synchronize; each stage's step of a
 microbatch is one replay of a captured HIP graph; value = tokens of all ranks /
-max-over-ranks time.  Roofline: per-kernel-class HIP events (inferd_span_profile_*)
-captured INSIDE a second set of decode graphs (event-record nodes around every kernel
-class, on the stream the kernels run on), replayed `--profile-steps` times right after the
-timed region; the dominant kernel class's algorithmic bytes per launch / its mean event
-time, against 8 TB/s HBM.  `traffic` = PMC-measured HBM bytes per launch of that class
+max-over-ranks time.  Roofline: per-kernel-class HIP events (inferd_span_profile_*) on
+the launch stream around every kernel of `--profile-steps` eager decode steps of the same
+workload, run right after the timed region (HIP cannot time event nodes inside a replayed
+graph); the dominant kernel class's algorithmic bytes per launch / its mean event time,
+against 8 TB/s HBM.  `traffic` = PMC-measured HBM bytes per launch of that class
 (tools/profile_decode.sh -> profiles/traffic_r01.json).  cpu_baseline: the oracle
 (oracle/qwen3_ref.py, `port`) on the host cores, rank 0 at N = 1 only.
 """
@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--cpu-layers", type=int, default=2, help="layers timed by the CPU baseline sample")
     p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing pass")
-    p.add_argument("--profile-steps", type=int, default=8, help="event-instrumented decode-graph replays")
+    p.add_argument("--profile-steps", type=int, default=8, help="eager event-instrumented decode steps")
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
     p.add_argument("--mode", choices=("decode", "prefill"), default="decode",
                    help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline)")
@@ -237,8 +237,8 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # ---- per-kernel HIP-event timings: the same decode step captured with event-record
-    # nodes around each kernel class, replayed right after the timed region
+    # ---- per-kernel HIP-event timings: the same decode kernels launched eagerly (events
+    # cannot be timed inside a replayed graph); right after the timed region, same cache state
     prof = None if args.no_profile else st.profile_decode(args.profile_steps)
     t = torch.tensor([elapsed, t_prefill], dtype=torch.float64, device=dev)
     if dist:

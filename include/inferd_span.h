@@ -32,7 +32,7 @@ extern "C" {
 #define INFERD_OK 0
 #define INFERD_ERR_ARG 1   /* bad argument / shape / unsupported configuration */
 #define INFERD_ERR_HIP 2   /* HIP runtime error (allocation, launch) */
-#define INFERD_ERR_STATE 3 /* handle not initialised */
+#define INFERD_ERR_STATE 3 /* handle not initialised / weights not ready (see set_weight) */
 
 #define INFERD_KV_PAGE_TOKENS 64
 
@@ -106,7 +106,12 @@ int inferd_span_init_synthetic(InferdSpan* span, uint64_t seed, void* stream);
  * state-dict leaf names (qwen3_server_module.py:101-124, :169-176):
  * q_proj k_proj v_proj o_proj q_norm k_norm input_layernorm post_attention_layernorm
  * gate_proj up_proj down_proj | embed_tokens norm lm_head.  Projections are packed into
- * the device fragment layout (fused [q;k;v] and [gate;up]). */
+ * the device fragment layout (fused [q;k;v] and [gate;up]).  input_layernorm is folded
+ * into q/k/v_proj and post_attention_layernorm into gate/up_proj at pack time
+ * (W[n][k] * w[k]; the GEMM scales rows by rsqrt(mean(x^2) + eps)), so a layer's norm
+ * weight must be set BEFORE the projections that consume it; re-setting a norm weight
+ * marks those projections stale and forward returns INFERD_ERR_STATE until they are set
+ * again. */
 int inferd_span_set_weight(InferdSpan* span, int32_t layer, const char* name,
                            const void* src, int64_t rows, int64_t cols, void* stream);
 
@@ -157,13 +162,6 @@ int inferd_span_error_flags(InferdSpan* span, int32_t* flags);
 #define INFERD_PROF_NCLASSES 8
 int inferd_span_profile_start(InferdSpan* span, int32_t max_pairs);
 int inferd_span_profile_stop(InferdSpan* span, double* total_ms, int32_t* counts, int32_t n_classes);
-// Event pairs recorded so far (a graph captured while profiling holds its pairs as graph
-// nodes: pairs [before, after) of its capture).
-int inferd_span_profile_pairs(InferdSpan* span, int32_t* n_pairs);
-// ADD the elapsed times of pairs [first_pair, first_pair + n_pairs) into total_ms / counts
-// per class (waits for them).  Call after each replay of a profiled graph.
-int inferd_span_profile_collect(InferdSpan* span, int32_t first_pair, int32_t n_pairs, double* total_ms,
-                                int32_t* counts, int32_t n_classes);
 
 /* Device base pointer of one layer's KV pool ([pages][K|V][kv_heads][64*128] bf16). */
 int inferd_span_kv_layer(InferdSpan* span, int32_t layer, void** out);

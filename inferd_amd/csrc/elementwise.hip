@@ -34,9 +34,10 @@ void launch_weightgen(u16* dst, int64_t n, uint64_t key, float scale, float cent
 }
 
 // ------------------------------------------------------------------ fragment packing
-// one thread per 16-byte chunk: chunk c = (nt*KT + kt)*64 + lane
+// one thread per 16-byte chunk: chunk c = (nt*KT + kt)*64 + lane.  With colscale, each
+// element becomes bf16(W[n][k] * colscale[k]) (fp32 product, one RNE rounding).
 __global__ void pack_kernel(const u16* __restrict__ src, int64_t ld, int N, int K,
-                            u16* __restrict__ dst) {
+                            u16* __restrict__ dst, const u16* __restrict__ colscale) {
   int KT = K / 32;
   int64_t nchunks = (int64_t)(N / 16) * KT * 64;
   int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -49,15 +50,42 @@ __global__ void pack_kernel(const u16* __restrict__ src, int64_t ld, int N, int 
     int64_t row = nt * 16 + (lane & 15);
     int col = kt * 32 + 8 * (lane >> 4);
     u16x8 v = *(const u16x8*)(src + row * ld + col);
+    if (colscale) {
+      const u16x8 w = *(const u16x8*)(colscale + col);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) * bf2f(w[j]));
+    }
     *(u16x8*)(dst + c * 8) = v;
   }
 }
 
-void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s) {
+void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s, const u16* colscale) {
   int64_t nchunks = (int64_t)(N / 16) * (K / 32) * 64;
   int64_t blocks = (nchunks + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, ld, N, K, dst);
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, ld, N, K, dst, colscale);
+}
+
+// rs[row] = 1 / sqrt(mean(x[row]^2) + eps): the row scale of a folded-RMSNorm GEMM (prefill)
+__global__ __launch_bounds__(256) void row_inv_rms_kernel(const u16* __restrict__ x, int64_t ldx, int K, float eps,
+                                                          float* __restrict__ rs) {
+  __shared__ float red[4];
+  const u16* xr = x + (int64_t)blockIdx.x * ldx;
+  float t = 0.f;
+  for (int c = threadIdx.x; c < K / 8; c += 256) {
+    const u16x8 p = *(const u16x8*)(xr + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t = fmaf(bf2f(p[j]), bf2f(p[j]), t);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) rs[blockIdx.x] = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + eps);
+}
+
+void launch_row_inv_rms(const u16* x, int64_t ldx, int M, int K, float eps, float* rs, hipStream_t s) {
+  hipLaunchKernelGGL(row_inv_rms_kernel, dim3(M), dim3(256), 0, s, x, ldx, K, eps, rs);
 }
 
 // inverse (tests / debugging): packed -> row-major

@@ -38,12 +38,14 @@ struct DecodeArgs {
   const u16* R;
   int64_t ldr;
   unsigned long long* keys;  // EPI_ARGMAX partial keys [n_tiles][M]
+  float eps;                 // NORM: RMSNorm epsilon
 };
 
-template <int MT, int S, int NW, int TW, int D, int EPI>
+template <int MT, int S, int NW, int TW, int D, int EPI, bool NORM>
 __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
+  __shared__ float sm_ss[NORM ? NW : 1][MT * 16];
   const int KT = g.KT, M = g.M;
   const int nt = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -61,6 +63,9 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[s][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssq[MT];  // NORM: this lane's share of sum(x^2) of row mt*16 + (lane & 15)
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) ssq[mt] = 0.f;
 
   const int nb = KT / TW;  // batches (the dispatcher guarantees KT % TW == 0)
   int b = wave;
@@ -99,6 +104,16 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
             for (int s = 0; s < S; ++s)
 #pragma unroll
               for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[d][u][mt], wv[d][s][u], acc[s][mt]);
+          if constexpr (NORM) {
+#pragma unroll
+            for (int u = 0; u < TW; ++u)
+#pragma unroll
+              for (int mt = 0; mt < MT; ++mt) {
+                const u16x8 xv = __builtin_bit_cast(u16x8, av[d][u][mt]);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ssq[mt] = fmaf(bf2f(xv[j]), bf2f(xv[j]), ssq[mt]);
+              }
+          }
           __builtin_amdgcn_sched_barrier(0);
           b += NW;
           if (b >= nb) fin = true;
@@ -111,6 +126,16 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) red[wave][(s * MT + mt) * 64 + lane] = acc[s][mt];
+  if constexpr (NORM) {
+    // lanes l, l^16, l^32, l^48 hold the four k-quarters of row (l & 15)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      float t = ssq[mt];
+      t += __shfl_xor(t, 16);
+      t += __shfl_xor(t, 32);
+      if (lane < 16) sm_ss[wave][mt * 16 + lane] = t;
+    }
+  }
   __syncthreads();
   // thread p < MT*64 owns (mt, lane ln) of every stream s: rows mt*16 + 4*(ln>>4) + r, col ln&15
   const int p = threadIdx.x;
@@ -126,6 +151,19 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   }
   const int mt = p >> 6, ln = p & 63;
   const int col = nt * 16 + (ln & 15);
+  if constexpr (NORM) {
+    // folded RMSNorm: out = rsqrt(mean(x^2) + eps) * (x @ (W * w)^T)   
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = mt * 16 + 4 * (ln >> 4) + r;
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) t += sm_ss[w][rr];
+      const float inv = 1.0f / sqrtf(t / (float)(KT * 32) + g.eps);
+#pragma unroll
+      for (int s = 0; s < S; ++s) v[s][r] *= inv;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = mt * 16 + 4 * (ln >> 4) + r;
@@ -163,27 +201,28 @@ struct DecodeCfg {
   static constexpr int D = (S == 1 && MT == 1) ? 3 : 2;
 };
 
-template <int MT, int EPI>
+template <int MT, int EPI, bool NORM>
 static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   using C = DecodeCfg<MT, S>;
   if (a.KT % C::TW == 0)
-    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI>), dim3(a.n_tiles), dim3(C::NW * 64), 0,
-                       s, a);
+    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM>), dim3(a.n_tiles),
+                       dim3(C::NW * 64), 0, s, a);
   else  // odd K/32 (single-op API only; every Qwen3 projection has K % 128 == 0)
-    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI>), dim3(a.n_tiles), dim3(C::NW * 64), 0, s, a);
+    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM>), dim3(a.n_tiles), dim3(C::NW * 64), 0,
+                       s, a);
 }
 
-template <int EPI>
+template <int EPI, bool NORM>
 static void decode_mt(const DecodeArgs& a, hipStream_t s) {
   if (a.M <= 16)
-    decode_launch<1, EPI>(a, s);
+    decode_launch<1, EPI, NORM>(a, s);
   else if (a.M <= 32)
-    decode_launch<2, EPI>(a, s);
+    decode_launch<2, EPI, NORM>(a, s);
   else if (a.M <= 48)
-    decode_launch<3, EPI>(a, s);
+    decode_launch<3, EPI, NORM>(a, s);
   else
-    decode_launch<4, EPI>(a, s);
+    decode_launch<4, EPI, NORM>(a, s);
 }
 
 // ============================================================ tiled (prefill) kernel
@@ -194,7 +233,8 @@ static void decode_mt(const DecodeArgs& a, hipStream_t s) {
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_tiled_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
-    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M) {
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
+    const float* __restrict__ rs) {
   // LDS: 2 buffers x (A 16 KiB + B 16 KiB), one array (guide §5 trap 4a)
   __shared__ __attribute__((aligned(16))) char lds[2 * 32768];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -295,19 +335,20 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wr * 64 + mt * 16 + 4 * (lane >> 4) + r;
       if (row >= M) continue;
+      const float sc = rs ? rs[row] : 1.0f;  // folded RMSNorm row scale
       if constexpr (EPI == EPI_SILU) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
           const int col = n0 + wc * 32 + nt * 16 + (lane & 15);
-          float g = rbf(acc[mt][nt][r]);
-          float u = rbf(acc[mt][nt + 2][r]);
+          float g = rbf(acc[mt][nt][r] * sc);
+          float u = rbf(acc[mt][nt + 2][r] * sc);
           C[(int64_t)row * ldc + col] = f2bf(rbf(silu_f(g)) * u);
         }
       } else {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
-          float o = acc[mt][nt][r];
+          float o = acc[mt][nt][r] * sc;
           if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(R[(int64_t)row * ldr + col]);
           C[(int64_t)row * ldc + col] = f2bf(o);
         }
@@ -326,7 +367,8 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_tiled256_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
-    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M) {
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
+    const float* __restrict__ rs) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 65536];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 2, wc = wave & 3;
@@ -406,19 +448,20 @@ __global__ __launch_bounds__(512) void gemm_tiled256_kernel(
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wr * 128 + mt * 16 + 4 * (lane >> 4) + r;
       if (row >= M) continue;
+      const float sc = rs ? rs[row] : 1.0f;  // folded RMSNorm row scale
       if constexpr (EPI == EPI_SILU) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
           const int col = n0 + wc * 32 + nt * 16 + (lane & 15);
-          const float gg = rbf(acc[mt][nt][r]);
-          const float uu = rbf(acc[mt][nt + 2][r]);
+          const float gg = rbf(acc[mt][nt][r] * sc);
+          const float uu = rbf(acc[mt][nt + 2][r] * sc);
           C[(int64_t)row * ldc + col] = f2bf(rbf(silu_f(gg)) * uu);
         }
       } else {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
-          float o = acc[mt][nt][r];
+          float o = acc[mt][nt][r] * sc;
           if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(R[(int64_t)row * ldr + col]);
           C[(int64_t)row * ldc + col] = f2bf(o);
         }
@@ -444,22 +487,28 @@ bool gemm_uses_tiled(int M, int N, int K, int epi) {
 }
 
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
-                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s) {
+                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
+                 const RowNorm* norm) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
+  const float* rs = nullptr;
+  if (norm && gemm_uses_tiled(M, N, K, epi)) {
+    launch_row_inv_rms(A, lda, M, K, norm->eps, norm->rs_ws, s);
+    rs = norm->rs_ws;
+  }
   if (gemm_uses_tiled(M, N, K, epi) && use_tiled256(M, N, epi)) {
     const int ncols = (epi == EPI_SILU) ? 128 : 256;
     dim3 g(N / ncols, (M + 255) / 256);
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
     switch (epi) {
       case EPI_NONE:
-        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_NONE>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_NONE>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
         break;
       case EPI_RESID:
-        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_RESID>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_RESID>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
         break;
       default:
-        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_SILU>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_SILU>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
         break;
     }
     return;
@@ -470,13 +519,13 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
     switch (epi) {
       case EPI_NONE:
-        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_NONE>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_NONE>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
         break;
       case EPI_RESID:
-        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_RESID>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_RESID>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
         break;
       default:
-        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_SILU>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
+        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_SILU>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
         break;
     }
     return;
@@ -495,11 +544,20 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     a.R = R ? R + (int64_t)m0 * ldr : nullptr;
     a.ldr = ldr;
     a.keys = keys;
-    switch (epi) {
-      case EPI_NONE: decode_mt<EPI_NONE>(a, s); break;
-      case EPI_RESID: decode_mt<EPI_RESID>(a, s); break;
-      case EPI_SILU: decode_mt<EPI_SILU>(a, s); break;
-      default: decode_mt<EPI_ARGMAX>(a, s); break;
+    a.eps = norm ? norm->eps : 0.f;
+    if (norm) {
+      switch (epi) {
+        case EPI_NONE: decode_mt<EPI_NONE, true>(a, s); break;
+        case EPI_SILU: decode_mt<EPI_SILU, true>(a, s); break;
+        default: return;  // the span folds norms into the NONE (qkv) and SILU (gate/up) GEMMs only
+      }
+    } else {
+      switch (epi) {
+        case EPI_NONE: decode_mt<EPI_NONE, false>(a, s); break;
+        case EPI_RESID: decode_mt<EPI_RESID, false>(a, s); break;
+        case EPI_SILU: decode_mt<EPI_SILU, false>(a, s); break;
+        default: decode_mt<EPI_ARGMAX, false>(a, s); break;
+      }
     }
     if (epi == EPI_ARGMAX) break;  // argmax requires M <= 64 (checked by the caller)
   }

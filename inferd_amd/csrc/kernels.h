@@ -15,7 +15,8 @@ enum GemmEpilogue {
 
 // elementwise.hip
 void launch_weightgen(u16* dst, int64_t n, uint64_t key, float scale, float center, hipStream_t s);
-void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s);
+// colscale (optional, bf16 [K]): packs bf16(W[n][k] * colscale[k]) (a folded RMSNorm weight)
+void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s, const u16* colscale = nullptr);
 void launch_unpack(const u16* src, int N, int K, u16* dst, hipStream_t s);
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
                     u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s);
@@ -34,8 +35,19 @@ void launch_decode_advance(int32_t* positions, int32_t* slots, int32_t* ctx_lens
 // packed weight holds 2N rows ([gate; up]).  For EPI_ARGMAX `partial` receives
 // (N/16) x M keys and `amax_keys` the per-row reduction (M <= 64).
 bool gemm_uses_tiled(int M, int N, int K, int epi);
+// Folded RMSNorm (epi NONE / SILU): Wp was packed with the norm weight folded in
+// (W[n][k] * w[k]); the GEMM reads the RAW activations and scales each output row by
+// rsqrt(mean(A_row^2) + eps) -- computed in-kernel from the A fragments on the decode path,
+// by a row kernel into rs_ws [M] floats on the tiled (prefill) path.
+struct RowNorm {
+  float eps;
+  float* rs_ws;
+};
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
-                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s);
+                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
+                 const RowNorm* norm = nullptr);
+// rs[row] = 1 / sqrt(mean(x[row][:K]^2) + eps)
+void launch_row_inv_rms(const u16* x, int64_t ldx, int M, int K, float eps, float* rs, hipStream_t s);
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
                           int32_t* ids, hipStream_t s);
 

@@ -56,7 +56,12 @@ struct LayerW {
   u16* post_ln = nullptr;
   u16* q_norm = nullptr;
   u16* k_norm = nullptr;
+  // The RMSNorm weights are folded into the packed projections that consume them
+  // (in_ln -> q/k/v, post_ln -> gate/up; see gemm.hip RowNorm).  A projection packed
+  // before its norm weight was (re)set is stale: forward refuses to run.
+  uint32_t stale = 0;
 };
+enum { STALE_Q = 1, STALE_K = 2, STALE_V = 4, STALE_GATE = 8, STALE_UP = 16 };
 
 // tensor ids shared with oracle/weightgen.py
 enum { T_Q = 0, T_K, T_V, T_O, T_QN, T_KN, T_INLN, T_POSTLN, T_GATE, T_UP, T_DOWN };
@@ -88,6 +93,7 @@ struct InferdSpan {
       *last = nullptr;
   float* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
+  float* rs_ws = nullptr;  // folded-norm row scales of the prefill GEMMs [max_tokens]
   unsigned long long* argmax_partial = nullptr;
   int32_t* err = nullptr;
   std::vector<void*> allocs;
@@ -207,6 +213,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
+  SALLOC(s->rs_ws, (size_t)c.max_tokens * 4);
   SALLOC(s->err, 256);
   if (hipMemset(s->err, 0, 4) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(INFERD_ERR_HIP, "init sync failed"));
@@ -224,6 +231,9 @@ struct Target {
   int packed;     // 1: fragment-pack at n-tile offset
   int64_t rows, cols;
   uint32_t tid_idx;
+  const u16* fold = nullptr;  // norm weight folded into this projection at pack time
+  uint32_t stale_bit = 0;     // this projection's STALE_* bit
+  uint32_t marks = 0;         // a norm weight: projections it makes stale
 };
 
 int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
@@ -238,17 +248,17 @@ int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
   if (layer >= c.n_layers) return fail(INFERD_ERR_ARG, "layer index out of span");
   LayerW& L = s->layers[layer];
   const int64_t qrows = (int64_t)H * HEAD_DIM, kvrows = (int64_t)KV * HEAD_DIM;
-  if (!strcmp(name, "q_proj")) { *t = {L.qkv, 1, qrows, h, T_Q}; return 0; }
-  if (!strcmp(name, "k_proj")) { *t = {L.qkv + qrows * h, 1, kvrows, h, T_K}; return 0; }
-  if (!strcmp(name, "v_proj")) { *t = {L.qkv + (qrows + kvrows) * h, 1, kvrows, h, T_V}; return 0; }
+  if (!strcmp(name, "q_proj")) { *t = {L.qkv, 1, qrows, h, T_Q, L.in_ln, STALE_Q}; return 0; }
+  if (!strcmp(name, "k_proj")) { *t = {L.qkv + qrows * h, 1, kvrows, h, T_K, L.in_ln, STALE_K}; return 0; }
+  if (!strcmp(name, "v_proj")) { *t = {L.qkv + (qrows + kvrows) * h, 1, kvrows, h, T_V, L.in_ln, STALE_V}; return 0; }
   if (!strcmp(name, "o_proj")) { *t = {L.o, 1, h, qrows, T_O}; return 0; }
-  if (!strcmp(name, "gate_proj")) { *t = {L.gateup, 1, I, h, T_GATE}; return 0; }
-  if (!strcmp(name, "up_proj")) { *t = {L.gateup + (int64_t)I * h, 1, I, h, T_UP}; return 0; }
+  if (!strcmp(name, "gate_proj")) { *t = {L.gateup, 1, I, h, T_GATE, L.post_ln, STALE_GATE}; return 0; }
+  if (!strcmp(name, "up_proj")) { *t = {L.gateup + (int64_t)I * h, 1, I, h, T_UP, L.post_ln, STALE_UP}; return 0; }
   if (!strcmp(name, "down_proj")) { *t = {L.down, 1, h, I, T_DOWN}; return 0; }
   if (!strcmp(name, "q_norm")) { *t = {L.q_norm, 0, 1, HEAD_DIM, T_QN}; return 0; }
   if (!strcmp(name, "k_norm")) { *t = {L.k_norm, 0, 1, HEAD_DIM, T_KN}; return 0; }
-  if (!strcmp(name, "input_layernorm")) { *t = {L.in_ln, 0, 1, h, T_INLN}; return 0; }
-  if (!strcmp(name, "post_attention_layernorm")) { *t = {L.post_ln, 0, 1, h, T_POSTLN}; return 0; }
+  if (!strcmp(name, "input_layernorm")) { *t = {L.in_ln, 0, 1, h, T_INLN, nullptr, 0, STALE_Q | STALE_K | STALE_V}; return 0; }
+  if (!strcmp(name, "post_attention_layernorm")) { *t = {L.post_ln, 0, 1, h, T_POSTLN, nullptr, 0, STALE_GATE | STALE_UP}; return 0; }
   return fail(INFERD_ERR_ARG, std::string("unknown layer weight ") + name);
 }
 // packed sub-blocks start at an n-tile boundary: offset rows*K elements == (rows/16)*KT*512
@@ -264,10 +274,14 @@ extern "C" int inferd_span_set_weight(InferdSpan* s, int32_t layer, const char* 
                                     std::to_string(t.rows) + "x" + std::to_string(t.cols));
   hipStream_t st = (hipStream_t)stream;
   if (t.packed)
-    launch_pack((const u16*)src, cols, (int)rows, (int)cols, t.dst, st);
+    launch_pack((const u16*)src, cols, (int)rows, (int)cols, t.dst, st, t.fold);
   else
     HIP_TRY(hipMemcpyAsync(t.dst, src, rows * cols * 2, hipMemcpyDeviceToDevice, st));
   LAUNCH_CHECK();
+  if (layer >= 0) {
+    LayerW& L = s->layers[layer];
+    L.stale = (L.stale | t.marks) & ~t.stale_bit;
+  }
   return INFERD_OK;
 }
 
@@ -280,9 +294,10 @@ extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* st
   if (c.has_lm_head && (int64_t)c.vocab * c.hidden > biggest) biggest = (int64_t)c.vocab * c.hidden;
   u16* tmp = nullptr;
   HIP_TRY(hipMalloc((void**)&tmp, biggest * 2));
-  static const char* layer_names[] = {"q_proj", "k_proj", "v_proj", "o_proj", "q_norm", "k_norm",
-                                      "input_layernorm", "post_attention_layernorm", "gate_proj",
-                                      "up_proj", "down_proj"};
+  // norm weights first: they are folded into the projections packed after them
+  static const char* layer_names[] = {"input_layernorm", "post_attention_layernorm", "q_norm", "k_norm",
+                                      "q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj",
+                                      "down_proj"};
   auto gen = [&](int layer, const char* name) -> int {
     Target t;
     if (resolve(s, layer, name, &t)) return INFERD_ERR_ARG;
@@ -294,10 +309,11 @@ extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* st
     const int64_t n = t.rows * t.cols;
     if (t.packed) {
       launch_weightgen(tmp, n, key, scale, center, st);
-      launch_pack(tmp, t.cols, (int)t.rows, (int)t.cols, t.dst, st);
+      launch_pack(tmp, t.cols, (int)t.rows, (int)t.cols, t.dst, st, t.fold);
     } else {
       launch_weightgen(t.dst, n, key, scale, center, st);
     }
+    if (layer >= 0) s->layers[layer].stale = (s->layers[layer].stale | t.marks) & ~t.stale_bit;
     return INFERD_OK;
   };
   int rc = 0;
@@ -368,15 +384,20 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   if (c.n_layers == 0 && x_out && x != x_out)
     HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
   const AttnBatch ab = to_attn(b);
+  for (int l = 0; l < c.n_layers; ++l)
+    if (s->layers[l].stale)
+      return fail(INFERD_ERR_STATE, "layer " + std::to_string(l) +
+                                        ": a projection was packed before its RMSNorm weight was set "
+                                        "(set input_layernorm / post_attention_layernorm first, then re-set "
+                                        "q/k/v_proj / gate/up_proj)");
+  // input_layernorm and post_attention_layernorm are folded into the qkv and gate/up GEMMs
+  const RowNorm rn = {c.rms_eps, s->rs_ws};
   long pe = -1;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
     u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
-    pe = s->prof_begin(PROF_NORM, st);
-    launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
-    s->prof_end(pe, st);
     pe = s->prof_begin(PROF_QKV, st);
-    launch_gemm(s->xn, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st);
+    launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &rn);
     s->prof_end(pe, st);
     pe = s->prof_begin(PROF_ROPE, st);
     launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
@@ -392,11 +413,8 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pe = s->prof_begin(PROF_O, st);
     launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);
     s->prof_end(pe, st);
-    pe = s->prof_begin(PROF_NORM, st);
-    launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
-    s->prof_end(pe, st);
     pe = s->prof_begin(PROF_GATEUP, st);
-    launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st);
+    launch_gemm(s->h, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, &rn);
     s->prof_end(pe, st);
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
     pe = s->prof_begin(PROF_DOWN, st);
@@ -439,8 +457,7 @@ extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, in
   if (!stream) return fail(INFERD_ERR_ARG, "graph capture needs a non-null stream");
   if (advance && !b->decode) return fail(INFERD_ERR_ARG, "advance needs a decode batch");
   hipStream_t st = (hipStream_t)stream;
-  // with profiling on, the per-kernel-class event pairs are captured as graph nodes
-  // (inferd_span_profile_collect reads them after each replay)
+  s->prof_on = false;  // event pairs are timed eagerly only (HIP cannot time captured events)
   HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
   int rc = INFERD_OK;
   if (advance)
@@ -510,29 +527,6 @@ extern "C" int inferd_span_profile_stop(InferdSpan* s, double* total_ms, int32_t
     }
   }
   s->prof_used = 0;
-  return INFERD_OK;
-}
-
-extern "C" int inferd_span_profile_pairs(InferdSpan* s, int32_t* n_pairs) {
-  if (!s || !n_pairs) return fail(INFERD_ERR_ARG, "null argument");
-  *n_pairs = (int32_t)(s->prof_used / 2);
-  return INFERD_OK;
-}
-
-extern "C" int inferd_span_profile_collect(InferdSpan* s, int32_t first_pair, int32_t n_pairs, double* total_ms,
-                                           int32_t* counts, int32_t n_classes) {
-  if (!s || first_pair < 0 || n_pairs < 0 || (size_t)(first_pair + n_pairs) * 2 > s->prof_used)
-    return fail(INFERD_ERR_ARG, "bad profile pair range");
-  for (int32_t k = first_pair; k < first_pair + n_pairs; ++k) {
-    HIP_TRY(hipEventSynchronize(s->prof_events[2 * k + 1]));
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, s->prof_events[2 * k], s->prof_events[2 * k + 1]));
-    const int c = s->prof_class[k];
-    if (c >= 0 && c < n_classes) {
-      total_ms[c] += ms;
-      counts[c] += 1;
-    }
-  }
   return INFERD_OK;
 }
 

@@ -166,7 +166,8 @@ def load_stage(parts_path: str, model_name: str, num_stages: int, stage: int, de
         start, end = int(meta["start_layer"]), int(meta["end_layer"])
         first, last = meta["first"] == "1", meta["last"] == "1"
         span = SpanRuntime(dims, start, end - start + 1, has_embed=first, has_lm_head=last, device=device)
-        for key in f.keys():
+        # norm weights first: the span folds them into the projections packed after them
+        for key in sorted(f.keys(), key=lambda k: 0 if k.endswith("norm.weight") else 1):
             t = f.get_tensor(key)
             if key.startswith("layers."):
                 _, j, *rest = key.split(".")

@@ -57,26 +57,22 @@ class SpanExecutor:
         self.graphs[m].launch()
 
     def profile_decode(self, microbatches, bufs, n_steps):
-        """Per-kernel-class timings of the decode graphs as they run in the timed loop:
-        one decode graph per microbatch is captured with the span's event pairs inside
-        (HIP event-record nodes around every kernel class), replayed n_steps times, and the
-        pair times are summed after every replay.  Returns {kernel class: (total ms, launches)}."""
-        span = self.span
-        span.profile_start(4096)
-        graphs, ranges = [], []
-        for m, sessions in enumerate(microbatches):
-            p0 = span.profile_pairs()
-            graphs.append(DecodeGraph(span, sessions, n_steps, **bufs[m]))
-            ranges.append((p0, span.profile_pairs() - p0))
-        acc = {}
+        """Eager (non-graph) decode steps with per-kernel-class HIP events on the launch
+        stream, for kernel timings (HIP cannot time event-record nodes inside a replayed
+        graph: hipEventElapsedTime rejects them).  Returns {kernel class: (total ms, launches)}."""
+        self.span.profile_start(1 << 17)
         for _ in range(n_steps):
-            for g, (p0, n) in zip(graphs, ranges):
-                g.launch()
-                span.profile_collect(p0, n, acc)
+            for m, sessions in enumerate(microbatches):
+                states = [self.span.reserve(sid, 1) for sid in sessions]
+                batch, keep = build_batch([(st, 1) for st in states], self.device)
+                b = bufs[m]
+                self.span.run(batch, ids=b.get("ids"), x=b.get("x"), hidden=b.get("hidden_out"),
+                              next_ids=b.get("next_ids"))
+                for st in states:
+                    st.length += 1
+                del keep
         torch.cuda.synchronize(self.device)
-        del graphs
-        span.profile_stop()
-        return {k: (v[0], v[1]) for k, v in acc.items()}
+        return self.span.profile_stop()
 
 
 class PipelineStage:
@@ -236,7 +232,7 @@ class PipelineStage:
         self.step_base += n_steps
 
     def profile_decode(self, n_steps: int):
-        """Per-kernel timings from event-instrumented decode-graph replays on this stage,
+        """Per-kernel timings from eager (event-instrumented) decode steps on this stage,
         without exchanges (kernel durations do not depend on where inputs came from)."""
         return self.ex.profile_decode(self.sessions, [self._bufs(m) for m in range(self.n_mb)], n_steps)
 

@@ -203,9 +203,11 @@ class SpanRuntime:
         torch.cuda.current_stream(self.device).synchronize()
 
     def load_layer_state_dict(self, layer: int, sd: dict):
-        """Keys as in Qwen3DecoderLayer (qwen3_server_module.py:165-176): self_attn.q_proj.weight ..."""
-        for k, v in sd.items():
-            leaf = k.split(".")[-2] if k.endswith(".weight") else k
+        """Keys as in Qwen3DecoderLayer (qwen3_server_module.py:165-176): self_attn.q_proj.weight ...
+        Norm weights are set first: the span folds them into the projections packed after."""
+        items = [(k.split(".")[-2] if k.endswith(".weight") else k, v) for k, v in sd.items()]
+        items.sort(key=lambda kv: 0 if kv[0].endswith("norm") else 1)
+        for leaf, v in items:
             self.set_weight(layer, leaf, v)
 
     # ----------------------------------------------------------------- sessions
@@ -245,25 +247,6 @@ class SpanRuntime:
         cnt = (C.c_int32 * n)()
         _lib.check(self.lib.inferd_span_profile_stop(self.handle, ms, cnt, n))
         return {name: (ms[i], cnt[i]) for i, name in enumerate(_lib.PROF_CLASSES)}
-
-    def profile_pairs(self) -> int:
-        import ctypes as C
-        n = C.c_int32()
-        _lib.check(self.lib.inferd_span_profile_pairs(self.handle, C.byref(n)))
-        return n.value
-
-    def profile_collect(self, first: int, count: int, acc: dict):
-        """Add the elapsed times of event pairs [first, first+count) into acc {class: [ms, n]}."""
-        import ctypes as C
-        n = len(_lib.PROF_CLASSES)
-        ms = (C.c_double * n)()
-        cnt = (C.c_int32 * n)()
-        _lib.check(self.lib.inferd_span_profile_collect(self.handle, first, count, ms, cnt, n))
-        for i, name in enumerate(_lib.PROF_CLASSES):
-            if cnt[i]:
-                a = acc.setdefault(name, [0.0, 0])
-                a[0] += ms[i]
-                a[1] += cnt[i]
 
     def reserve(self, session_id, n_tokens: int) -> SeqState:
         """Make sure `session_id` has pages for n_tokens more tokens (no forward)."""

@@ -192,3 +192,23 @@ def test_q06_full_model_greedy_cached():
         out = s.forward([("s", 1)], ids=nxt, want_next_ids=True, want_logits=True, want_hidden=False)
     agree = sum(a == b for a, b in zip(gpu_tokens, ref_tokens))
     print(f"greedy agreement {agree}/{len(gpu_tokens)}")
+
+
+def test_norm_fold_order_enforced():
+    """The RMSNorm weights are folded into q/k/v and gate/up at pack time: re-setting a norm
+    weight after its projections leaves them stale and forward must refuse (no silent use of
+    the old fold); re-setting the projections restores the exact synthetic span."""
+    from inferd_amd import _lib
+    s = span("tiny", 0, 1, True, False)
+    ids = torch.arange(8, dtype=torch.int32)
+    ref = s.forward([(None, 8)], ids=ids)["hidden"]
+    d = s.dims
+    w_in = torch.ones(d.hidden, dtype=torch.bfloat16) * 1.05
+    s.set_weight(0, "input_layernorm", w_in)
+    with pytest.raises(RuntimeError, match="RMSNorm weight"):
+        s.forward([(None, 8)], ids=ids)
+    # restore: synthetic init packs norms first, then the projections
+    s.init_synthetic(SEED)
+    again = s.forward([(None, 8)], ids=ids)["hidden"]
+    assert torch.equal(again.cpu(), ref.cpu())
+    assert _lib.load() is not None
