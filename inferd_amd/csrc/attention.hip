@@ -82,30 +82,33 @@ __device__ __forceinline__ void attend_page(const u16* __restrict__ kblk, const 
 }
 
 // ------------------------------------------------------------------ decode (1 token/seq)
-// Workgroup (chunk, g, b) = 4 waves; wave w attends pages [chunk*4*ppw + w*ppw, +ppw) of
-// sequence b for the n_rep query heads of kv head g; the 4 waves merge through LDS.  A
-// sequence with a single chunk writes its output directly.  Otherwise every chunk stores
-// its unnormalised partial (O, m, l) and the LAST chunk to arrive merges all chunks
-// (fixed chunk order -> deterministic) and resets the counter.  Hand-off per
-// cdna_hip_programming.md §6 Guideline 16 (write-through form): sc1 partial stores -> every
-// wave s_waitcnt vmcnt(0) -> barrier -> lane 0 relaxed agent fetch_add; the last arriver:
-// agent acquire fence + vmcnt(0) + barrier -> plain loads.
-// The merge is parallel: per-chunk scale factors first (LDS), then independent loads.
+// Workgroup (chunk, g, b) = NW waves over chunk `chunk` of the nc even page ranges of
+// sequence b, for the n_rep query heads of kv head g; pages are interleaved over the waves
+// (wave w: pages p0+w, p0+w+NW, ...).  Each wave runs a K/V software pipeline: K(i+1) is
+// issued as soon as S(i) has consumed K(i), V(i+1) as soon as O += V(i) P(i) has consumed
+// V(i), so one 16 KiB half-page per wave is always in flight (sched_barrier keeps the
+// compiler from sinking the loads).  The NW waves merge through LDS.  A sequence with a
+// single chunk writes its output directly.  Otherwise every chunk stores its unnormalised
+// partial (O, m, l) and the LAST chunk to arrive merges all chunks (fixed chunk order ->
+// deterministic) and resets the counter.  Hand-off per cdna_hip_programming.md §6
+// Guideline 16 (write-through form): sc1 partial stores -> every wave s_waitcnt vmcnt(0) ->
+// barrier -> lane 0 relaxed agent fetch_add; the last arriver: agent acquire fence +
+// vmcnt(0) + barrier -> plain loads, all issued in parallel (no load inside a serial loop).
+// Shape (NW, nc): tools/attn_lab.hip sweeps -- few long-running workgroups win; the launcher
+// aims at ~2048 waves in total with >= 4 pages per workgroup.
 // Workspace: [DECODE_COUNTER_BYTES of u32 counters | partials, PART_STRIDE f32 per head].
 #define PART_STRIDE (HEAD_DIM + 4)
 #define DECODE_COUNTER_BYTES 65536   // B * KV <= 16384; zero before first use, left zero
 #define MAX_DECODE_CHUNKS 64
 
-__global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict__ q,
-                                                          const u16* __restrict__ kv, AttnBatch b,
-                                                          int H, int KV, int ppw, float scale_log2,
-                                                          int n_chunks_max,
-                                                          unsigned* __restrict__ counters,
-                                                          float* __restrict__ part,
-                                                          u16* __restrict__ out) {
-  __shared__ float sm_m[4][16], sm_l[4][16];
-  __shared__ float sm_o[4][16][HEAD_DIM + 4];
-  __shared__ float sm_f[MAX_DECODE_CHUNKS][16];
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restrict__ q, const u16* __restrict__ kv,
+                                                      AttnBatch b, int H, int KV, int nc_req, float scale_log2,
+                                                      int n_chunks_max, unsigned* __restrict__ counters,
+                                                      float* __restrict__ part, u16* __restrict__ out) {
+  __shared__ float sm_m[NW][16], sm_l[NW][16];
+  __shared__ float sm_o[NW][16][HEAD_DIM + 4];
+  __shared__ float sm_f[MAX_DECODE_CHUNKS][16], sm_lc[MAX_DECODE_CHUNKS][16];
   __shared__ float sm_L[16];
   __shared__ int sm_last;
   const int chunk = blockIdx.x, g = blockIdx.y, bseq = blockIdx.z;
@@ -113,34 +116,111 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict_
   const int n_rep = H / KV;
   const int ctx = b.ctx_lens[bseq];
   const int n_pages = (ctx + KV_PAGE - 1) / KV_PAGE;
-  const int cp = 4 * ppw;
-  const int nc = (n_pages + cp - 1) / cp;
-  if (chunk >= nc) return;  // uniform over the workgroup
+  const int nc = min(nc_req, n_pages);
+  if (chunk >= nc) return;
+  const int cp0 = (chunk * n_pages) / nc, cp1 = ((chunk + 1) * n_pages) / nc;
   const int tok = b.seq_start[bseq + 1] - 1;
   const int hn = lane & 15;
   bf16x8 qf[4];
-  if (hn < n_rep) {
-    const u16* qp = q + ((int64_t)tok * H + g * n_rep + hn) * HEAD_DIM + 8 * (lane >> 4);
+  {
+    const int hh = hn < n_rep ? hn : 0;
+    const u16* qp = q + ((int64_t)tok * H + g * n_rep + hh) * HEAD_DIM + 8 * (lane >> 4);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const bf16x8*)(qp + ks * 32);
-  } else {
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[ks] = as_bf16x8(u16x8{0, 0, 0, 0, 0, 0, 0, 0});
   }
   float m_i = -INFINITY, l_i = 0.f;
   f32x4 o[8];
 #pragma unroll
   for (int db = 0; db < 8; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
-  const int p0 = chunk * cp + wave * ppw;
-  const int p1 = min(n_pages, p0 + ppw);
-  for (int pi = p0; pi < p1; ++pi) {
-    const int phys = bt[pi];
-    const u16* kblk = kv + ((int64_t)(phys * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
-    const u16* vblk = kv + ((int64_t)(phys * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
-    attend_page(kblk, vblk, qf, pi * KV_PAGE, ctx - 1, scale_log2, m_i, l_i, o, lane);
+  const int lim = ctx - 1;
+  int pi = cp0 + wave;
+  if (pi < cp1) {
+    bf16x8 kf[16], vf[16];
+    auto kaddr = [&](int p) {
+      return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 0) * KV + g) * KV_BLOCK_ELEMS) + lane;
+    };
+    auto vaddr = [&](int p) {
+      return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 1) * KV + g) * KV_BLOCK_ELEMS) + lane;
+    };
+    {
+      const bf16x8* kb = kaddr(pi);
+      const bf16x8* vb = vaddr(pi);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) kf[i] = __builtin_nontemporal_load(kb + i * 64);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) vf[i] = __builtin_nontemporal_load(vb + i * 64);
+    }
+    for (;;) {
+      const int nxt = pi + NW;
+      const bool more = nxt < cp1;
+      const int page_tok0 = pi * KV_PAGE;
+      f32x4 sc[4];
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb) {
+        sc[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) sc[tb] = mfma16(kf[tb * 4 + ks], qf[ks], sc[tb]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) {
+        const bf16x8* kb = kaddr(nxt);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) kf[i] = __builtin_nontemporal_load(kb + i * 64);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      float pmax = -INFINITY;
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
+          const float s = (t <= lim) ? sc[tb][r] * scale_log2 : -INFINITY;
+          sc[tb][r] = s;
+          pmax = fmaxf(pmax, s);
+        }
+      pmax = fmaxf(pmax, __shfl_xor(pmax, 16));
+      pmax = fmaxf(pmax, __shfl_xor(pmax, 32));
+      const float m_new = fmaxf(m_i, pmax);
+      const float alpha = exp2f(m_i - m_new);
+      float psum = 0.f;
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(sc[tb][r] - m_new);
+          sc[tb][r] = p;
+          psum += p;
+        }
+      psum += __shfl_xor(psum, 16);
+      psum += __shfl_xor(psum, 32);
+      l_i = l_i * alpha + psum;
+      m_i = m_new;
+#pragma unroll
+      for (int db = 0; db < 8; ++db) o[db] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pf[j] = (__bf16)sc[2 * kt][j];
+          pf[4 + j] = (__bf16)sc[2 * kt + 1][j];
+        }
+#pragma unroll
+        for (int db = 0; db < 8; ++db) o[db] = mfma16(vf[kt * 8 + db], pf, o[db]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (!more) break;
+      {
+        const bf16x8* vb = vaddr(nxt);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) vf[i] = __builtin_nontemporal_load(vb + i * 64);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      pi = nxt;
+    }
   }
-  // merge the 4 waves of this chunk through LDS
+  // merge the 4 waves through LDS (as attn_decode_kernel)
   if (lane < 16) {
     sm_m[wave][lane] = m_i;
     sm_l[wave][lane] = l_i;
@@ -153,20 +233,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict_
   u16* op = out + (int64_t)tok * H * HEAD_DIM + (int64_t)g * n_rep * HEAD_DIM;
   const int stride = n_rep * PART_STRIDE;
   float* base = part + ((int64_t)bseq * KV + g) * n_chunks_max * stride;
-  for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += 256) {
+  for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += NW * 64) {
     const int n = idx / HEAD_DIM, d = idx % HEAD_DIM;
-    const float M = fmaxf(fmaxf(sm_m[0][n], sm_m[1][n]), fmaxf(sm_m[2][n], sm_m[3][n]));
+    float M = sm_m[0][n];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) M = fmaxf(M, sm_m[w][n]);
     float acc = 0.f, L = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const float f = exp2f(sm_m[w][n] - M);
+    for (int w = 0; w < NW; ++w) {
+      const float f = (sm_m[w][n] == -INFINITY) ? 0.f : exp2f(sm_m[w][n] - M);
       acc += sm_o[w][n][d] * f;
       L += sm_l[w][n] * f;
     }
     if (nc == 1) {
       op[n * HEAD_DIM + d] = f2bf(acc / L);
     } else {
-      // write-through (sc1) partial stores: visible chip-wide once drained, no release fence
       float* pc = base + (int64_t)chunk * stride + n * PART_STRIDE;
       __hip_atomic_store(pc + d, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (d == 0) {
@@ -176,7 +257,6 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict_
     }
   }
   if (nc == 1) return;
-  // publish the partial (every storing wave drains, then one ticket); the last chunk merges
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -191,10 +271,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict_
   }
   __syncthreads();
   if (!sm_last) return;
-  // per-chunk scale factors f[c][n] = 2^(m_c - M_n) and the normaliser L_n
-  for (int idx = threadIdx.x; idx < nc * n_rep; idx += 256) {
+  for (int idx = threadIdx.x; idx < nc * n_rep; idx += NW * 64) {
     const int c = idx / n_rep, n = idx % n_rep;
     sm_f[c][n] = base[(int64_t)c * stride + n * PART_STRIDE + HEAD_DIM];
+    sm_lc[c][n] = base[(int64_t)c * stride + n * PART_STRIDE + HEAD_DIM + 1];
   }
   __syncthreads();
   if (threadIdx.x < n_rep) {
@@ -205,35 +285,40 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const u16* __restrict_
     for (int c = 0; c < nc; ++c) {
       const float f = exp2f(sm_f[c][n] - M);
       sm_f[c][n] = f;
-      L += base[(int64_t)c * stride + n * PART_STRIDE + HEAD_DIM + 1] * f;
+      L += sm_lc[c][n] * f;
     }
     sm_L[n] = L;
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += 256) {
+  for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += NW * 64) {
     const int n = idx / HEAD_DIM, d = idx % HEAD_DIM;
     const float* pc = base + n * PART_STRIDE + d;
     float acc = 0.f;
-#pragma unroll 8
+#pragma unroll 16
     for (int c = 0; c < nc; ++c) acc += pc[(int64_t)c * stride] * sm_f[c][n];
     op[n * HEAD_DIM + d] = f2bf(acc / sm_L[n]);
   }
 }
 
-static int decode_ppw(int B, int KV, int max_ctx) {
-  static int env = -2;
-  if (env == -2) {
-    const char* e = getenv("INFERD_DECODE_PPW");
-    env = e ? atoi(e) : -1;
-  }
-  const int n_pages = (max_ctx + KV_PAGE - 1) / KV_PAGE;
-  // ~2 four-wave workgroups per CU (512) over the (seq, kv-head, page) stream: measured on
-  // B=16 x 2.1k ctx x 8 kv heads, 1 page/wave 31.8 us, 2: 29.9, 4: 28.2, 8: 33.7
-  int ppw = env > 0 ? env : (B * KV * n_pages + 4 * 512 - 1) / (4 * 512);
-  if (ppw < 1) ppw = 1;
-  // chunks of 4*ppw pages; at most MAX_DECODE_CHUNKS chunks per sequence
-  const int min_ppw = (n_pages + 4 * MAX_DECODE_CHUNKS - 1) / (4 * MAX_DECODE_CHUNKS);
-  return ppw < min_ppw ? min_ppw : ppw;
+static int env_int(const char* name) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : 0;
+}
+
+// (waves per workgroup, chunks per (seq, kv head)) for a decode batch
+static void decode_shape(int B, int KV, int max_ctx, int* nw, int* nc) {
+  static const int env_nw = env_int("INFERD_ATTN_NW"), env_nc = env_int("INFERD_ATTN_NC");
+  const int np = (max_ctx + KV_PAGE - 1) / KV_PAGE;
+  const int S = B * KV;
+  int w = (S * 8 <= 2048 && np < 96) ? 8 : 4;
+  if (env_nw == 4 || env_nw == 8) w = env_nw;
+  int c = 2048 / (S * w);
+  const int cmax = np / 4 > 1 ? np / 4 : 1;
+  c = c < 1 ? 1 : (c > cmax ? cmax : c);
+  if (env_nc > 0) c = env_nc;
+  if (c > MAX_DECODE_CHUNKS) c = MAX_DECODE_CHUNKS;
+  *nw = w;
+  *nc = c;
 }
 
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx) {
@@ -241,15 +326,23 @@ size_t attn_decode_ws_bytes(int B, int H, int max_ctx) {
   return DECODE_COUNTER_BYTES + (size_t)B * H * MAX_DECODE_CHUNKS * PART_STRIDE * sizeof(float);
 }
 
-void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
-                        float scale, u16* out, float* ws, hipStream_t s) {
-  const int ppw = decode_ppw(b.B, KV, b.max_ctx);
-  const int n_pages = (b.max_ctx + KV_PAGE - 1) / KV_PAGE;
-  const int n_chunks = (n_pages + 4 * ppw - 1) / (4 * ppw);
+void launch_attn_decode_shape(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale,
+                              u16* out, float* ws, hipStream_t s, int nw, int nc) {
   unsigned* counters = (unsigned*)ws;
   float* part = (float*)((char*)ws + DECODE_COUNTER_BYTES);
-  hipLaunchKernelGGL(attn_decode_kernel, dim3(n_chunks, KV, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, ppw,
-                     scale * LOG2E, n_chunks, counters, part, out);
+  if (nw == 8)
+    hipLaunchKernelGGL(attn_decode_kernel<8>, dim3(nc, KV, b.B), dim3(512), 0, s, q, kv_layer, b, H, KV, nc,
+                       scale * LOG2E, nc, counters, part, out);
+  else
+    hipLaunchKernelGGL(attn_decode_kernel<4>, dim3(nc, KV, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, nc,
+                       scale * LOG2E, nc, counters, part, out);
+}
+
+void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
+                        float scale, u16* out, float* ws, hipStream_t s) {
+  int nw, nc;
+  decode_shape(b.B, KV, b.max_ctx, &nw, &nc);
+  launch_attn_decode_shape(q, kv_layer, b, H, KV, scale, out, ws, s, nw, nc);
 }
 
 // ------------------------------------------------------------------ prefill (causal)
