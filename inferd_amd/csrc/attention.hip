@@ -19,67 +19,26 @@
 
 #define LOG2E 1.4426950408889634f
 
-// One 64-token page of online-softmax attention for one wave.
-// qf: Q^T fragments (4 k-steps of 32 dims); keys t <= lim are visible (lane-local limit).
-__device__ __forceinline__ void attend_page(const u16* __restrict__ kblk, const u16* __restrict__ vblk,
-                                            const bf16x8 (&qf)[4], int page_tok0, int lim,
-                                            float scale_log2, float& m_i, float& l_i,
-                                            f32x4 (&o)[8], int lane) {
-  const bf16x8* kb = (const bf16x8*)kblk + lane;
-  const bf16x8* vb = (const bf16x8*)vblk + lane;
-  bf16x8 kf[16], vf[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) kf[i] = kb[i * 64];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) vf[i] = vb[i * 64];
-  f32x4 sc[4];
-#pragma unroll
-  for (int tb = 0; tb < 4; ++tb) {
-    sc[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) sc[tb] = mfma16(kf[tb * 4 + ks], qf[ks], sc[tb]);
-  }
-  float pmax = -INFINITY;
-#pragma unroll
-  for (int tb = 0; tb < 4; ++tb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
-      const float s = (t <= lim) ? sc[tb][r] * scale_log2 : -INFINITY;
-      sc[tb][r] = s;
-      pmax = fmaxf(pmax, s);
-    }
-  pmax = fmaxf(pmax, __shfl_xor(pmax, 16));
-  pmax = fmaxf(pmax, __shfl_xor(pmax, 32));
-  const float m_new = fmaxf(m_i, pmax);
-  const float alpha = exp2f(m_i - m_new);
-  float psum = 0.f;
-#pragma unroll
-  for (int tb = 0; tb < 4; ++tb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float p = exp2f(sc[tb][r] - m_new);
-      sc[tb][r] = p;
-      psum += p;
-    }
-  psum += __shfl_xor(psum, 16);
-  psum += __shfl_xor(psum, 32);
-  l_i = l_i * alpha + psum;
-  m_i = m_new;
-#pragma unroll
-  for (int db = 0; db < 8; ++db) o[db] *= alpha;
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    bf16x8 pf;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pf[j] = (__bf16)sc[2 * kt][j];
-      pf[4 + j] = (__bf16)sc[2 * kt + 1][j];
-    }
-#pragma unroll
-    for (int db = 0; db < 8; ++db) o[db] = mfma16(vf[kt * 8 + db], pf, o[db]);
-  }
+// Cross-lane helpers (gfx950 v_permlane{16,32}_swap: one VALU op, no LDS round trip).
+// In the S^T accumulator layout the 4 lanes l, l^16, l^32, l^48 hold the same query.
+__device__ __forceinline__ float max_q4(float v) {
+  const unsigned u = __float_as_uint(v);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  const unsigned w = __float_as_uint(v);
+  auto q = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
 }
+__device__ __forceinline__ float sum_q4(float v) {
+  const unsigned u = __float_as_uint(v);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  const unsigned w = __float_as_uint(v);
+  auto q = __builtin_amdgcn_permlane16_swap(w, w, false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+// bare v_exp_f32 (arguments are <= 0 or -inf here: no range reduction needed)
+__device__ __forceinline__ float exp2_raw(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // ------------------------------------------------------------------ decode (1 token/seq)
 // Workgroup (chunk, g, b) = NW waves over chunk `chunk` of the nc even page ranges of
@@ -169,35 +128,38 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
         for (int i = 0; i < 16; ++i) kf[i] = __builtin_nontemporal_load(kb + i * 64);
       }
       __builtin_amdgcn_sched_barrier(0);
-      float pmax = -INFINITY;
+      if (page_tok0 + KV_PAGE - 1 > lim) {  // the sequence's last page: causal/length mask
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
+            sc[tb][r] = (t <= lim) ? sc[tb][r] : -INFINITY;
+          }
+      }
+      float pmax = sc[0][0];
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (tb | r) pmax = fmaxf(pmax, sc[tb][r]);
+      const float m_new = fmaxf(m_i, max_q4(pmax) * scale_log2);
+      if (__builtin_amdgcn_ballot_w64(m_new > m_i)) {
+        const float alpha = exp2_raw(m_i - m_new);
+        l_i *= alpha;
+#pragma unroll
+        for (int db = 0; db < 8; ++db) o[db] *= alpha;
+        m_i = m_new;
+      }
+      const float mneg = -m_i;
 #pragma unroll
       for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
-          const float s = (t <= lim) ? sc[tb][r] * scale_log2 : -INFINITY;
-          sc[tb][r] = s;
-          pmax = fmaxf(pmax, s);
-        }
-      pmax = fmaxf(pmax, __shfl_xor(pmax, 16));
-      pmax = fmaxf(pmax, __shfl_xor(pmax, 32));
-      const float m_new = fmaxf(m_i, pmax);
-      const float alpha = exp2f(m_i - m_new);
-      float psum = 0.f;
-#pragma unroll
-      for (int tb = 0; tb < 4; ++tb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(sc[tb][r] - m_new);
+          const float p = exp2_raw(fmaf(sc[tb][r], scale_log2, mneg));
           sc[tb][r] = p;
-          psum += p;
+          l_i += p;  // this lane's share; reduced over the query's 4 lanes after the loop
         }
-      psum += __shfl_xor(psum, 16);
-      psum += __shfl_xor(psum, 32);
-      l_i = l_i * alpha + psum;
-      m_i = m_new;
-#pragma unroll
-      for (int db = 0; db < 8; ++db) o[db] *= alpha;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         bf16x8 pf;
@@ -220,7 +182,8 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
       pi = nxt;
     }
   }
-  // merge the 4 waves through LDS (as attn_decode_kernel)
+  // merge the NW waves through LDS
+  l_i = sum_q4(l_i);
   if (lane < 16) {
     sm_m[wave][lane] = m_i;
     sm_l[wave][lane] = l_i;
@@ -354,8 +317,20 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 // lds[tile * 1 KiB + lane * 16] (contiguous, bank-conflict free), and each K/V fragment feeds
 // the MFMAs of both column blocks.  Waves whose rows all precede a page skip its compute but
 // keep the barriers.
+//
+// Softmax VALU per page is the kernel's pole (64 MFMAs vs ~550 VALU ops before), so:
+//  * the causal mask is applied only on pages that cross one of the wave's rows' limits
+//    (wave-uniform test), every other page is mask-free;
+//  * the running max m is kept in log2-scaled units and p = exp2(fma(s, c, -m)) with a bare
+//    v_exp_f32 (arguments are <= 0 / -inf);
+//  * O and l are rescaled only when some row's max actually grew (wave-uniform branch) --
+//    the same values as rescaling by exp2(0) = 1 every page;
+//  * l is kept per lane (each lane's share of its query's row sum) and reduced across the 4
+//    lanes of a query once, at the end;
+//  * row max reductions use v_permlane{32,16}_swap instead of ds_bpermute.
+template <bool MASK>
 __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, const bf16x8 (&qf)[2][4],
-                                                 int page_tok0, const int (&lim)[2], float scale_log2,
+                                                 int page_tok0, const int (&lim)[2], float c,
                                                  float (&m_i)[2], float (&l_i)[2], f32x4 (&o)[2][8], int lane) {
   f32x4 sc[2][4];
 #pragma unroll
@@ -373,35 +348,40 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
   bf16x8 pf[2][2];
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) {
-    float pmax = -INFINITY;
+    if constexpr (MASK) {
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
+          sc[nb][tb][r] = (t <= lim[nb]) ? sc[nb][tb][r] : -INFINITY;
+        }
+    }
+    float pmax = sc[nb][0][0];
 #pragma unroll
     for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
-        const float s = (t <= lim[nb]) ? sc[nb][tb][r] * scale_log2 : -INFINITY;
-        sc[nb][tb][r] = s;
-        pmax = fmaxf(pmax, s);
-      }
-    pmax = fmaxf(pmax, __shfl_xor(pmax, 16));
-    pmax = fmaxf(pmax, __shfl_xor(pmax, 32));
-    const float m_new = fmaxf(m_i[nb], pmax);
-    const float alpha = exp2f(m_i[nb] - m_new);
+      for (int r = 0; r < 4; ++r)
+        if (tb | r) pmax = fmaxf(pmax, sc[nb][tb][r]);
+    const float m_new = fmaxf(m_i[nb], max_q4(pmax) * c);
+    if (__builtin_amdgcn_ballot_w64(m_new > m_i[nb])) {
+      const float alpha = exp2_raw(m_i[nb] - m_new);
+      l_i[nb] *= alpha;
+#pragma unroll
+      for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
+      m_i[nb] = m_new;
+    }
+    const float mneg = -m_i[nb];
     float psum = 0.f;
 #pragma unroll
     for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = exp2f(sc[nb][tb][r] - m_new);
+        const float p = exp2_raw(fmaf(sc[nb][tb][r], c, mneg));
         sc[nb][tb][r] = p;
         psum += p;
       }
-    psum += __shfl_xor(psum, 16);
-    psum += __shfl_xor(psum, 32);
-    l_i[nb] = l_i[nb] * alpha + psum;
-    m_i[nb] = m_new;
-#pragma unroll
-    for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
+    l_i[nb] += psum;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -446,10 +426,14 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
   }
-  // pages: up to the workgroup's last row; a wave computes up to its own last row
+  // pages: up to the workgroup's last row; a wave computes up to its own last row and
+  // masks only pages that reach past its smallest row limit
   const int wg_last = b.positions[t0 + min(qb0 + 127, T - 1)];
   const int wave_first_row = qb0 + wave * 32;
   const int wave_last = wave_first_row < T ? b.positions[t0 + min(wave_first_row + 31, T - 1)] : -1;
+  int wave_min_lim = min(lim[0], lim[1]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wave_min_lim = min(wave_min_lim, __shfl_xor(wave_min_lim, o));
   const int n_pages = wg_last / KV_PAGE + 1;
   const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
   auto stage = [&](int buf, int pi) {
@@ -475,14 +459,17 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   for (int pi = 0; pi < n_pages; ++pi) {
     const int cur = pi & 1;
     if (pi + 1 < n_pages) stage(cur ^ 1, pi + 1);
-    if (pi * KV_PAGE <= wave_last)
-      prefill_page_lds(lds + cur * 32768, qf, pi * KV_PAGE, lim, scale_log2, m_i, l_i, o, lane);
+    const int tok0 = pi * KV_PAGE;
+    if (tok0 + KV_PAGE - 1 <= wave_min_lim)
+      prefill_page_lds<false>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, o, lane);
+    else if (tok0 <= wave_last)
+      prefill_page_lds<true>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, o, lane);
     __syncthreads();  // next page landed (vmcnt(0)) and everyone is done with this buffer
   }
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) {
+    const float inv = 1.0f / sum_q4(l_i[nb]);
     if (!valid[nb]) continue;
-    const float inv = 1.0f / l_i[nb];
     u16* op = out + (int64_t)tokrow[nb] * H * HEAD_DIM + h * HEAD_DIM;
 #pragma unroll
     for (int db = 0; db < 8; ++db) {

@@ -470,13 +470,253 @@ __global__ __launch_bounds__(512) void gemm_tiled256_kernel(
   }
 }
 
-static bool use_tiled256(int M, int N, int epi) {
-  static int env = -1;
-  if (env < 0) {
-    const char* e = getenv("INFERD_GEMM_TILE");
-    env = e ? atoi(e) : 256;
+// ============================================================ ring-staged 256x256 (prefill)
+// Same 256x256x64 block tile and 2 (M) x 4 (N) wave grid as gemm_tiled256, but the
+// staging never drains (cdna_hip_programming.md §5 "Pipelining across barriers"):
+//  * LDS is a ring of 10 half-tile slots of 16 KiB (the whole 160 KiB).  A K-step's
+//    tile is four half-tiles consumed in this order: A0 (rows qr=0 of both wave rows),
+//    B0 (columns qc=0 of every wave column), B1, A1.  Half-tile s lives in slot s % 10.
+//  * One K-step = 4 phases, one per output quadrant of a wave (64 rows x 32 cols, 16
+//    MFMAs): (A0,B0) (A0,B1) (A1,B1) (A1,B0).  Phase P reads its register sub-tiles,
+//    issues half-tile P+6 (2 global_load_lds_dwordx4 per thread), waits with a COUNTED
+//    vmcnt for the half-tile phase P+1 reads (4 half-tiles stay in flight), passes a raw
+//    s_barrier, runs its 16 MFMAs at raised priority and passes a second s_barrier.
+//  * Waves 4-7 run one barrier behind waves 0-3 (each SIMD holds one wave of each half),
+//    so on every SIMD one wave is in its MFMA segment while its partner reads LDS.
+//  * Hazards (derived in DESIGN.md §4): a slot is re-filled only >= 2 phases after its
+//    last read, which bounds the look-ahead to ring - 4 = 6 half-tiles.
+//  * Operands are swapped (C^T = W * A^T) so each lane's 4 accumulator registers are 4
+//    consecutive output columns: the epilogue stores 8 bytes per lane.
+//  * blockIdx is remapped XCD-aware (blocks sharing an XCD get consecutive tiles) and
+//    grouped 8 row-blocks deep so an XCD's concurrent blocks share A rows and W columns.
+#define RING_SLOTS 10
+#define RING_AHEAD 6
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
+    const float* __restrict__ rs, int grid_m, int grid_n) {
+  __shared__ __attribute__((aligned(16))) char lds[RING_SLOTS * 16384];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  // ---- XCD-aware tile order (bijective for any grid size)
+  int bm, bn;
+  {
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    constexpr int GM = 8;
+    const int group = wg / (GM * grid_n);
+    const int first_m = group * GM;
+    const int gsz = min(grid_m - first_m, GM);
+    const int in = wg - group * GM * grid_n;
+    bm = first_m + in % gsz;
+    bn = in / gsz;
   }
-  if (env != 256 || M < 512) return false;
+  const int m0 = bm * 256;
+  const int n0 = bn * ((EPI == EPI_SILU) ? 128 : 256);
+  const int nK = KT / 2;       // 64-deep K-steps
+  const int S = 4 * nK;        // half-tiles
+
+  // ---- staging sources: this wave's two 1 KiB pieces of each half-tile kind
+  const u16* a_src[2][2];      // [half][piece]
+  const u16* b_src[2];         // [half] (the 2 pieces are the 2 consecutive k-tiles)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int qp = 2 * wave + p;                 // piece 0..15: image rows 8qp..8qp+7
+      const int i = 8 * qp + (lane >> 3);          // image row 0..127
+      int grow = m0 + (i >> 6) * 128 + h * 64 + (i & 63);
+      grow = grow < M ? grow : M - 1;
+      const int chunk = (lane & 7) ^ ((i >> 1) & 7);
+      a_src[h][p] = A + (int64_t)grow * lda + chunk * 8;
+    }
+    // image n-tile nl = wave: wave column nl>>1, sub-tile nl&1
+    int gnt;
+    if constexpr (EPI == EPI_SILU)
+      gnt = (h == 0 ? 0 : n_tiles_w / 2) + n0 / 16 + (wave >> 1) * 2 + (wave & 1);
+    else
+      gnt = n0 / 16 + (wave >> 1) * 4 + h * 2 + (wave & 1);
+    b_src[h] = Wp + (int64_t)gnt * KT * 512 + lane * 8;
+  }
+  // kind: 0 = A0, 1 = B0, 2 = B1, 3 = A1 (the consumption order within a K-step)
+  auto issue = [&](int kind, int t, int slot) {
+    char* base = lds + slot * 16384 + wave * 2048;
+    if (kind == 0 || kind == 3) {
+      const int h = kind == 0 ? 0 : 1;
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[h][0] + t * 64), (void*)base, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(a_src[h][1] + t * 64), (void*)(base + 1024), 16, 0, 0);
+    } else {
+      const u16* src = b_src[kind - 1] + (int64_t)t * 1024;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)base, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(src + 512), (void*)(base + 1024), 16, 0, 0);
+    }
+  };
+  auto issue_s = [&](int s) {
+    int slot = s % RING_SLOTS;
+    issue(s & 3, s >> 2, slot);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 areg[4][2], breg[2][2];
+
+  auto read_a = [&](int slot) {
+    const char* base = lds + slot * 16384;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const int i = wr * 64 + mt * 16 + (lane & 15);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = ks * 4 + (lane >> 4);
+        areg[mt][ks] = *(const bf16x8*)(base + i * 128 + 16 * (c ^ ((i >> 1) & 7)));
+      }
+    }
+  };
+  auto read_b = [&](int slot) {
+    const char* base = lds + slot * 16384 + lane * 16;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) breg[nt][ks] = *(const bf16x8*)(base + ((wc * 2 + nt) * 2 + ks) * 1024);
+  };
+  auto mfmas = [&](auto QR, auto QC) {
+    constexpr int qr = decltype(QR)::value, qc = decltype(QC)::value;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt)
+          acc[qr * 4 + mt][qc * 2 + nt] = mfma16(breg[nt][ks], areg[mt][ks], acc[qr * 4 + mt][qc * 2 + nt]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto wrap = [](int x) { return x >= RING_SLOTS ? x - RING_SLOTS : x; };
+
+  // one phase: reads, optional issue of half-tile `s_issue`, counted wait, barrier, MFMAs, barrier
+  auto phase = [&](auto J, int rb, int s_issue, auto VM) {
+    constexpr int j = decltype(J)::value;
+    constexpr int vm = decltype(VM)::value;
+    if constexpr (j == 0) { read_a(rb); read_b(wrap(rb + 1)); }
+    if constexpr (j == 1) read_b(wrap(rb + 2));
+    if constexpr (j == 2) read_a(wrap(rb + 3));
+    if constexpr (j == 3) read_b(wrap(rb + 1));
+    if (s_issue >= 0) issue_s(s_issue);
+    if constexpr (vm >= 0) vm_wait<vm>();
+    raw_barrier();
+    if constexpr (j == 0) mfmas(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    if constexpr (j == 1) mfmas(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+    if constexpr (j == 2) mfmas(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+    if constexpr (j == 3) mfmas(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+    raw_barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using VNONE = std::integral_constant<int, -1>;
+
+  // prologue: half-tiles 0..5 in flight, wait for 0 and 1 (A0, B0 of step 0)
+#pragma unroll
+  for (int s = 0; s < RING_AHEAD; ++s) issue(s & 3, s >> 2, s);
+  vm_wait<8>();
+  raw_barrier();
+  if (wr == 1) raw_barrier();  // stagger: waves 4-7 one barrier behind
+
+  int rb = 0;  // slot of the current step's A0 half-tile = (4t) % 10
+  int t = 0;
+  // steady state: every phase issues, 4 half-tiles stay in flight after each wait
+  for (; t < nK - 2; ++t) {
+    const int s0 = 4 * t + RING_AHEAD;
+    phase(I0{}, rb, s0, std::integral_constant<int, 8>{});
+    phase(I1{}, rb, s0 + 1, std::integral_constant<int, 8>{});
+    phase(I2{}, rb, s0 + 2, std::integral_constant<int, 8>{});
+    phase(I3{}, rb, s0 + 3, std::integral_constant<int, 8>{});
+    rb = wrap(rb + 4);
+  }
+  // step nK-2: issues S-2, S-1 then drains
+  phase(I0{}, rb, S - 2, std::integral_constant<int, 8>{});
+  phase(I1{}, rb, S - 1, std::integral_constant<int, 8>{});
+  phase(I2{}, rb, -1, std::integral_constant<int, 6>{});
+  phase(I3{}, rb, -1, std::integral_constant<int, 4>{});
+  rb = wrap(rb + 4);
+  // step nK-1
+  phase(I0{}, rb, -1, std::integral_constant<int, 2>{});
+  phase(I1{}, rb, -1, std::integral_constant<int, 0>{});
+  phase(I2{}, rb, -1, VNONE{});
+  phase(I3{}, rb, -1, VNONE{});
+  if (wr == 0) raw_barrier();  // close the stagger
+
+  // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + (lane & 15);
+    if (row >= M) continue;
+    const float sc = rs ? rs[row] : 1.0f;  // folded RMSNorm row scale
+    if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = n0 + wc * 32 + nt * 16 + 4 * (lane >> 4);
+        u16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gg = rbf(acc[i][nt][r] * sc);
+          const float uu = rbf(acc[i][2 + nt][r] * sc);
+          v[r] = f2bf(rbf(silu_f(gg)) * uu);
+        }
+        *(u16x4*)(C + (int64_t)row * ldc + col) = v;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + 4 * (lane >> 4);
+        u16x4 v;
+        u16x4 rr;
+        if constexpr (EPI == EPI_RESID) rr = *(const u16x4*)(R + (int64_t)row * ldr + col);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float o = acc[i][j][r] * sc;
+          if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(rr[r]);
+          v[r] = f2bf(o);
+        }
+        *(u16x4*)(C + (int64_t)row * ldc + col) = v;
+      }
+    }
+  }
+}
+
+// INFERD_GEMM_TILE selects the prefill GEMM (read per call so one process can A/B them):
+// "ring" (default) | "256" | "128"
+static int gemm_tile_variant() {
+  const char* e = getenv("INFERD_GEMM_TILE");
+  if (!e || !*e) return 0;
+  if (e[0] == 'r') return 0;
+  return atoi(e);
+}
+
+static bool use_ring256(int M, int N, int K, int epi) {
+  if (gemm_tile_variant() != 0 || M < 512 || K < 192) return false;
+  return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
+}
+
+static bool use_tiled256(int M, int N, int epi) {
+  if (gemm_tile_variant() == 128 || M < 512) return false;
   return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
 }
 
@@ -495,6 +735,26 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
   if (norm && gemm_uses_tiled(M, N, K, epi)) {
     launch_row_inv_rms(A, lda, M, K, norm->eps, norm->rs_ws, s);
     rs = norm->rs_ws;
+  }
+  if (gemm_uses_tiled(M, N, K, epi) && use_ring256(M, N, K, epi)) {
+    const int ncols = (epi == EPI_SILU) ? 128 : 256;
+    const int gm = (M + 255) / 256, gn = N / ncols;
+    const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
+    switch (epi) {
+      case EPI_NONE:
+        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_NONE>, dim3(gm * gn), dim3(512), 0, s, A, lda, Wp, KT, ntw, C,
+                           ldc, R, ldr, M, rs, gm, gn);
+        break;
+      case EPI_RESID:
+        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_RESID>, dim3(gm * gn), dim3(512), 0, s, A, lda, Wp, KT, ntw, C,
+                           ldc, R, ldr, M, rs, gm, gn);
+        break;
+      default:
+        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_SILU>, dim3(gm * gn), dim3(512), 0, s, A, lda, Wp, KT, ntw, C,
+                           ldc, R, ldr, M, rs, gm, gn);
+        break;
+    }
+    return;
   }
   if (gemm_uses_tiled(M, N, K, epi) && use_tiled256(M, N, epi)) {
     const int ncols = (epi == EPI_SILU) ? 128 : 256;

@@ -137,6 +137,29 @@ def test_gemm_swiglu(lib, M, K):
     assert (bf16_ulp_diff(c.cpu(), ref.cpu()) > 2).float().mean() < 2e-3
 
 
+@pytest.mark.parametrize("variant", ["ring", "256", "128"])
+@pytest.mark.parametrize("M,N,K", [(512, 512, 192), (777, 768, 1088), (2048, 1024, 4096), (1300, 256, 640)])
+def test_gemm_prefill_variants(lib, monkeypatch, variant, M, N, K):
+    """Every prefill GEMM body (INFERD_GEMM_TILE) on ragged M, short and long K, all epilogues."""
+    monkeypatch.setenv("INFERD_GEMM_TILE", variant)
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.03).to(torch.bfloat16)
+    ref = a.float() @ w.float().t()
+    c = _gemm(lib, a, w, lib.EPI_NONE)
+    assert (bf16_ulp_diff(c.cpu(), ref.to(torch.bfloat16).cpu()) > 1).float().mean() < 1e-3
+    r = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    c2 = _gemm(lib, a, w, lib.EPI_RESID, r)
+    ref2 = (ref.to(torch.bfloat16).float() + r.float()).to(torch.bfloat16)
+    assert (bf16_ulp_diff(c2.cpu(), ref2.cpu()) > 1).float().mean() < 1e-3
+    half = N // 2
+    c3 = _gemm(lib, a, w, lib.EPI_SILU)
+    gr = ref[:, :half].to(torch.bfloat16)
+    ur = ref[:, half:].to(torch.bfloat16)
+    ref3 = torch.nn.functional.silu(gr) * ur
+    assert (bf16_ulp_diff(c3.cpu(), ref3.cpu()) > 2).float().mean() < 2e-3
+
+
 def test_qk_norm_rope_golden_and_cache(lib):
     """QK-norm + RoPE vs the reference's own output (units.npz), K/V written to the cache."""
     from golden_io import load, tensor
