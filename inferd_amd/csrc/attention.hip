@@ -37,6 +37,10 @@ __device__ __forceinline__ float sum_q4(float v) {
   auto q = __builtin_amdgcn_permlane16_swap(w, w, false, false);
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
+// Prefill online softmax keeps its reference max m until a row's max grows by more than
+// RESCALE_THR (log2 units): p = exp2(s*c - m) <= 2^8 stays exact in fp32 and keeps bf16's
+// relative precision, and the O/l rescale pass runs only on real growth (guide T13).
+#define RESCALE_THR 8.0f
 // bare v_exp_f32 (arguments are <= 0 or -inf here: no range reduction needed)
 __device__ __forceinline__ float exp2_raw(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -334,16 +338,13 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
                                                  float (&m_i)[2], float (&l_i)[2], f32x4 (&o)[2][8], int lane) {
   f32x4 sc[2][4];
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int tb = 0; tb < 4; ++tb) sc[nb][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
   for (int tb = 0; tb < 4; ++tb)
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const bf16x8 kf = *(const bf16x8*)(lds + (tb * 4 + ks) * 1024 + lane * 16);
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) sc[nb][tb] = mfma16(kf, qf[nb][ks], sc[nb][tb]);
+      for (int nb = 0; nb < 2; ++nb)
+        sc[nb][tb] = mfma16(kf, qf[nb][ks], ks ? sc[nb][tb] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
   bf16x8 pf[2][2];
 #pragma unroll
@@ -357,14 +358,13 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
           sc[nb][tb][r] = (t <= lim[nb]) ? sc[nb][tb][r] : -INFINITY;
         }
     }
-    float pmax = sc[nb][0][0];
+    float pm[4];  // 4 independent max chains
 #pragma unroll
     for (int tb = 0; tb < 4; ++tb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (tb | r) pmax = fmaxf(pmax, sc[nb][tb][r]);
+      pm[tb] = fmaxf(fmaxf(sc[nb][tb][0], sc[nb][tb][1]), fmaxf(sc[nb][tb][2], sc[nb][tb][3]));
+    const float pmax = fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3]));
     const float m_new = fmaxf(m_i[nb], max_q4(pmax) * c);
-    if (__builtin_amdgcn_ballot_w64(m_new > m_i[nb])) {
+    if (__builtin_amdgcn_ballot_w64(m_new > m_i[nb] + RESCALE_THR)) {
       const float alpha = exp2_raw(m_i[nb] - m_new);
       l_i[nb] *= alpha;
 #pragma unroll
@@ -372,16 +372,14 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
       m_i[nb] = m_new;
     }
     const float mneg = -m_i[nb];
-    float psum = 0.f;
+    float ps[4];  // 4 independent sum chains
 #pragma unroll
-    for (int tb = 0; tb < 4; ++tb)
+    for (int tb = 0; tb < 4; ++tb) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = exp2_raw(fmaf(sc[nb][tb][r], c, mneg));
-        sc[nb][tb][r] = p;
-        psum += p;
-      }
-    l_i[nb] += psum;
+      for (int r = 0; r < 4; ++r) sc[nb][tb][r] = exp2_raw(fmaf(sc[nb][tb][r], c, mneg));
+      ps[tb] = (sc[nb][tb][0] + sc[nb][tb][1]) + (sc[nb][tb][2] + sc[nb][tb][3]);
+    }
+    l_i[nb] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -481,9 +479,215 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   }
 }
 
+// ------------------------------------------------------------------ prefill, 8 waves
+#define PREFILL8_MAX_PAGES 8192  // block-table entries staged in LDS (512k-token context)
+// grid (ceil(max_q_len/256), H, B), 512 threads, 1 workgroup per CU.  The workgroup owns
+// 256 query rows of one head; wave (hf = wave>>2, k = wave&3) owns rows 64k + 32hf .. +31
+// (two 16-row MFMA column blocks), so the two waves sharing a SIMD (w and w+4) have
+// neighbouring rows and near-equal causal work.
+// Each page i runs as two segments separated by raw barriers:
+//   S1(i): QK(i) and PV(i-1)  -- 64 MFMAs, K/V fragments read from LDS
+//   S2(i): softmax(i) (VALU), issue of the K page i+3 and V page i+2 (LDS-DMA), counted wait
+// Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave is in its MFMA
+// segment while its partner runs softmax.  K and V each have a 4-slot LDS ring (128 KiB);
+// a page's K/V are issued 3 segments-pairs ahead and waited with counted vmcnt (waves
+// 0-3: 8 outstanding, waves 4-7: 4 -- they reach the shared barriers one segment later);
+// slot reuse and visibility are derived in DESIGN.md §4.  Per page the workgroup stages
+// 32 KiB once for 256 rows.
+__global__ __launch_bounds__(512, 1) void attn_prefill8_kernel(const u16* __restrict__ q,
+                                                             const u16* __restrict__ kv, AttnBatch b,
+                                                             int H, int KV, float c, u16* __restrict__ out) {
+  // K slots 0-3, V slots 4-7, then this sequence's block table (read with ds_read so that no
+  // vector load -- whose wait would drain the in-flight LDS-DMA -- sits in the loop)
+  __shared__ __attribute__((aligned(16))) char lds[8 * 16384 + PREFILL8_MAX_PAGES * 4];
+  const int bseq = blockIdx.z, h = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int hf = wave >> 2, kw = wave & 3;
+  const int n_rep = H / KV, g = h / n_rep;
+  const int t0 = b.seq_start[bseq];
+  const int T = b.seq_start[bseq + 1] - t0;
+  const int nqb = (T + 255) / 256;
+  if ((int)blockIdx.x >= nqb) return;  // uniform over the workgroup
+  const int qb0 = (nqb - 1 - (int)blockIdx.x) * 256;  // heaviest blocks dispatch first
+  const int row0 = qb0 + kw * 64 + hf * 32;
+  bf16x8 qf[2][4];
+  int lim[2], tokrow[2];
+  bool valid[2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const int row = row0 + nb * 16 + (lane & 15);
+    valid[nb] = row < T;
+    tokrow[nb] = t0 + (valid[nb] ? row : T - 1);
+    lim[nb] = b.positions[tokrow[nb]];
+    const u16* qp = q + ((int64_t)tokrow[nb] * H + h) * HEAD_DIM + 8 * (lane >> 4);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
+  }
+  const int wave_last = row0 < T ? b.positions[t0 + min(row0 + 31, T - 1)] : -1;
+  int wave_min_lim = min(lim[0], lim[1]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wave_min_lim = min(wave_min_lim, __shfl_xor(wave_min_lim, o));
+  const int n_pages = b.positions[t0 + min(qb0 + 255, T - 1)] / KV_PAGE + 1;
+  int* tab = (int*)(lds + 8 * 16384);
+  {
+    const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
+    for (int j = threadIdx.x; j < n_pages; j += 512) tab[j] = bt[j];
+    // V slot 3 is read by page 0's (all-zero-P) PV before any page lands there: zero it so
+    // 0 * garbage cannot produce NaN
+    for (int j = threadIdx.x; j < 1024; j += 512) ((f32x4*)(lds + 7 * 16384))[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+  }
+  // this wave's two 1 KiB pieces of a K (or V) page: tiles 2*wave, 2*wave+1
+  auto issue = [&](int kind, int j) {  // kind 0 = K, 1 = V
+    if (j >= n_pages) return;
+    const int phys = __builtin_amdgcn_readfirstlane(tab[j]);
+    const u16* blk = kv + ((int64_t)(phys * 2 + kind) * KV + g) * KV_BLOCK_ELEMS + wave * 1024 + lane * 8;
+    char* dst = lds + (kind * 4 + (j & 3)) * 16384 + wave * 2048;
+    __builtin_amdgcn_global_load_lds((const void*)blk, (void*)dst, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(blk + 512), (void*)(dst + 1024), 16, 0, 0);
+  };
+  float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
+  f32x4 o[2][8], sc[2][4];
+  bf16x8 pf[2][2];
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+    for (int db = 0; db < 8; ++db) o[nb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pf[nb][0] = bf16x8{};
+    pf[nb][1] = bf16x8{};
+  }
+
+  // prologue: K0, K1, V0, K2, V1 landed before the first barrier
+  issue(0, 0);
+  issue(0, 1);
+  issue(1, 0);
+  issue(0, 2);
+  issue(1, 1);
+  vm_wait<0>();
+  raw_barrier();
+  if (hf) raw_barrier();  // stagger: waves 4-7 one segment behind
+
+  for (int i = 0; i <= n_pages; ++i) {
+    // ---------------- S1(i): QK(i), PV(i-1), both unconditional (a wave past its last row
+    // computes unused scores; pf is zero when there is no pending P).  Fragments are read in
+    // batches of 8 one batch ahead of the MFMAs that consume them (LDS latency hidden
+    // behind 16 MFMAs; the partner wave is in its VALU segment and cannot cover it).
+    const bool qk = i < n_pages && i * KV_PAGE <= wave_last;
+    {
+      const char* kb = lds + (i & 3) * 16384 + lane * 16;
+      const char* vb = lds + (4 + ((i + 3) & 3)) * 16384 + lane * 16;
+      // 32 fragments (16 K, then 16 V), each read 8 fragments (= 16 MFMAs) ahead of use;
+      // <= 9 LDS reads outstanding (lgkmcnt counts to 15)
+      constexpr int LA = 8;
+      bf16x8 fr[32];
+      auto rd = [&](int f) {
+        fr[f] = *(const bf16x8*)((f < 16 ? kb + f * 1024 : vb + (f - 16) * 1024));
+      };
+#pragma unroll
+      for (int f = 0; f < LA; ++f) rd(f);
+#pragma unroll
+      for (int f = 0; f < 32; ++f) {
+        if (f + LA < 32) rd(f + LA);
+        __builtin_amdgcn_sched_barrier(0);
+        if (f < 16) {
+          const int tb = f >> 2, ks = f & 3;
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+            sc[nb][tb] = mfma16(fr[f], qf[nb][ks], ks ? sc[nb][tb] : f32x4{0.f, 0.f, 0.f, 0.f});
+        } else {
+          const int kt = (f - 16) >> 3, db = (f - 16) & 7;
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb) o[nb][db] = mfma16(fr[f], pf[nb][kt], o[nb][db]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (i == n_pages) break;
+    raw_barrier();
+    // ---------------- S2(i): staging, softmax(i), counted wait
+    issue(0, i + 3);
+    issue(1, i + 2);
+    if (!qk) {
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) pf[nb][kt] = bf16x8{};
+    } else {
+      const int tok0 = i * KV_PAGE;
+      const bool mask = tok0 + KV_PAGE - 1 > wave_min_lim;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        if (mask) {
+#pragma unroll
+          for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int t = tok0 + tb * 16 + 4 * (lane >> 4) + r;
+              sc[nb][tb][r] = (t <= lim[nb]) ? sc[nb][tb][r] : -INFINITY;
+            }
+        }
+        float pm[4];  // 4 independent max chains
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb)
+          pm[tb] = fmaxf(fmaxf(sc[nb][tb][0], sc[nb][tb][1]), fmaxf(sc[nb][tb][2], sc[nb][tb][3]));
+        const float pmax = fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3]));
+        const float m_new = fmaxf(m_i[nb], max_q4(pmax) * c);
+        if (__builtin_amdgcn_ballot_w64(m_new > m_i[nb] + RESCALE_THR)) {
+          const float alpha = exp2_raw(m_i[nb] - m_new);
+          l_i[nb] *= alpha;
+#pragma unroll
+          for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
+          m_i[nb] = m_new;
+        }
+        const float mneg = -m_i[nb];
+        float ps[4];  // 4 independent sum chains
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sc[nb][tb][r] = exp2_raw(fmaf(sc[nb][tb][r], c, mneg));
+          ps[tb] = (sc[nb][tb][0] + sc[nb][tb][1]) + (sc[nb][tb][2] + sc[nb][tb][3]);
+        }
+        l_i[nb] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pf[nb][kt][j] = (__bf16)sc[nb][2 * kt][j];
+            pf[nb][kt][4 + j] = (__bf16)sc[nb][2 * kt + 1][j];
+          }
+      }
+    }
+    if (hf)
+      vm_wait<4>();
+    else
+      vm_wait<8>();
+    raw_barrier();
+  }
+  if (!hf) raw_barrier();  // close the stagger
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) {
+    const float inv = 1.0f / sum_q4(l_i[nb]);
+    if (!valid[nb]) continue;
+    u16* op = out + (int64_t)tokrow[nb] * H * HEAD_DIM + h * HEAD_DIM;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[nb][db][r] * inv);
+      *(u16x4*)(op + db * 16 + 4 * (lane >> 4)) = v;
+    }
+  }
+}
+
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
                          float scale, u16* out, hipStream_t s) {
-  dim3 g((b.max_q_len + 127) / 128, H, b.B);
-  hipLaunchKernelGGL(attn_prefill_kernel, g, dim3(256), 0, s, q, kv_layer, b, H, KV,
-                     scale * LOG2E, out);
+  // INFERD_ATTN_PREFILL=8 selects the 8-wave staggered kernel (tools/attn_bench.py A/B);
+  // the 4-wave kernel is the default (faster on the box: 712 vs 578 TF/s at 32B / 8k).
+  if (env_int("INFERD_ATTN_PREFILL") == 8 && b.max_ctx <= PREFILL8_MAX_PAGES * KV_PAGE) {
+    hipLaunchKernelGGL(attn_prefill8_kernel, dim3((b.max_q_len + 255) / 256, H, b.B), dim3(512), 0, s, q, kv_layer,
+                       b, H, KV, scale * LOG2E, out);
+    return;
+  }
+  hipLaunchKernelGGL(attn_prefill_kernel, dim3((b.max_q_len + 127) / 128, H, b.B), dim3(256), 0, s, q, kv_layer, b,
+                     H, KV, scale * LOG2E, out);
 }

@@ -50,6 +50,20 @@ __device__ __forceinline__ bf16x8 as_bf16x8(const u16x8& v) { return __builtin_b
 
 __device__ __forceinline__ int vperm(int g, int j) { return j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4); }
 
+// Counted wait on this wave's vector-memory queue (loads, stores and LDS-DMA in issue
+// order).  Inline asm: invisible to hipcc's own waitcnt pass, so it is never merged away.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// Workgroup barrier that does NOT drain vmcnt (__syncthreads() would wait for every
+// in-flight global_load_lds); memory clobber + sched barriers pin LDS accesses around it.
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Host+device splitmix64 (oracle/weightgen.py defines the same function).
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;

@@ -492,42 +492,62 @@ __global__ __launch_bounds__(512) void gemm_tiled256_kernel(
 #define RING_SLOTS 10
 #define RING_AHEAD 6
 
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void raw_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_barrier" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
+
+// Tail split (SplitTail): when the tile count leaves a partial last round on an XCD
+// (Qwen3-32B o/down: 640 tiles = 2.5 rounds of 256 CUs), each XCD's last `rem` tiles are
+// cut into `split` K-slices so the last round is full.  Slices publish fp32 partials
+// write-through (8-byte sc1 stores), take a ticket, and the last arriver of a tile polls
+// the done counter, acquires, sums the partials in slice order (deterministic) and runs
+// the epilogue (cdna_hip_programming.md §5 split-K, §6 Guideline 16 R1).
+struct SplitTail {
+  int split;            // 1 = no split
+  int tiles_per_xcd;    // tiles owned by one XCD's contiguous block range
+  int full_per_xcd;     // of which are computed whole
+  int units_per_xcd;    // full_per_xcd + (tiles_per_xcd - full_per_xcd) * split
+  float* ws;            // per split tile: split x (256 x 256) fp32 partials
+  unsigned* cnt;        // [2][8 * rem] arrival tickets, done counters (zero between launches)
+};
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
     u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    const float* __restrict__ rs, int grid_m, int grid_n) {
+    const float* __restrict__ rs, int grid_m, int grid_n, SplitTail st) {
   __shared__ __attribute__((aligned(16))) char lds[RING_SLOTS * 16384];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 2, wc = wave & 3;
   // ---- XCD-aware tile order (bijective for any grid size)
-  int bm, bn;
+  int bm, bn, slice = 0, nsl = 1, sidx = 0;
   {
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    int tile = wg;
+    if (st.split > 1) {  // grid = 8 * units_per_xcd
+      const int x = wg / st.units_per_xcd, li = wg - x * st.units_per_xcd;
+      if (li < st.full_per_xcd) {
+        tile = x * st.tiles_per_xcd + li;
+      } else {
+        const int j = li - st.full_per_xcd;
+        tile = x * st.tiles_per_xcd + st.full_per_xcd + j / st.split;
+        slice = j % st.split;
+        nsl = st.split;
+        sidx = x * (st.tiles_per_xcd - st.full_per_xcd) + j / st.split;
+      }
+    }
     constexpr int GM = 8;
-    const int group = wg / (GM * grid_n);
+    const int group = tile / (GM * grid_n);
     const int first_m = group * GM;
     const int gsz = min(grid_m - first_m, GM);
-    const int in = wg - group * GM * grid_n;
+    const int in = tile - group * GM * grid_n;
     bm = first_m + in % gsz;
     bn = in / gsz;
   }
   const int m0 = bm * 256;
   const int n0 = bn * ((EPI == EPI_SILU) ? 128 : 256);
-  const int nK = KT / 2;       // 64-deep K-steps
-  const int S = 4 * nK;        // half-tiles
+  const int nK = KT / 2 / nsl;  // 64-deep K-steps of this slice
+  const int S = 4 * nK;         // half-tiles
+  const int k0 = slice * nK;    // first K-step
 
   // ---- staging sources: this wave's two 1 KiB pieces of each half-tile kind
   const u16* a_src[2][2];      // [half][piece]
@@ -541,7 +561,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
       int grow = m0 + (i >> 6) * 128 + h * 64 + (i & 63);
       grow = grow < M ? grow : M - 1;
       const int chunk = (lane & 7) ^ ((i >> 1) & 7);
-      a_src[h][p] = A + (int64_t)grow * lda + chunk * 8;
+      a_src[h][p] = A + (int64_t)grow * lda + chunk * 8 + k0 * 64;
     }
     // image n-tile nl = wave: wave column nl>>1, sub-tile nl&1
     int gnt;
@@ -549,7 +569,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
       gnt = (h == 0 ? 0 : n_tiles_w / 2) + n0 / 16 + (wave >> 1) * 2 + (wave & 1);
     else
       gnt = n0 / 16 + (wave >> 1) * 4 + h * 2 + (wave & 1);
-    b_src[h] = Wp + (int64_t)gnt * KT * 512 + lane * 8;
+    b_src[h] = Wp + ((int64_t)gnt * KT + 2 * k0) * 512 + lane * 8;
   }
   // kind: 0 = A0, 1 = B0, 2 = B1, 3 = A1 (the consumption order within a K-step)
   auto issue = [&](int kind, int t, int slot) {
@@ -663,6 +683,73 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
   phase(I3{}, rb, -1, VNONE{});
   if (wr == 0) raw_barrier();  // close the stagger
 
+  if (nsl > 1) {  // ---- tail split: publish or combine
+    __syncthreads();  // every wave is past its last LDS read: lds is free
+    unsigned* ticket_lds = (unsigned*)lds;
+    unsigned* cnt = st.cnt + sidx;
+    unsigned* done = st.cnt + 8 * (st.tiles_per_xcd - st.full_per_xcd) + sidx;
+    if (threadIdx.x == 0) ticket_lds[0] = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned ticket = ticket_lds[0];
+    float* part = st.ws + (size_t)sidx * nsl * 65536;
+    if (ticket + 1 < (unsigned)nsl) {  // not last: publish this slice's partial write-through
+      unsigned long long* dst = (unsigned long long*)(part + (size_t)slice * 65536);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const unsigned long long v = ((unsigned long long)__float_as_uint(acc[i][j][2 * hh + 1]) << 32) |
+                                         __float_as_uint(acc[i][j][2 * hh]);
+            __hip_atomic_store(dst + (((i * 4 + j) * 2 + hh) * 512 + threadIdx.x), v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (threadIdx.x == 0) {
+      while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 < (unsigned)nsl)
+        __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    f32x4 sum[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < nsl; ++sl) {  // fixed slice order
+      if (sl == slice) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sum[i][j] += acc[i][j];
+      } else {
+        const unsigned long long* src = (const unsigned long long*)(part + (size_t)sl * 65536);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+              const unsigned long long v = src[((i * 4 + j) * 2 + hh) * 512 + threadIdx.x];
+              sum[i][j][2 * hh] += __uint_as_float((unsigned)v);
+              sum[i][j][2 * hh + 1] += __uint_as_float((unsigned)(v >> 32));
+            }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = sum[i][j];
+  }
+
   // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -710,6 +797,50 @@ static int gemm_tile_variant() {
   return atoi(e);
 }
 
+// Tail-split plan for `tiles` 256x256 tiles of nK K-steps on 8 XCDs x 32 CUs (one 512-thread
+// workgroup per CU).  INFERD_GEMM_SPLIT=0 disables it.  The fp32 partial workspace and the
+// counters are allocated once (zeroed) and grown on demand; never inside a graph capture.
+static float* g_split_ws = nullptr;
+static size_t g_split_ws_bytes = 0;
+static unsigned* g_split_cnt = nullptr;
+static int g_split_cnt_n = 0;
+
+static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
+  SplitTail st = {1, 0, 0, 0, nullptr, nullptr};
+  const char* e = getenv("INFERD_GEMM_SPLIT");
+  if (e && *e && atoi(e) == 0) return st;
+  if (tiles % 8) return st;
+  const int per = tiles / 8, rem = per % 32;
+  if (rem == 0 || 32 % rem) return st;
+  const int split = 32 / rem;
+  if (split > 8 || nK % split || nK / split < 3) return st;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return st;
+  const size_t bytes = (size_t)8 * rem * split * 65536 * sizeof(float);
+  if (bytes > g_split_ws_bytes) {
+    if (g_split_ws) (void)hipFree(g_split_ws);
+    g_split_ws = nullptr;
+    g_split_ws_bytes = 0;
+    if (hipMalloc((void**)&g_split_ws, bytes) != hipSuccess) return st;
+    g_split_ws_bytes = bytes;
+  }
+  if (2 * 8 * rem > g_split_cnt_n) {
+    if (g_split_cnt) (void)hipFree(g_split_cnt);
+    g_split_cnt = nullptr;
+    g_split_cnt_n = 0;
+    if (hipMalloc((void**)&g_split_cnt, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
+    if (hipMemset(g_split_cnt, 0, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
+    g_split_cnt_n = 2 * 8 * rem;
+  }
+  st.split = split;
+  st.tiles_per_xcd = per;
+  st.full_per_xcd = per - rem;
+  st.units_per_xcd = per - rem + rem * split;
+  st.ws = g_split_ws;
+  st.cnt = g_split_cnt;
+  return st;
+}
+
 static bool use_ring256(int M, int N, int K, int epi) {
   if (gemm_tile_variant() != 0 || M < 512 || K < 192) return false;
   return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
@@ -740,18 +871,20 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     const int ncols = (epi == EPI_SILU) ? 128 : 256;
     const int gm = (M + 255) / 256, gn = N / ncols;
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
+    const SplitTail st = plan_split_tail(gm * gn, K / 64, s);
+    const int grid = st.split > 1 ? 8 * st.units_per_xcd : gm * gn;
     switch (epi) {
       case EPI_NONE:
-        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_NONE>, dim3(gm * gn), dim3(512), 0, s, A, lda, Wp, KT, ntw, C,
-                           ldc, R, ldr, M, rs, gm, gn);
+        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_NONE>, dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                           ldr, M, rs, gm, gn, st);
         break;
       case EPI_RESID:
-        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_RESID>, dim3(gm * gn), dim3(512), 0, s, A, lda, Wp, KT, ntw, C,
-                           ldc, R, ldr, M, rs, gm, gn);
+        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_RESID>, dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc,
+                           R, ldr, M, rs, gm, gn, st);
         break;
       default:
-        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_SILU>, dim3(gm * gn), dim3(512), 0, s, A, lda, Wp, KT, ntw, C,
-                           ldc, R, ldr, M, rs, gm, gn);
+        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_SILU>, dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                           ldr, M, rs, gm, gn, st);
         break;
     }
     return;

@@ -138,9 +138,11 @@ def test_gemm_swiglu(lib, M, K):
 
 
 @pytest.mark.parametrize("variant", ["ring", "256", "128"])
-@pytest.mark.parametrize("M,N,K", [(512, 512, 192), (777, 768, 1088), (2048, 1024, 4096), (1300, 256, 640)])
+@pytest.mark.parametrize("M,N,K", [(512, 512, 192), (777, 768, 1088), (2048, 1024, 4096), (1300, 256, 640),
+                                   (4096, 2048, 1024)])
 def test_gemm_prefill_variants(lib, monkeypatch, variant, M, N, K):
-    """Every prefill GEMM body (INFERD_GEMM_TILE) on ragged M, short and long K, all epilogues."""
+    """Every prefill GEMM body (INFERD_GEMM_TILE) on ragged M, short and long K, all epilogues.
+    (2048, 1024, 4096) and (4096, 2048, 1024) run the ring kernel's tail split (K cut 8 / 2 ways)."""
     monkeypatch.setenv("INFERD_GEMM_TILE", variant)
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
@@ -272,6 +274,10 @@ def test_attention_decode(lib, H, KV):
 
 
 @pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2)])
-def test_attention_prefill(lib, H, KV):
-    err, ref = _attn_case(lib, H, KV, [1, 17, 64, 130], [0, 5, 0, 200], seed=H + 1)
+@pytest.mark.parametrize("variant", ["4", "8"])
+def test_attention_prefill(lib, monkeypatch, H, KV, variant):
+    """Both prefill kernels (8-wave staggered, 4-wave) on ragged prompts, with and without
+    cached prefixes, including a 700-token prompt (several 256-row blocks, > 4 pages)."""
+    monkeypatch.setenv("INFERD_ATTN_PREFILL", variant)
+    err, ref = _attn_case(lib, H, KV, [1, 17, 64, 130, 700], [0, 5, 0, 200, 61], seed=H + 1)
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()

@@ -1,0 +1,92 @@
+"""Attention kernel timing on the GPU box through the C-ABI (inferd_attention).
+
+prefill: Qwen3-32B dims (H=64, KV=8), B x T causal prompt (BASELINE config 5)
+decode : Qwen3-8B dims (H=32, KV=8), B=16 single tokens at ctx 2048 (BASELINE config 3)
+Random bf16 q and K/V (uniform, rule 25); algorithmic flops count T(T+1)/2 keys per row.
+Variants are selected per call through environment variables (e.g. INFERD_ATTN_PREFILL=<v>),
+interleaved over rounds in one process.
+
+usage: python tools/attn_bench.py [--mode prefill|decode] [--env NAME=v1,v2]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from inferd_amd import _lib  # noqa: E402
+from inferd_amd.runtime import PagePool, SeqState, build_batch  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--mode", default="prefill")
+    p.add_argument("--T", type=int, default=8192)
+    p.add_argument("--B", type=int, default=1)
+    p.add_argument("--ctx", type=int, default=2048)
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--env", default="", help="NAME=v1,v2 : variants to interleave")
+    args = p.parse_args()
+    L = _lib.load()
+    dev = torch.device("cuda", 0)
+    if args.mode == "prefill":
+        H, KV, B, T, P = 64, 8, args.B, args.T, 0
+    else:
+        H, KV, B, T, P = 32, 8, 16, 1, args.ctx - 1
+    n = T + P
+    pages_per = (n + 63) // 64
+    pool = PagePool(B * pages_per)
+    seqs = []
+    for _ in range(B):
+        st = SeqState()
+        st.pages = pool.alloc(pages_per)
+        st.length = P
+        seqs.append((st, T))
+    batch, keep = build_batch(seqs, dev)
+    kv = (torch.rand(B * pages_per * 2 * KV * 64 * 128, device=dev) * 2 - 1).to(torch.bfloat16)
+    q = (torch.rand(B * T, H, 128, device=dev) * 4 - 2).to(torch.bfloat16)
+    out = torch.empty(B * T, H * 128, dtype=torch.bfloat16, device=dev)
+    ws_bytes = L.inferd_attention_workspace_bytes(B, H, n)
+    ws = torch.zeros(max(ws_bytes, 256), dtype=torch.uint8, device=dev)
+    st = _lib.stream_ptr()
+    if args.mode == "prefill":
+        flops = B * 4.0 * H * 128 * T * (T + 1) / 2
+        bytes_ = None
+    else:
+        flops = B * 4.0 * H * 128 * n
+        bytes_ = B * n * KV * 128 * 2 * 2
+    name, vals = (args.env.split("=") + [""])[:2] if args.env else ("", "")
+    variants = vals.split(",") if vals else [""]
+    times = {v: [] for v in variants}
+    outs = {}
+    for rnd in range(args.rounds):
+        for v in variants:
+            if name:
+                os.environ[name] = v
+            call = lambda: _lib.check(L.inferd_attention(q.data_ptr(), kv.data_ptr(), batch, H, KV,  # noqa: E731
+                                                         out.data_ptr(), ws.data_ptr(), ws_bytes, st))
+            call()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.reps):
+                call()
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / args.reps)
+            if rnd == 0:
+                outs[v] = out.clone()
+    for v in variants:
+        t = sorted(times[v])
+        med = t[len(t) // 2]
+        line = f"{args.mode} {name}={v!r}: {med * 1e3:9.1f} us  {flops / med / 1e9:7.1f} TF/s"
+        if bytes_:
+            line += f"  {bytes_ / med / 1e6:7.1f} GB/s"
+        d = (outs[v].float() - outs[variants[0]].float()).abs().max().item()
+        print(line + f"  maxdiff={d:.3g}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,7 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--variants", default="ring,256")
+    p.add_argument("--env-name", default="INFERD_GEMM_TILE", help="environment variable the variants set")
     p.add_argument("--shapes", default=",".join(SHAPES))
     args = p.parse_args()
     L = _lib.load()
@@ -53,7 +54,7 @@ def main():
     for rnd in range(args.rounds):
         for name, (a, wp, c, r, n, k, epi) in bufs.items():
             for v in variants:
-                os.environ["INFERD_GEMM_TILE"] = v
+                os.environ[args.env_name] = v
                 call = lambda: _lib.check(L.inferd_gemm(a.data_ptr(), wp.data_ptr(), c.data_ptr(),  # noqa: E731
                                                         None if r is None else r.data_ptr(), M, n, k, epi, st))
                 call()
