@@ -64,11 +64,83 @@ __device__ __forceinline__ float exp2_raw(float x) { return __builtin_amdgcn_exp
 #define DECODE_COUNTER_BYTES 65536   // B * KV <= 16384; zero before first use, left zero
 #define MAX_DECODE_CHUNKS 64
 
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restrict__ q, const u16* __restrict__ kv,
+// FUSED: the kernel also does the decode token's Qwen3 QK-norm + RoPE + cache write
+// (qk_norm_rope_kv_kernel's arithmetic, same rounding points): every workgroup normalises
+// and rotates its n_rep query heads from the raw qkv row in registers (a lane's 32 dims of
+// a head are 4 fragments; the RMS sum is reduced over the head's 4 lanes; the RoPE partner
+// dim d +- 64 is the same lane's fragment ks +- 2), and the one wave that will read the
+// token's page writes its K (normed, rotated) and V into the cache first, then waits for
+// its own stores (vmcnt(0)) before loading that page -- no other wave reads that token.
+struct DecodeFuse {
+  const u16* qkv;
+  int64_t ldqkv;
+  const u16* qn_w;
+  const u16* kn_w;
+  const u16* cos_t;
+  const u16* sin_t;
+  float eps;
+};
+
+// K/V of the decode token `tok` for kv head g -> cache (lanes 0-15 K, 16-31 V; all 64 lanes
+// run the arithmetic so the 16-wide shuffles see full groups)
+__device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __restrict__ kv, const AttnBatch& b,
+                                                int bseq, int tok, int g, int H, int KV, int lane) {
+  const int pos = b.positions[tok];
+  const int pg = pos / KV_PAGE;
+  if (pg >= b.max_pages) return;
+  const int page = b.block_table[(int64_t)bseq * b.max_pages + pg], s = pos & (KV_PAGE - 1);
+  const int c = lane & 15;
+  const u16x8 kraw = *(const u16x8*)(f.qkv + (int64_t)tok * f.ldqkv + (int64_t)(H + g) * HEAD_DIM + c * 8);
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = bf2f(kraw[j]);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+  const float inv = 1.0f / sqrtf(ss / 128.0f + f.eps);
+  const u16x8 wv = *(const u16x8*)(f.kn_w + c * 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = rbf(bf2f(wv[j]) * rbf(x[j] * inv));
+  float pr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pr[j] = __shfl_xor(x[j], 8, 16);
+  const int ci = (c & 7) * 8;
+  const u16x8 cv = *(const u16x8*)(f.cos_t + (int64_t)pos * 64 + ci);
+  const u16x8 sv = *(const u16x8*)(f.sin_t + (int64_t)pos * 64 + ci);
+  u16x8 ko;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float rot = c < 8 ? -pr[j] : pr[j];
+    ko[j] = f2bf(rbf(x[j] * bf2f(cv[j])) + rbf(rot * bf2f(sv[j])));
+  }
+  if (lane < 16) {
+    u16* blk = kv + ((int64_t)(page * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
+    const int tb = s >> 4, ks = c >> 2, ln = (s & 15) + 16 * (c & 3);
+    *(u16x8*)(blk + ((tb * 4 + ks) * 64 + ln) * 8) = ko;
+  } else if (lane < 32) {
+    const u16x8 vraw =
+        *(const u16x8*)(f.qkv + (int64_t)tok * f.ldqkv + (int64_t)(H + KV + g) * HEAD_DIM + c * 8);
+    u16* blk = kv + ((int64_t)(page * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
+    const int kt = s >> 5, tp = s & 31;
+    const int gg = tp < 16 ? (tp >> 2) : ((tp - 16) >> 2);
+    const int jj = tp < 16 ? (tp & 3) : 4 + ((tp - 16) & 3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = c * 8 + j;
+      const int db = d >> 4, ln = (d & 15) + 16 * gg;
+      blk[((kt * 8 + db) * 64 + ln) * 8 + jj] = vraw[j];
+    }
+  }
+}
+
+template <int NW, bool FUSED>
+__global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restrict__ q, u16* __restrict__ kv,
                                                       AttnBatch b, int H, int KV, int nc_req, float scale_log2,
                                                       int n_chunks_max, unsigned* __restrict__ counters,
-                                                      float* __restrict__ part, u16* __restrict__ out) {
+                                                      float* __restrict__ part, u16* __restrict__ out,
+                                                      DecodeFuse fz) {
   __shared__ float sm_m[NW][16], sm_l[NW][16];
   __shared__ float sm_o[NW][16][HEAD_DIM + 4];
   __shared__ float sm_f[MAX_DECODE_CHUNKS][16], sm_lc[MAX_DECODE_CHUNKS][16];
@@ -84,8 +156,46 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
   const int cp0 = (chunk * n_pages) / nc, cp1 = ((chunk + 1) * n_pages) / nc;
   const int tok = b.seq_start[bseq + 1] - 1;
   const int hn = lane & 15;
+  // the wave that reads the token's page (the sequence's last page) writes its K/V
+  const int last_page = n_pages - 1;
+  const bool writer = FUSED && chunk == nc - 1 && wave == (last_page - cp0) % NW;
+  if (writer) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
   bf16x8 qf[4];
-  {
+  if constexpr (FUSED) {
+    const int hh = hn < n_rep ? hn : 0;
+    const int d0 = 8 * (lane >> 4);
+    const u16* qp = fz.qkv + (int64_t)tok * fz.ldqkv + (int64_t)(g * n_rep + hh) * HEAD_DIM + d0;
+    float x[4][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const u16x8 r = *(const u16x8*)(qp + ks * 32);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        x[ks][j] = bf2f(r[j]);
+        ss += x[ks][j] * x[ks][j];
+      }
+    }
+    const float inv = 1.0f / sqrtf(sum_q4(ss) / 128.0f + fz.eps);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const u16x8 wv = *(const u16x8*)(fz.qn_w + d0 + ks * 32);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[ks][j] = rbf(bf2f(wv[j]) * rbf(x[ks][j] * inv));
+    }
+    const int pos = b.positions[tok];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int dc = d0 + (ks & 1) * 32;  // dim mod 64 of element 0
+      const u16x8 cv = *(const u16x8*)(fz.cos_t + (int64_t)pos * 64 + dc);
+      const u16x8 sv = *(const u16x8*)(fz.sin_t + (int64_t)pos * 64 + dc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float rot = ks < 2 ? -x[ks + 2][j] : x[ks - 2][j];
+        qf[ks][j] = (__bf16)(rbf(x[ks][j] * bf2f(cv[j])) + rbf(rot * bf2f(sv[j])));
+      }
+    }
+  } else {
     const int hh = hn < n_rep ? hn : 0;
     const u16* qp = q + ((int64_t)tok * H + g * n_rep + hh) * HEAD_DIM + 8 * (lane >> 4);
 #pragma unroll
@@ -106,6 +216,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
     auto vaddr = [&](int p) {
       return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 1) * KV + g) * KV_BLOCK_ELEMS) + lane;
     };
+    if (writer && pi == last_page) vm_wait<0>();  // own K/V stores landed before the page loads
     {
       const bf16x8* kb = kaddr(pi);
       const bf16x8* vb = vaddr(pi);
@@ -127,6 +238,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
       }
       __builtin_amdgcn_sched_barrier(0);
       if (more) {
+        if (writer && nxt == last_page) vm_wait<0>();
         const bf16x8* kb = kaddr(nxt);
 #pragma unroll
         for (int i = 0; i < 16; ++i) kf[i] = __builtin_nontemporal_load(kb + i * 64);
@@ -293,23 +405,44 @@ size_t attn_decode_ws_bytes(int B, int H, int max_ctx) {
   return DECODE_COUNTER_BYTES + (size_t)B * H * MAX_DECODE_CHUNKS * PART_STRIDE * sizeof(float);
 }
 
+template <bool FUSED>
+static void attn_decode_go(const u16* q, u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
+                           float* ws, hipStream_t s, const DecodeFuse& fz) {
+  int nw, nc;
+  decode_shape(b.B, KV, b.max_ctx, &nw, &nc);
+  unsigned* counters = (unsigned*)ws;
+  float* part = (float*)((char*)ws + DECODE_COUNTER_BYTES);
+  if (nw == 8)
+    hipLaunchKernelGGL((attn_decode_kernel<8, FUSED>), dim3(nc, KV, b.B), dim3(512), 0, s, q, kv_layer, b, H, KV, nc,
+                       scale * LOG2E, nc, counters, part, out, fz);
+  else
+    hipLaunchKernelGGL((attn_decode_kernel<4, FUSED>), dim3(nc, KV, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, nc,
+                       scale * LOG2E, nc, counters, part, out, fz);
+}
+
+// explicit (waves, chunks) shape, for tools/attn_lab.hip sweeps
 void launch_attn_decode_shape(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale,
                               u16* out, float* ws, hipStream_t s, int nw, int nc) {
   unsigned* counters = (unsigned*)ws;
   float* part = (float*)((char*)ws + DECODE_COUNTER_BYTES);
   if (nw == 8)
-    hipLaunchKernelGGL(attn_decode_kernel<8>, dim3(nc, KV, b.B), dim3(512), 0, s, q, kv_layer, b, H, KV, nc,
-                       scale * LOG2E, nc, counters, part, out);
+    hipLaunchKernelGGL((attn_decode_kernel<8, false>), dim3(nc, KV, b.B), dim3(512), 0, s, q, (u16*)kv_layer, b, H,
+                       KV, nc, scale * LOG2E, nc, counters, part, out, DecodeFuse{});
   else
-    hipLaunchKernelGGL(attn_decode_kernel<4>, dim3(nc, KV, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, nc,
-                       scale * LOG2E, nc, counters, part, out);
+    hipLaunchKernelGGL((attn_decode_kernel<4, false>), dim3(nc, KV, b.B), dim3(256), 0, s, q, (u16*)kv_layer, b, H,
+                       KV, nc, scale * LOG2E, nc, counters, part, out, DecodeFuse{});
 }
 
 void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
                         float scale, u16* out, float* ws, hipStream_t s) {
-  int nw, nc;
-  decode_shape(b.B, KV, b.max_ctx, &nw, &nc);
-  launch_attn_decode_shape(q, kv_layer, b, H, KV, scale, out, ws, s, nw, nc);
+  attn_decode_go<false>(q, (u16*)kv_layer, b, H, KV, scale, out, ws, s, DecodeFuse{});
+}
+
+void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
+                              const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
+                              float scale, u16* out, float* ws, hipStream_t s) {
+  const DecodeFuse fz = {qkv, ldqkv, qn_w, kn_w, cos_t, sin_t, eps};
+  attn_decode_go<true>(nullptr, kv_layer, b, H, KV, scale, out, ws, s, fz);
 }
 
 // ------------------------------------------------------------------ prefill (causal)

@@ -66,6 +66,12 @@ struct AttnBatch {
 // q [M][H][128] bf16 -> out [M][H*128] bf16.  kv_layer: this layer's pool base.
 void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
                         float scale, u16* out, float* ws, hipStream_t s);
+// Decode attention with the token's QK-norm + RoPE + K/V cache write fused in (replaces
+// launch_qk_norm_rope_kv + launch_attn_decode on the decode path): qkv is the raw
+// [M][(H+2KV)*128] projection output.
+void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
+                              const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
+                              float scale, u16* out, float* ws, hipStream_t s);
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx);
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
                          float scale, u16* out, hipStream_t s);

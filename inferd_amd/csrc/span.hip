@@ -360,6 +360,13 @@ static AttnBatch to_attn(const InferdBatch* b) {
   return a;
 }
 
+// INFERD_FUSE_DECODE_ROPE=0 restores the separate qk_norm_rope_kv launch on decode steps
+// (A/B and parity checks); read at capture/launch time.
+static bool fuse_decode_rope() {
+  const char* e = getenv("INFERD_FUSE_DECODE_ROPE");
+  return !(e && *e == '0');
+}
+
 extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const int32_t* ids,
                                    const void* x_in, void* x_out, int32_t* next_ids, void* logits,
                                    void* layer_out, void* stream) {
@@ -399,16 +406,23 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pe = s->prof_begin(PROF_QKV, st);
     launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &rn);
     s->prof_end(pe, st);
-    pe = s->prof_begin(PROF_ROPE, st);
-    launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
-                           s->sin_t, s->q, kv_l, M, H, KV, c.rms_eps, st);
-    s->prof_end(pe, st);
-    pe = s->prof_begin(PROF_ATTN, st);
-    if (b->decode)
-      launch_attn_decode(s->q, kv_l, ab, H, KV, scale, s->attn, s->attn_ws, st);
-    else
-      launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
-    s->prof_end(pe, st);
+    if (b->decode && fuse_decode_rope()) {  // QK-norm + RoPE + cache write inside attention
+      pe = s->prof_begin(PROF_ATTN, st);
+      launch_attn_decode_fused(s->qkv, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
+                               scale, s->attn, s->attn_ws, st);
+      s->prof_end(pe, st);
+    } else {
+      pe = s->prof_begin(PROF_ROPE, st);
+      launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
+                             s->sin_t, s->q, kv_l, M, H, KV, c.rms_eps, st);
+      s->prof_end(pe, st);
+      pe = s->prof_begin(PROF_ATTN, st);
+      if (b->decode)
+        launch_attn_decode(s->q, kv_l, ab, H, KV, scale, s->attn, s->attn_ws, st);
+      else
+        launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
+      s->prof_end(pe, st);
+    }
     // h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
     pe = s->prof_begin(PROF_O, st);
     launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);

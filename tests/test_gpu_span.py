@@ -212,3 +212,30 @@ def test_norm_fold_order_enforced():
     again = s.forward([(None, 8)], ids=ids)["hidden"]
     assert torch.equal(again.cpu(), ref.cpu())
     assert _lib.load() is not None
+
+
+def test_decode_fused_rope_matches_separate(monkeypatch):
+    """Decode attention with QK-norm + RoPE + cache write fused in (default) against the
+    separate qk_norm_rope_kv launch (INFERD_FUSE_DECODE_ROPE=0): Qwen3-8B-dims heads
+    (32 q / 8 kv), ragged contexts that put the new token at a page start, mid-page and page
+    end; 5 decode steps each.  The fused path sums the q RMS in another order, so hidden
+    states may differ by a bf16 rounding (the cached K/V written in step k feed step k+1)."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["qwen3-8b"]
+    lens = [63, 64, 100, 130]
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("INFERD_FUSE_DECODE_ROPE", fused)
+        s = SpanRuntime(d, 0, 2, has_embed=True, has_lm_head=False, device=DEV, max_positions=1024,
+                        kv_pages=32, max_tokens=512, max_seqs=4)
+        s.init_synthetic(SEED)
+        prompts = [torch.randint(0, d.vocab, (n,), generator=torch.Generator().manual_seed(n)) for n in lens]
+        s.forward([(f"s{i}", n) for i, n in enumerate(lens)], ids=torch.cat(prompts), want_hidden=False)
+        hs = []
+        for step in range(5):
+            ids = torch.tensor([(7 * step + 3 * i) % d.vocab for i in range(len(lens))])
+            hs.append(s.forward([(f"s{i}", 1) for i in range(len(lens))], ids=ids, want_hidden=True)["hidden"].cpu())
+        outs.append(torch.stack(hs))
+    e = rel_err(outs[0], outs[1])
+    print(f"fused vs separate decode hidden rel err {e:.2e}")
+    assert e < 2e-2
