@@ -816,7 +816,8 @@ void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, 
                          float scale, u16* out, hipStream_t s) {
   // INFERD_ATTN_PREFILL=8 selects the 8-wave staggered kernel (tools/attn_bench.py A/B);
   // the 4-wave kernel is the default (faster on the box: 712 vs 578 TF/s at 32B / 8k).
-  if (env_int("INFERD_ATTN_PREFILL") == 8 && b.max_ctx <= PREFILL8_MAX_PAGES * KV_PAGE) {
+  const int variant = env_int("INFERD_ATTN_PREFILL");
+  if (variant == 8 && b.max_ctx <= PREFILL8_MAX_PAGES * KV_PAGE) {
     hipLaunchKernelGGL(attn_prefill8_kernel, dim3((b.max_q_len + 255) / 256, H, b.B), dim3(512), 0, s, q, kv_layer,
                        b, H, KV, scale * LOG2E, out);
     return;
