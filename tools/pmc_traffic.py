@@ -38,16 +38,16 @@ def rows(d):
     return out
 
 
-PREFILL_KEYS = ("gemm_tiled", "attn_prefill")
+PREFILL_KEYS = ("gemm_tiled", "gemm_ring", "attn_prefill", "row_inv_rms")
 
 
 def classify(name):
     """Bench kernel class of a decode-phase dispatch name (None: not a decode kernel)."""
     if "gemm_decode_kernel" in name:
-        m = re.search(r"gemm_decode_kernel<([-\d, ]+)>", name)
+        m = re.search(r"gemm_decode_kernel<([^>]+)>", name)
         if not m:
             return "gemm_decode"
-        epi = int(m.group(1).split(",")[-1])
+        epi = int(m.group(1).split(",")[5])  # <MT, S, NW, TW, D, EPI, NORM>
         return {0: "qkv_gemm", 1: "resid_gemm", 2: "gateup_gemm", 3: "lm_head_argmax"}[epi]
     for key, cls in (("attn_decode_kernel", "attention"), ("qk_norm_rope_kv", "qk_norm_rope_kv"),
                      ("rmsnorm", "rmsnorm"), ("argmax_reduce", "lm_head_argmax")):
