@@ -72,14 +72,59 @@ __device__ __forceinline__ float exp2_raw(float x) { return __builtin_amdgcn_exp
 // token's page writes its K (normed, rotated) and V into the cache first, then waits for
 // its own stores (vmcnt(0)) before loading that page -- no other wave reads that token.
 struct DecodeFuse {
-  const u16* qkv;
+  const u16* qkv;  // bf16 [M][ldqkv] q/k/v rows, or null when `part` is given
   int64_t ldqkv;
   const u16* qn_w;
   const u16* kn_w;
   const u16* cos_t;
   const u16* sin_t;
   float eps;
+  // split-K q/k/v (launch_gemm_decode_partial): value = bf16(sum_s part[s] * rsqrt(sum_s
+  // ssq[s] / K + eps)) -- the same rounding point as the unsplit GEMM's epilogue
+  const float* part;  // [ksl][M][ldqkv]
+  const float* ssq;   // [ksl][M]
+  int ksl;
+  int K;
 };
+
+// 8 consecutive q/k/v values of row `tok` starting at column `col` (fp32, bf16-rounded)
+__device__ __forceinline__ void qkv8(const DecodeFuse& f, int M, int tok, int col, float (&x)[8]) {
+  if (f.part) {
+    // all slices' loads issued together (predicated, unrolled to the maximum slice count)
+    f32x4 pa[4], pb[4];
+    float ps[4];
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      if (sl < f.ksl) {
+        const f32x4* p = (const f32x4*)(f.part + ((int64_t)sl * M + tok) * f.ldqkv + col);
+        pa[sl] = p[0];
+        pb[sl] = p[1];
+        ps[sl] = f.ssq[sl * M + tok];
+      } else {
+        pa[sl] = pb[sl] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ps[sl] = 0.f;
+      }
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float ss = 0.f;
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {  // fixed slice order (zeros past ksl add exactly)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[j] += pa[sl][j];
+        acc[4 + j] += pb[sl][j];
+      }
+      ss += ps[sl];
+    }
+    const float inv = 1.0f / sqrtf(ss / (float)f.K + f.eps);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = rbf(acc[j] * inv);
+  } else {
+    const u16x8 r = *(const u16x8*)(f.qkv + (int64_t)tok * f.ldqkv + col);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = bf2f(r[j]);
+  }
+}
 
 // K/V of the decode token `tok` for kv head g -> cache (lanes 0-15 K, 16-31 V; all 64 lanes
 // run the arithmetic so the 16-wide shuffles see full groups)
@@ -90,10 +135,8 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
   if (pg >= b.max_pages) return;
   const int page = b.block_table[(int64_t)bseq * b.max_pages + pg], s = pos & (KV_PAGE - 1);
   const int c = lane & 15;
-  const u16x8 kraw = *(const u16x8*)(f.qkv + (int64_t)tok * f.ldqkv + (int64_t)(H + g) * HEAD_DIM + c * 8);
   float x[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = bf2f(kraw[j]);
+  qkv8(f, b.M, tok, (H + g) * HEAD_DIM + c * 8, x);
   float ss = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ss += x[j] * x[j];
@@ -120,8 +163,11 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
     const int tb = s >> 4, ks = c >> 2, ln = (s & 15) + 16 * (c & 3);
     *(u16x8*)(blk + ((tb * 4 + ks) * 64 + ln) * 8) = ko;
   } else if (lane < 32) {
-    const u16x8 vraw =
-        *(const u16x8*)(f.qkv + (int64_t)tok * f.ldqkv + (int64_t)(H + KV + g) * HEAD_DIM + c * 8);
+    float vx[8];
+    qkv8(f, b.M, tok, (H + KV + g) * HEAD_DIM + c * 8, vx);
+    u16x8 vraw;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vraw[j] = f2bf(vx[j]);
     u16* blk = kv + ((int64_t)(page * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
     const int kt = s >> 5, tp = s & 31;
     const int gg = tp < 16 ? (tp >> 2) : ((tp - 16) >> 2);
@@ -159,22 +205,45 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
   // the wave that reads the token's page (the sequence's last page) writes its K/V
   const int last_page = n_pages - 1;
   const bool writer = FUSED && chunk == nc - 1 && wave == (last_page - cp0) % NW;
-  if (writer) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
+  const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
+  const int lim = ctx - 1;
+  int pi = cp0 + wave;
+  const bool has_page = pi < cp1;
+  auto kaddr = [&](int p) {
+    return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 0) * KV + g) * KV_BLOCK_ELEMS) + lane;
+  };
+  auto vaddr = [&](int p) {
+    return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 1) * KV + g) * KV_BLOCK_ELEMS) + lane;
+  };
+  // The first page's K/V loads are issued before the token's q/k/v arithmetic so their
+  // latency overlaps it; the writer stores the token's K/V first only when that first page
+  // is the token's own page (its stores must land before it loads that page).
+  bf16x8 kf[16], vf[16];
+  if (writer && pi == last_page) {
+    decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
+    vm_wait<0>();
+  }
+  if (has_page) {
+    const bf16x8* kb = kaddr(pi);
+    const bf16x8* vb = vaddr(pi);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) kf[i] = __builtin_nontemporal_load(kb + i * 64);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) vf[i] = __builtin_nontemporal_load(vb + i * 64);
+  }
+  if (writer && pi != last_page) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
   bf16x8 qf[4];
   if constexpr (FUSED) {
     const int hh = hn < n_rep ? hn : 0;
     const int d0 = 8 * (lane >> 4);
-    const u16* qp = fz.qkv + (int64_t)tok * fz.ldqkv + (int64_t)(g * n_rep + hh) * HEAD_DIM + d0;
+    const int qcol = (g * n_rep + hh) * HEAD_DIM + d0;
     float x[4][8];
     float ss = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const u16x8 r = *(const u16x8*)(qp + ks * 32);
+      qkv8(fz, b.M, tok, qcol + ks * 32, x[ks]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        x[ks][j] = bf2f(r[j]);
-        ss += x[ks][j] * x[ks][j];
-      }
+      for (int j = 0; j < 8; ++j) ss += x[ks][j] * x[ks][j];
     }
     const float inv = 1.0f / sqrtf(sum_q4(ss) / 128.0f + fz.eps);
 #pragma unroll
@@ -205,26 +274,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
   f32x4 o[8];
 #pragma unroll
   for (int db = 0; db < 8; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
-  const int lim = ctx - 1;
-  int pi = cp0 + wave;
-  if (pi < cp1) {
-    bf16x8 kf[16], vf[16];
-    auto kaddr = [&](int p) {
-      return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 0) * KV + g) * KV_BLOCK_ELEMS) + lane;
-    };
-    auto vaddr = [&](int p) {
-      return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 1) * KV + g) * KV_BLOCK_ELEMS) + lane;
-    };
-    if (writer && pi == last_page) vm_wait<0>();  // own K/V stores landed before the page loads
-    {
-      const bf16x8* kb = kaddr(pi);
-      const bf16x8* vb = vaddr(pi);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) kf[i] = __builtin_nontemporal_load(kb + i * 64);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) vf[i] = __builtin_nontemporal_load(vb + i * 64);
-    }
+  if (has_page) {
     for (;;) {
       const int nxt = pi + NW;
       const bool more = nxt < cp1;
@@ -440,8 +490,9 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 
 void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
                               const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
-                              float scale, u16* out, float* ws, hipStream_t s) {
-  const DecodeFuse fz = {qkv, ldqkv, qn_w, kn_w, cos_t, sin_t, eps};
+                              float scale, u16* out, float* ws, hipStream_t s, const float* part,
+                              const float* ssq, int ksl, int K) {
+  const DecodeFuse fz = {qkv, ldqkv, qn_w, kn_w, cos_t, sin_t, eps, part, ssq, ksl, K};
   attn_decode_go<true>(nullptr, kv_layer, b, H, KV, scale, out, ws, s, fz);
 }
 

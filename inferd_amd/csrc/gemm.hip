@@ -39,6 +39,13 @@ struct DecodeArgs {
   int64_t ldr;
   unsigned long long* keys;  // EPI_ARGMAX partial keys [n_tiles][M]
   float eps;                 // NORM: RMSNorm epsilon
+  // EPI_PARTIAL (K split over gridDim.y slices, reduced by the consumer): slice y covers
+  // k-tiles [y * KT / gridDim.y, (y + 1) * KT / gridDim.y); it writes its fp32 accumulator
+  // to part[y][row][col] (row stride ldp) and, with NORM, its rows' sums of squares to
+  // ssq[y][row] -- both unscaled.
+  float* part;
+  int64_t ldp;
+  float* ssq;
 };
 
 template <int MT, int S, int NW, int TW, int D, int EPI, bool NORM>
@@ -46,17 +53,20 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
   __shared__ float sm_ss[NORM ? NW : 1][MT * 16];
-  const int KT = g.KT, M = g.M;
+  const int M = g.M;
   const int nt = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bf16x8* w0 = (const bf16x8*)(g.Wp + (int64_t)nt * KT * 512) + lane;
-  const bf16x8* w1 = (const bf16x8*)(g.Wp + (int64_t)(nt + g.n_tiles) * KT * 512) + lane;
+  // K range of this workgroup (all of K unless EPI_PARTIAL splits it over gridDim.y)
+  const int kt0 = (EPI == EPI_PARTIAL) ? (int)blockIdx.y * (g.KT / (int)gridDim.y) : 0;
+  const int KT = (EPI == EPI_PARTIAL) ? g.KT / (int)gridDim.y : g.KT;
+  const bf16x8* w0 = (const bf16x8*)(g.Wp + ((int64_t)nt * g.KT + kt0) * 512) + lane;
+  const bf16x8* w1 = (const bf16x8*)(g.Wp + ((int64_t)(nt + g.n_tiles) * g.KT + kt0) * 512) + lane;
   const u16* a[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int row = mt * 16 + (lane & 15);
     row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
-    a[mt] = g.A + (int64_t)row * g.lda + 8 * (lane >> 4);
+    a[mt] = g.A + (int64_t)row * g.lda + 8 * (lane >> 4) + kt0 * 32;
   }
   f32x4 acc[S][MT];
 #pragma unroll
@@ -151,6 +161,23 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   }
   const int mt = p >> 6, ln = p & 63;
   const int col = nt * 16 + (ln & 15);
+  if constexpr (EPI == EPI_PARTIAL) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = mt * 16 + 4 * (ln >> 4) + r;
+      if (row >= M) continue;
+      g.part[((int64_t)blockIdx.y * M + row) * g.ldp + col] = v[0][r];
+      if constexpr (NORM) {
+        if (nt == 0 && (ln & 15) == 0) {
+          float t = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) t += sm_ss[w][row];
+          g.ssq[blockIdx.y * M + row] = t;
+        }
+      }
+    }
+    return;
+  }
   if constexpr (NORM) {
     // folded RMSNorm: out = rsqrt(mean(x^2) + eps) * (x @ (W * w)^T)   
 #pragma unroll
@@ -159,7 +186,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
       float t = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) t += sm_ss[w][rr];
-      const float inv = 1.0f / sqrtf(t / (float)(KT * 32) + g.eps);
+      const float inv = 1.0f / sqrtf(t / (float)(g.KT * 32) + g.eps);
 #pragma unroll
       for (int s = 0; s < S; ++s) v[s][r] *= inv;
     }
@@ -223,6 +250,26 @@ static void decode_mt(const DecodeArgs& a, hipStream_t s) {
     decode_launch<3, EPI, NORM>(a, s);
   else
     decode_launch<4, EPI, NORM>(a, s);
+}
+
+// q/k/v projection of a decode step with K split over `kslices` workgroup slices and the
+// reduction (+ folded-norm scale) left to the consumer (launch_attn_decode_fused): with
+// NW = 4 the 384 x 2 workgroups of Qwen3-8B sit 3 per CU, every CU streaming the same bytes.
+void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
+                                float* part, float* ssq, float eps, hipStream_t s) {
+  DecodeArgs a = {};
+  a.A = A;
+  a.lda = lda;
+  a.Wp = Wp;
+  a.KT = K / 32;
+  a.n_tiles = N / 16;
+  a.M = M;
+  a.eps = eps;
+  a.part = part;
+  a.ldp = N;
+  a.ssq = ssq;
+  hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, true>), dim3(N / 16, kslices), dim3(256), 0, s,
+                     a);
 }
 
 // ============================================================ tiled (prefill) kernel

@@ -11,6 +11,7 @@ enum GemmEpilogue {
   EPI_RESID = 1,   // C = bf16(bf16(acc) + R)              (o_proj / down_proj + residual)
   EPI_SILU = 2,    // C = bf16(bf16(silu(bf16(g))) * bf16(u)) with [gate; up] packed weight
   EPI_ARGMAX = 3,  // per-row partial argmax keys of bf16(acc) (+ optional bf16 logits in C)
+  EPI_PARTIAL = 4, // internal: fp32 K-slice partials (+ row sums of squares), reduced by the consumer
 };
 
 // elementwise.hip
@@ -46,6 +47,10 @@ struct RowNorm {
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
                  const RowNorm* norm = nullptr);
+// decode q/k/v with K split over `kslices` (M <= 16, NORM folded): part [kslices][M][N] fp32,
+// ssq [kslices][M] fp32; the fused decode attention reduces them
+void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
+                                float* part, float* ssq, float eps, hipStream_t s);
 // rs[row] = 1 / sqrt(mean(x[row][:K]^2) + eps)
 void launch_row_inv_rms(const u16* x, int64_t ldx, int M, int K, float eps, float* rs, hipStream_t s);
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
@@ -69,9 +74,12 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 // Decode attention with the token's QK-norm + RoPE + K/V cache write fused in (replaces
 // launch_qk_norm_rope_kv + launch_attn_decode on the decode path): qkv is the raw
 // [M][(H+2KV)*128] projection output.
+// With `part` non-null the q/k/v come from launch_gemm_decode_partial's fp32 K-slices
+// (part [ksl][M][ldqkv], ssq [ksl][M], K = hidden) instead of the bf16 rows `qkv`.
 void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
                               const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
-                              float scale, u16* out, float* ws, hipStream_t s);
+                              float scale, u16* out, float* ws, hipStream_t s, const float* part = nullptr,
+                              const float* ssq = nullptr, int ksl = 0, int K = 0);
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx);
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
                          float scale, u16* out, hipStream_t s);

@@ -69,6 +69,8 @@ const uint32_t T_EMBED = 0xFFFF0000u, T_NORM = 0xFFFF0001u, T_LM = 0xFFFF0002u;
 const float LINEAR_SCALE = 0.034641016151377546f;  // float32(0.02 * sqrt(3))
 const float NORM_SCALE = 0.1f;
 
+#define QKV_KSL_MAX 4  // decode q/k/v K-slices (qkv_split)
+
 // kernel classes timed by inferd_span_profile_* (order = INFERD_PROF_* in the header)
 enum { PROF_NORM = 0, PROF_QKV, PROF_ROPE, PROF_ATTN, PROF_O, PROF_GATEUP, PROF_DOWN, PROF_LMHEAD, PROF_NCLS };
 
@@ -94,6 +96,8 @@ struct InferdSpan {
   float* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
   float* rs_ws = nullptr;  // folded-norm row scales of the prefill GEMMs [max_tokens]
+  float* qkv_part = nullptr;  // decode split-K q/k/v partials [QKV_KSL_MAX][16][qkv_rows]
+  float* qkv_ssq = nullptr;   // and their row sums of squares [QKV_KSL_MAX][16]
   unsigned long long* argmax_partial = nullptr;
   int32_t* err = nullptr;
   std::vector<void*> allocs;
@@ -214,6 +218,8 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
   SALLOC(s->rs_ws, (size_t)c.max_tokens * 4);
+  SALLOC(s->qkv_part, (size_t)QKV_KSL_MAX * 16 * s->qkv_rows() * 4);
+  SALLOC(s->qkv_ssq, (size_t)QKV_KSL_MAX * 16 * 4);
   SALLOC(s->err, 256);
   if (hipMemset(s->err, 0, 4) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(INFERD_ERR_HIP, "init sync failed"));
@@ -367,6 +373,15 @@ static bool fuse_decode_rope() {
   return !(e && *e == '0');
 }
 
+// Decode q/k/v GEMM K-slices (reduced inside the fused attention); INFERD_QKV_SPLIT=1 keeps
+// the single-pass bf16 GEMM.  Needs M <= 16 and K/32 divisible by 4 * slices.
+static int qkv_split(int K) {
+  const char* e = getenv("INFERD_QKV_SPLIT");
+  int k = e && *e ? atoi(e) : 2;
+  if (k < 1 || k > QKV_KSL_MAX || (K / 32) % (4 * k)) k = 1;
+  return k;
+}
+
 extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const int32_t* ids,
                                    const void* x_in, void* x_out, int32_t* next_ids, void* logits,
                                    void* layer_out, void* stream) {
@@ -403,13 +418,22 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
     u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
+    const bool fused = b->decode && fuse_decode_rope();
+    const int ksl = (fused && M <= 16) ? qkv_split(h) : 1;
     pe = s->prof_begin(PROF_QKV, st);
-    launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &rn);
+    if (ksl > 1)
+      launch_gemm_decode_partial(x, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, s->qkv_ssq, c.rms_eps, st);
+    else
+      launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &rn);
     s->prof_end(pe, st);
-    if (b->decode && fuse_decode_rope()) {  // QK-norm + RoPE + cache write inside attention
+    if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
-      launch_attn_decode_fused(s->qkv, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
-                               scale, s->attn, s->attn_ws, st);
+      if (ksl > 1)
+        launch_attn_decode_fused(nullptr, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
+                                 scale, s->attn, s->attn_ws, st, s->qkv_part, s->qkv_ssq, ksl, h);
+      else
+        launch_attn_decode_fused(s->qkv, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
+                                 scale, s->attn, s->attn_ws, st);
       s->prof_end(pe, st);
     } else {
       pe = s->prof_begin(PROF_ROPE, st);
