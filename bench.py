@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing pass")
     p.add_argument("--profile-steps", type=int, default=8, help="eager event-instrumented decode steps")
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
+    p.add_argument("--spans", default="", help="comma-separated layers per stage (BASELINE config 4: an uneven, "
+                                                "balance.py-like split, e.g. 5,27,4); default: even split")
     p.add_argument("--mode", choices=("decode", "prefill"), default="decode",
                    help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline)")
     p.add_argument("--prefill-layers", type=int, default=8)
@@ -206,7 +208,12 @@ def main():
 
     d = MODELS[args.model]
     B, ctx, K, W = args.batch, args.ctx, args.steps, args.warmup
-    spans = even_split(d.layers, world)
+    if args.spans:
+        sizes = [int(v) for v in args.spans.split(",")]
+        assert len(sizes) == world and sum(sizes) == d.layers, f"--spans {args.spans}: need {world} stages, {d.layers} layers"
+        spans = [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
+    else:
+        spans = even_split(d.layers, world)
     first, n_layers = spans[rank]
     n_mb = world                                   # microbatches in flight
     st = P.PipelineStage(d, rank, world, first, n_layers, device=dev, seed=args.seed,
@@ -244,6 +251,13 @@ def main():
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, t_prefill = float(t[0]), float(t[1])
+    # per-stage compute per microbatch step (event-timed kernels) -> imbalance / hand-off
+    stage_ms = torch.zeros(world, dtype=torch.float64, device=dev)
+    if prof:
+        stage_ms[rank] = sum(ms for ms, n in prof.values()) / (args.profile_steps * n_mb)
+    if dist:
+        dist.all_reduce(stage_ms, op=dist.ReduceOp.SUM)
+    stage_ms = [float(v) for v in stage_ms.cpu()]
 
     tokens = K * n_mb * B
     value = tokens / elapsed
@@ -300,6 +314,14 @@ def main():
                               "peak": HBM_PEAK_GBS, "unit": "GB/s per GPU",
                               "frac": round(sb / (ms_per_step * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4)},
             "kernels": kernels,
+            "stages": None if not prof else {
+                "spans": [n for _, n in spans],
+                "compute_ms_per_microbatch": [round(v, 4) for v in stage_ms],
+                "tick_ms": round(ms_per_step / n_mb, 4),
+                "bubble_frac": round(1 - sum(stage_ms) / (world * max(stage_ms)), 4) if max(stage_ms) > 0 else None,
+                "handoff_ms_per_tick": round(ms_per_step / n_mb - max(stage_ms), 4),
+                "note": "compute from event-timed eager kernels (slightly above in-graph time); tick = "
+                        "ms_per_step / microbatches; handoff = tick - slowest stage"},
             "prefill": {"tokens": n_mb * B * ctx, "seconds": round(t_prefill, 3),
                         "tokens_per_s": round(n_mb * B * ctx / t_prefill, 1)},
             "cpu_baseline": None,

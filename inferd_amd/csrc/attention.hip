@@ -202,36 +202,46 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
   const int cp0 = (chunk * n_pages) / nc, cp1 = ((chunk + 1) * n_pages) / nc;
   const int tok = b.seq_start[bseq + 1] - 1;
   const int hn = lane & 15;
-  // the wave that reads the token's page (the sequence's last page) writes its K/V
-  const int last_page = n_pages - 1;
-  const bool writer = FUSED && chunk == nc - 1 && wave == (last_page - cp0) % NW;
+  // Work items are 32-token half pages (K: 8 fragments, V: the 8 fragments of one kt), so
+  // a chunk's 16-17 pages spread over the 8 waves in 4-5 items each instead of 2-3 pages:
+  // the slowest wave sets the workgroup's time.  Halves past the last token are skipped.
   const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
   const int lim = ctx - 1;
-  int pi = cp0 + wave;
-  const bool has_page = pi < cp1;
-  auto kaddr = [&](int p) {
-    return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 0) * KV + g) * KV_BLOCK_ELEMS) + lane;
+  const int u_begin = 2 * cp0, u_end = min(2 * cp1, (lim >> 5) + 1);
+  const int u_tok = lim >> 5;  // the token's own half page (last chunk)
+  const bool writer = FUSED && chunk == nc - 1 && wave == (u_tok - u_begin) % NW;
+  int u = u_begin + wave;
+  const bool has_item = u < u_end;
+  auto kaddr = [&](int uu) {
+    return (const bf16x8*)(kv + ((int64_t)(bt[uu >> 1] * 2 + 0) * KV + g) * KV_BLOCK_ELEMS) + (uu & 1) * 512 + lane;
   };
-  auto vaddr = [&](int p) {
-    return (const bf16x8*)(kv + ((int64_t)(bt[p] * 2 + 1) * KV + g) * KV_BLOCK_ELEMS) + lane;
+  auto vaddr = [&](int uu) {
+    return (const bf16x8*)(kv + ((int64_t)(bt[uu >> 1] * 2 + 1) * KV + g) * KV_BLOCK_ELEMS) + (uu & 1) * 512 + lane;
   };
-  // The first page's K/V loads are issued before the token's q/k/v arithmetic so their
-  // latency overlaps it; the writer stores the token's K/V first only when that first page
-  // is the token's own page (its stores must land before it loads that page).
-  bf16x8 kf[16], vf[16];
-  if (writer && pi == last_page) {
+  // The first two items' K/V loads (a 2-deep register ring: item j+2 is issued as soon as
+  // item j's registers are consumed, so each wave always has two half pages in flight) are
+  // issued before the token's q/k/v arithmetic so their latency overlaps it.  The writer
+  // stores the token's K/V first when one of those items holds the token (its stores must
+  // land before it loads that half page), otherwise right after.
+  bf16x8 kf[2][8], vf[2][8];
+  const int u1 = u + NW;
+  const bool tok_early = writer && (u == u_tok || u1 == u_tok);
+  if (tok_early) {
     decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
     vm_wait<0>();
   }
-  if (has_page) {
-    const bf16x8* kb = kaddr(pi);
-    const bf16x8* vb = vaddr(pi);
+  auto load_item = [&](auto ST, int uu) {
+    constexpr int st = decltype(ST)::value;
+    const bf16x8* kb = kaddr(uu);
+    const bf16x8* vb = vaddr(uu);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) kf[i] = __builtin_nontemporal_load(kb + i * 64);
+    for (int i = 0; i < 8; ++i) kf[st][i] = __builtin_nontemporal_load(kb + i * 64);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) vf[i] = __builtin_nontemporal_load(vb + i * 64);
-  }
-  if (writer && pi != last_page) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
+    for (int i = 0; i < 8; ++i) vf[st][i] = __builtin_nontemporal_load(vb + i * 64);
+  };
+  if (has_item) load_item(std::integral_constant<int, 0>{}, u);
+  if (u1 < u_end) load_item(std::integral_constant<int, 1>{}, u1);
+  if (writer && !tok_early) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
   bf16x8 qf[4];
   if constexpr (FUSED) {
     const int hh = hn < n_rep ? hn : 0;
@@ -274,78 +284,75 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
   f32x4 o[8];
 #pragma unroll
   for (int db = 0; db < 8; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if (has_page) {
-    for (;;) {
-      const int nxt = pi + NW;
-      const bool more = nxt < cp1;
-      const int page_tok0 = pi * KV_PAGE;
-      f32x4 sc[4];
+  // one item with its registers in ring stage ST; returns false after the wave's last item
+  auto item = [&](auto ST) -> bool {
+    constexpr int st = decltype(ST)::value;
+    const int nxt = u + 2 * NW;  // refills this stage
+    const bool more = nxt < u_end;
+    const int tok0 = u * 32;
+    f32x4 sc[2];
 #pragma unroll
-      for (int tb = 0; tb < 4; ++tb) {
-        sc[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t2 = 0; t2 < 2; ++t2) {
+      sc[t2] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) sc[tb] = mfma16(kf[tb * 4 + ks], qf[ks], sc[tb]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (more) {
-        if (writer && nxt == last_page) vm_wait<0>();
-        const bf16x8* kb = kaddr(nxt);
+      for (int ks = 0; ks < 4; ++ks) sc[t2] = mfma16(kf[st][t2 * 4 + ks], qf[ks], sc[t2]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      if (writer && nxt == u_tok) vm_wait<0>();
+      const bf16x8* kb = kaddr(nxt);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) kf[i] = __builtin_nontemporal_load(kb + i * 64);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (page_tok0 + KV_PAGE - 1 > lim) {  // the sequence's last page: causal/length mask
+      for (int i = 0; i < 8; ++i) kf[st][i] = __builtin_nontemporal_load(kb + i * 64);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (tok0 + 31 > lim) {  // the half page holding the token: length mask
 #pragma unroll
-        for (int tb = 0; tb < 4; ++tb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int t = page_tok0 + tb * 16 + 4 * (lane >> 4) + r;
-            sc[tb][r] = (t <= lim) ? sc[tb][r] : -INFINITY;
-          }
-      }
-      float pmax = sc[0][0];
-#pragma unroll
-      for (int tb = 0; tb < 4; ++tb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (tb | r) pmax = fmaxf(pmax, sc[tb][r]);
-      const float m_new = fmaxf(m_i, max_q4(pmax) * scale_log2);
-      if (__builtin_amdgcn_ballot_w64(m_new > m_i)) {
-        const float alpha = exp2_raw(m_i - m_new);
-        l_i *= alpha;
-#pragma unroll
-        for (int db = 0; db < 8; ++db) o[db] *= alpha;
-        m_i = m_new;
-      }
-      const float mneg = -m_i;
-#pragma unroll
-      for (int tb = 0; tb < 4; ++tb)
+      for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2_raw(fmaf(sc[tb][r], scale_log2, mneg));
-          sc[tb][r] = p;
-          l_i += p;  // this lane's share; reduced over the query's 4 lanes after the loop
+          const int t = tok0 + t2 * 16 + 4 * (lane >> 4) + r;
+          sc[t2][r] = (t <= lim) ? sc[t2][r] : -INFINITY;
         }
+    }
+    const float pmax = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                             fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+    const float m_new = fmaxf(m_i, max_q4(pmax) * scale_log2);
+    if (__builtin_amdgcn_ballot_w64(m_new > m_i)) {
+      const float alpha = exp2_raw(m_i - m_new);
+      l_i *= alpha;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        bf16x8 pf;
+      for (int db = 0; db < 8; ++db) o[db] *= alpha;
+      m_i = m_new;
+    }
+    const float mneg = -m_i;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pf[j] = (__bf16)sc[2 * kt][j];
-          pf[4 + j] = (__bf16)sc[2 * kt + 1][j];
-        }
+    for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-        for (int db = 0; db < 8; ++db) o[db] = mfma16(vf[kt * 8 + db], pf, o[db]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (!more) break;
-      {
-        const bf16x8* vb = vaddr(nxt);
+      for (int r = 0; r < 4; ++r) sc[t2][r] = exp2_raw(fmaf(sc[t2][r], scale_log2, mneg));
+    // this lane's share of the row sum; reduced over the query's 4 lanes after the loop
+    l_i += ((sc[0][0] + sc[0][1]) + (sc[0][2] + sc[0][3])) + ((sc[1][0] + sc[1][1]) + (sc[1][2] + sc[1][3]));
+    bf16x8 pf;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) vf[i] = __builtin_nontemporal_load(vb + i * 64);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      pi = nxt;
+    for (int j = 0; j < 4; ++j) {
+      pf[j] = (__bf16)sc[0][j];
+      pf[4 + j] = (__bf16)sc[1][j];
+    }
+#pragma unroll
+    for (int db = 0; db < 8; ++db) o[db] = mfma16(vf[st][db], pf, o[db]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      const bf16x8* vb = vaddr(nxt);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vf[st][i] = __builtin_nontemporal_load(vb + i * 64);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    u += NW;
+    return u < u_end;
+  };
+  if (has_item) {
+    for (;;) {
+      if (!item(std::integral_constant<int, 0>{})) break;
+      if (!item(std::integral_constant<int, 1>{})) break;
     }
   }
   // merge the NW waves through LDS
