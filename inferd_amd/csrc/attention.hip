@@ -189,8 +189,6 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
                                                       DecodeFuse fz) {
   __shared__ float sm_m[NW][16], sm_l[NW][16];
   __shared__ float sm_o[NW][16][HEAD_DIM + 4];
-  __shared__ float sm_f[MAX_DECODE_CHUNKS][16], sm_lc[MAX_DECODE_CHUNKS][16];
-  __shared__ float sm_L[16];
   __shared__ int sm_last;
   const int chunk = blockIdx.x, g = blockIdx.y, bseq = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -399,40 +397,30 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
     const unsigned prev =
         __hip_atomic_fetch_add(&counters[bseq * KV + g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sm_last = (prev == (unsigned)(nc - 1));
-    if (sm_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&counters[bseq * KV + g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (sm_last) __hip_atomic_store(&counters[bseq * KV + g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (!sm_last) return;
-  for (int idx = threadIdx.x; idx < nc * n_rep; idx += NW * 64) {
-    const int c = idx / n_rep, n = idx % n_rep;
-    sm_f[c][n] = base[(int64_t)c * stride + n * PART_STRIDE + HEAD_DIM];
-    sm_lc[c][n] = base[(int64_t)c * stride + n * PART_STRIDE + HEAD_DIM + 1];
-  }
-  __syncthreads();
-  if (threadIdx.x < n_rep) {
-    const int n = threadIdx.x;
-    float M = -INFINITY;
-    for (int c = 0; c < nc; ++c) M = fmaxf(M, sm_f[c][n]);
-    float L = 0.f;
-    for (int c = 0; c < nc; ++c) {
-      const float f = exp2f(sm_f[c][n] - M);
-      sm_f[c][n] = f;
-      L += sm_lc[c][n] * f;
-    }
-    sm_L[n] = L;
-  }
-  __syncthreads();
+  // Last arriver: every partial was stored write-through (sc1) and drained before its
+  // workgroup's ticket add, and every load of one here is an sc1 load, so no acquire fence
+  // is needed (MI355X_MICROARCH.md, visibility "Valid forms", row 1: one workgroup per CU,
+  // unsharded counter, last adder told by the returned value).  One pass per (head, dim),
+  // chunks merged in fixed order (deterministic).
   for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += NW * 64) {
     const int n = idx / HEAD_DIM, d = idx % HEAD_DIM;
-    const float* pc = base + n * PART_STRIDE + d;
-    float acc = 0.f;
-#pragma unroll 16
-    for (int c = 0; c < nc; ++c) acc += pc[(int64_t)c * stride] * sm_f[c][n];
-    op[n * HEAD_DIM + d] = f2bf(acc / sm_L[n]);
+    const float* pn = base + n * PART_STRIDE;
+    float M = -INFINITY;
+    for (int c = 0; c < nc; ++c)
+      M = fmaxf(M, __hip_atomic_load(pn + (int64_t)c * stride + HEAD_DIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    float acc = 0.f, L = 0.f;
+    for (int c = 0; c < nc; ++c) {
+      const float* pc = pn + (int64_t)c * stride;
+      const float f =
+          exp2f(__hip_atomic_load(pc + HEAD_DIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - M);
+      L += __hip_atomic_load(pc + HEAD_DIM + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
+      acc += __hip_atomic_load(pc + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
+    }
+    op[n * HEAD_DIM + d] = f2bf(acc / L);
   }
 }
 
