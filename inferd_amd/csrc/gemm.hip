@@ -537,7 +537,22 @@ __global__ __launch_bounds__(512) void gemm_tiled256_kernel(
 //  * blockIdx is remapped XCD-aware (blocks sharing an XCD get consecutive tiles) and
 //    grouped 8 row-blocks deep so an XCD's concurrent blocks share A rows and W columns.
 #define RING_SLOTS 10
-#define RING_AHEAD 6
+
+// vm_wait with a run-time count (even values 0..14; -1 = no wait); a constant argument
+// folds to the single s_waitcnt
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  switch (n) {
+    case 0: vm_wait<0>(); break;
+    case 2: vm_wait<2>(); break;
+    case 4: vm_wait<4>(); break;
+    case 6: vm_wait<6>(); break;
+    case 8: vm_wait<8>(); break;
+    case 10: vm_wait<10>(); break;
+    case 12: vm_wait<12>(); break;
+    case 14: vm_wait<14>(); break;
+    default: break;
+  }
+}
 
 
 // Tail split (SplitTail): when the tile count leaves a partial last round on an XCD
@@ -555,7 +570,7 @@ struct SplitTail {
   unsigned* cnt;        // [2][8 * rem] arrival tickets, done counters (zero between launches)
 };
 
-template <int EPI>
+template <int EPI, bool KEEPB>
 __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
     u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
@@ -641,7 +656,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 areg[4][2], breg[2][2];
+  // KEEPB: both B sub-tiles stay in registers for the whole K-step (B0 is not re-read by
+  // the last quadrant), so every slot's last read is no later than its own index and the
+  // look-ahead grows from ring - 4 to ring - 2 half-tiles.
+  constexpr int D = KEEPB ? RING_SLOTS - 2 : RING_SLOTS - 4;
+  bf16x8 areg[4][2], breg[2][2][2];  // breg[quadrant column][nt][ks]
 
   auto read_a = [&](int slot) {
     const char* base = lds + slot * 16384;
@@ -655,15 +674,17 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
       }
     }
   };
-  auto read_b = [&](int slot) {
+  auto read_b = [&](auto QC, int slot) {
+    constexpr int qc = decltype(QC)::value;
     const char* base = lds + slot * 16384 + lane * 16;
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) breg[nt][ks] = *(const bf16x8*)(base + ((wc * 2 + nt) * 2 + ks) * 1024);
+      for (int ks = 0; ks < 2; ++ks) breg[qc][nt][ks] = *(const bf16x8*)(base + ((wc * 2 + nt) * 2 + ks) * 1024);
   };
   auto mfmas = [&](auto QR, auto QC) {
     constexpr int qr = decltype(QR)::value, qc = decltype(QC)::value;
+    constexpr int bq = KEEPB ? qc : 0;  // without KEEPB one B register set is reused
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -671,63 +692,74 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt)
-          acc[qr * 4 + mt][qc * 2 + nt] = mfma16(breg[nt][ks], areg[mt][ks], acc[qr * 4 + mt][qc * 2 + nt]);
+          acc[qr * 4 + mt][qc * 2 + nt] = mfma16(breg[bq][nt][ks], areg[mt][ks], acc[qr * 4 + mt][qc * 2 + nt]);
     __builtin_amdgcn_s_setprio(0);
   };
   auto wrap = [](int x) { return x >= RING_SLOTS ? x - RING_SLOTS : x; };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
 
-  // one phase: reads, optional issue of half-tile `s_issue`, counted wait, barrier, MFMAs, barrier
-  auto phase = [&](auto J, int rb, int s_issue, auto VM) {
+  // One phase P = 4t + j: reads, issue of half-tile P + D (when it exists; its kind
+  // (j + D) & 3 is a compile-time constant), counted wait, barrier, MFMAs, barrier.
+  // VM >= 0: that constant wait; VM == -2: the run-time wait of wait_at(P) (tail steps).
+  auto wait_at = [&](int P) {  // what phase P+1 reads: half-tile P+2 (quadrants 0-2)
+    if (P >= S - 1 || ((P + 1) & 3) == 3) return -1;
+    const int last = P + D < S - 1 ? P + D : S - 1;
+    return 2 * (last - (P + 2));
+  };
+  auto phase = [&](auto J, auto VM, int t, int rb) {
     constexpr int j = decltype(J)::value;
-    constexpr int vm = decltype(VM)::value;
-    if constexpr (j == 0) { read_a(rb); read_b(wrap(rb + 1)); }
-    if constexpr (j == 1) read_b(wrap(rb + 2));
+    constexpr int vmc = decltype(VM)::value;
+    const int P = 4 * t + j;
+    if constexpr (j == 0) { read_a(rb); read_b(Q0{}, wrap(rb + 1)); }
+    if constexpr (j == 1) read_b(std::integral_constant<int, KEEPB ? 1 : 0>{}, wrap(rb + 2));
     if constexpr (j == 2) read_a(wrap(rb + 3));
-    if constexpr (j == 3) read_b(wrap(rb + 1));
-    if (s_issue >= 0) issue_s(s_issue);
-    if constexpr (vm >= 0) vm_wait<vm>();
+    if constexpr (j == 3 && !KEEPB) read_b(Q0{}, wrap(rb + 1));
+    const int si = P + D;
+    if (vmc >= 0 || si < S) issue((j + D) & 3, si >> 2, si % RING_SLOTS);
+    if constexpr (vmc >= 0)
+      vm_wait<vmc>();
+    else
+      vm_wait_rt(wait_at(P));
     raw_barrier();
-    if constexpr (j == 0) mfmas(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-    if constexpr (j == 1) mfmas(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
-    if constexpr (j == 2) mfmas(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
-    if constexpr (j == 3) mfmas(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+    if constexpr (j == 0) mfmas(Q0{}, Q0{});
+    if constexpr (j == 1) mfmas(Q0{}, Q1{});
+    if constexpr (j == 2) mfmas(Q1{}, Q1{});
+    if constexpr (j == 3) mfmas(Q1{}, Q0{});
     raw_barrier();
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  using VNONE = std::integral_constant<int, -1>;
+  using VSTEADY = std::integral_constant<int, 2 * (D - 2)>;
+  using VTAIL = std::integral_constant<int, -2>;
 
-  // prologue: half-tiles 0..5 in flight, wait for 0 and 1 (A0, B0 of step 0)
+  // prologue: half-tiles 0..D-1 in flight, wait for 0 and 1 (A0, B0 of step 0)
 #pragma unroll
-  for (int s = 0; s < RING_AHEAD; ++s) issue(s & 3, s >> 2, s);
-  vm_wait<8>();
+  for (int s = 0; s < D; ++s) issue(s & 3, s >> 2, s);
+  vm_wait<2 * (D - 2)>();
   raw_barrier();
   if (wr == 1) raw_barrier();  // stagger: waves 4-7 one barrier behind
 
   int rb = 0;  // slot of the current step's A0 half-tile = (4t) % 10
   int t = 0;
-  // steady state: every phase issues, 4 half-tiles stay in flight after each wait
-  for (; t < nK - 2; ++t) {
-    const int s0 = 4 * t + RING_AHEAD;
-    phase(I0{}, rb, s0, std::integral_constant<int, 8>{});
-    phase(I1{}, rb, s0 + 1, std::integral_constant<int, 8>{});
-    phase(I2{}, rb, s0 + 2, std::integral_constant<int, 8>{});
-    phase(I3{}, rb, s0 + 3, std::integral_constant<int, 8>{});
+  // steady state: all four phases issue (4t + 3 + D <= S - 1), constant wait
+  for (; 4 * t + 3 + D <= S - 1; ++t) {
+    phase(I0{}, VSTEADY{}, t, rb);
+    phase(I1{}, VSTEADY{}, t, rb);
+    phase(I2{}, VSTEADY{}, t, rb);
+    phase(I3{}, VSTEADY{}, t, rb);
     rb = wrap(rb + 4);
   }
-  // step nK-2: issues S-2, S-1 then drains
-  phase(I0{}, rb, S - 2, std::integral_constant<int, 8>{});
-  phase(I1{}, rb, S - 1, std::integral_constant<int, 8>{});
-  phase(I2{}, rb, -1, std::integral_constant<int, 6>{});
-  phase(I3{}, rb, -1, std::integral_constant<int, 4>{});
-  rb = wrap(rb + 4);
-  // step nK-1
-  phase(I0{}, rb, -1, std::integral_constant<int, 2>{});
-  phase(I1{}, rb, -1, std::integral_constant<int, 0>{});
-  phase(I2{}, rb, -1, VNONE{});
-  phase(I3{}, rb, -1, VNONE{});
+  // tail: the last (D + 3) / 4 steps issue what is left and drain with exact counts
+  for (; t < nK; ++t) {
+    phase(I0{}, VTAIL{}, t, rb);
+    phase(I1{}, VTAIL{}, t, rb);
+    phase(I2{}, VTAIL{}, t, rb);
+    phase(I3{}, VTAIL{}, t, rb);
+    rb = wrap(rb + 4);
+  }
   if (wr == 0) raw_barrier();  // close the stagger
 
   if (nsl > 1) {  // ---- tail split: publish or combine
@@ -767,36 +799,29 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
       __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    f32x4 sum[8][4];
+    // fixed slice order, in place (a second 128-register accumulator would spill)
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sl = 0; sl < nsl; ++sl) {  // fixed slice order
-      if (sl == slice) {
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) sum[i][j] += acc[i][j];
-      } else {
-        const unsigned long long* src = (const unsigned long long*)(part + (size_t)sl * 65536);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
+        for (int hh = 0; hh < 2; ++hh) {
+          float v0 = 0.f, v1 = 0.f;
+          for (int sl = 0; sl < nsl; ++sl) {
+            if (sl == slice) {
+              v0 += acc[i][j][2 * hh];
+              v1 += acc[i][j][2 * hh + 1];
+            } else {
+              const unsigned long long* src = (const unsigned long long*)(part + (size_t)sl * 65536);
               const unsigned long long v = __hip_atomic_load(src + ((i * 4 + j) * 2 + hh) * 512 + threadIdx.x,
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              sum[i][j][2 * hh] += __uint_as_float((unsigned)v);
-              sum[i][j][2 * hh + 1] += __uint_as_float((unsigned)(v >> 32));
+              v0 += __uint_as_float((unsigned)v);
+              v1 += __uint_as_float((unsigned)(v >> 32));
             }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = sum[i][j];
+          }
+          acc[i][j][2 * hh] = v0;
+          acc[i][j][2 * hh + 1] = v1;
+        }
   }
 
   // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
@@ -853,6 +878,23 @@ static float* g_split_ws = nullptr;
 static size_t g_split_ws_bytes = 0;
 static unsigned* g_split_cnt = nullptr;
 static int g_split_cnt_n = 0;
+
+static int env_or(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
+template <int EPI>
+static void ring_launch(bool keepb, int grid, hipStream_t s, const u16* A, int64_t lda, const u16* Wp, int KT, int ntw,
+                        u16* C, int64_t ldc, const u16* R, int64_t ldr, int M, const float* rs, int gm, int gn,
+                        const SplitTail& st) {
+  if (keepb)
+    hipLaunchKernelGGL((gemm_ring256_kernel<EPI, true>), dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                       ldr, M, rs, gm, gn, st);
+  else
+    hipLaunchKernelGGL((gemm_ring256_kernel<EPI, false>), dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                       ldr, M, rs, gm, gn, st);
+}
 
 static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
   SplitTail st = {1, 0, 0, 0, nullptr, nullptr};
@@ -922,18 +964,17 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
     const SplitTail st = plan_split_tail(gm * gn, K / 64, s);
     const int grid = st.split > 1 ? 8 * st.units_per_xcd : gm * gn;
+    // INFERD_GEMM_KEEPB=0 selects the look-ahead-6 schedule that re-reads B0 (A/B)
+    const bool keepb = env_or("INFERD_GEMM_KEEPB", 1) != 0;
     switch (epi) {
       case EPI_NONE:
-        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_NONE>, dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                           ldr, M, rs, gm, gn, st);
+        ring_launch<EPI_NONE>(keepb, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);
         break;
       case EPI_RESID:
-        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_RESID>, dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc,
-                           R, ldr, M, rs, gm, gn, st);
+        ring_launch<EPI_RESID>(keepb, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);
         break;
       default:
-        hipLaunchKernelGGL(gemm_ring256_kernel<EPI_SILU>, dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                           ldr, M, rs, gm, gn, st);
+        ring_launch<EPI_SILU>(keepb, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);
         break;
     }
     return;
