@@ -273,7 +273,7 @@ def test_attention_decode(lib, H, KV):
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
 
 
-@pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2)])
+@pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2), (64, 8)])
 @pytest.mark.parametrize("variant", ["4", "8"])
 def test_attention_prefill(lib, monkeypatch, H, KV, variant):
     """Both prefill kernels (8-wave staggered, 4-wave) on ragged prompts, with and without

@@ -239,3 +239,51 @@ def test_decode_fused_rope_matches_separate(monkeypatch):
     e = rel_err(outs[0], outs[1])
     print(f"fused vs separate decode hidden rel err {e:.2e}")
     assert e < 2e-2
+
+
+def test_config1_q06_two_spans_greedy_dict_protocol():
+    """BASELINE config 1 on the GPU engine: Qwen3-0.6B as two 14-layer spans behind the
+    node-facing dict protocol (generated_ids -> bf16 hidden_meta -> next_token_id), greedy
+    full-recompute decode of a 32-token prompt (send_message.py:46-60 semantics), against
+    the oracle's two-span chain with the same attention semantics (SDPA)."""
+    from inferd_amd.partitioned_models import PartitionedQwen2
+    d = R.CONFIGS["qwen3-0.6b"]
+    n0 = PartitionedQwen2("qwen3-0.6b", 2, 0, f"synthetic:{SEED}:qwen3-0.6b:0:13")
+    n1 = PartitionedQwen2("qwen3-0.6b", 2, 1, f"synthetic:{SEED}:qwen3-0.6b:14:27")
+    b0 = R.RefSpan(d, SEED, 0, 13, True, False, torch.bfloat16, "sdpa")
+    b1 = R.RefSpan(d, SEED, 14, 27, False, True, torch.bfloat16, "sdpa")
+    ids = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(11)).tolist()
+    agree = checked = 0
+    for step in range(6):
+        o1 = n1.forward(n0.forward({"generated_ids": ids}))
+        lg = b1.forward(b0.forward(torch.tensor([ids])))[0, -1]
+        rid, m = int(torch.argmax(lg)), R.top2_margin(lg)
+        print(f"step {step}: gpu {o1['next_token_id']} ref {rid} margin {m:.4f}")
+        if m > MARGIN_FLOOR:
+            checked += 1
+            agree += int(o1["next_token_id"] == rid)
+            assert o1["next_token_id"] == rid, step
+        ids = ids + [rid]
+    print(f"config 1: {agree}/{checked} greedy steps above the margin floor agree")
+
+
+def test_config5_q32b_layer_prefill_vs_oracle():
+    """BASELINE config 5 dims on the prefill path: one Qwen3-32B-dims layer (64 q / 8 kv
+    heads, h 5120, I 25600) prefilling a 520-token prompt -- the ring-staged 256x256 GEMMs
+    (M >= 512), the tail split (2 x 21 tiles), the 4-wave prefill attention and the
+    QK-norm + RoPE kernel -- against the oracle layer, then 2 cached decode steps."""
+    d = R.CONFIGS["qwen3-32b"]
+    s = span("qwen3-32b", 9, 1, False, False, max_tokens=640, kv_pages=24, max_seqs=2, max_positions=1024)
+    oracle = R.RefSpan(d, SEED, 9, 9, False, False, torch.bfloat16, "sdpa")
+    g = torch.Generator().manual_seed(21)
+    x = (torch.randn(1, 520, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+    out = s.forward([("p", 520)], x=x[0])["hidden"]
+    e = rel_err(out, oracle.forward_cached("p", x)[0])
+    print(f"32B layer prefill 520: rel err {e:.2e}")
+    assert e < TOL_REL
+    for step in range(2):
+        xd = (torch.randn(1, 1, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+        out = s.forward([("p", 1)], x=xd[0])["hidden"]
+        e = rel_err(out, oracle.forward_cached("p", xd)[0])
+        print(f"32B layer decode {step}: rel err {e:.2e}")
+        assert e < TOL_REL

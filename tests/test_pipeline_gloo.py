@@ -61,15 +61,23 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_steps, q):
+def _split(d, world, sizes):
+    """layer ranges per stage: even (bench.even_split) or the given sizes (BASELINE config 4's
+    uneven, balance.py-like split; bench.py --spans)"""
+    from bench import even_split
+    if not sizes:
+        return even_split(d.layers, world)
+    return [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
+
+
+def _worker(rank, world, port, n_steps, q, sizes=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     from inferd_amd.pipeline import PipelineStage
-    from bench import even_split
     d = R.CONFIGS["tiny"]
-    first, n = even_split(d.layers, world)[rank]
+    first, n = _split(d, world, sizes)[rank]
     ex = OracleExecutor(d, first, n, rank == 0, rank == world - 1)
     B = 3
     st = PipelineStage(d, rank, world, first, n, device="cpu", seed=SEED, n_microbatches=world, batch=B,
@@ -87,11 +95,10 @@ def _worker(rank, world, port, n_steps, q):
     dist.destroy_process_group()
 
 
-def _reference(world, n_steps):
+def _reference(world, n_steps, sizes=None):
     """Single process: the same spans chained directly (bf16 hand-off, like the pipeline)."""
-    from bench import even_split
     d = R.CONFIGS["tiny"]
-    split = even_split(d.layers, world)
+    split = _split(d, world, sizes)
     spans = [R.RefSpan(d, SEED, f, f + n - 1, i == 0, i == world - 1, torch.bfloat16, "sdpa")
              for i, (f, n) in enumerate(split)]
 
@@ -114,20 +121,20 @@ def _reference(world, n_steps):
     return feeds
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_pipeline_matches_single_process(world):
+@pytest.mark.parametrize("world,sizes", [(2, None), (3, None), (3, [1, 2, 1]), (2, [3, 1])])
+def test_pipeline_matches_single_process(world, sizes):
     n_steps = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_steps, q, sizes)) for r in range(world)]
     for p in procs:
         p.start()
     rec = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    ref = _reference(world, n_steps)
+    ref = _reference(world, n_steps, sizes)
     seen = 0
     for k, m, ids in rec:
         if k == "final":
