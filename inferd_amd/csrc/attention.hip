@@ -577,19 +577,40 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
     }
 }
 
+// Block order (grid x = max_q_blocks * H per sequence, y = sequence): mode 1 (used when
+// that count is a multiple of 8) deals each XCD a contiguous range of (kv group, query block,
+// head) with the n_rep heads of a group fastest, so the heads that read the same K/V pages
+// run together on one XCD (one L2); query blocks heaviest first, so light blocks fill the
+// tail.  Mode 0: head-major, heaviest query block first.
 __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restrict__ q,
                                                            const u16* __restrict__ kv,
                                                            AttnBatch b, int H, int KV,
                                                            float scale_log2,
-                                                           u16* __restrict__ out) {
+                                                           u16* __restrict__ out, int order) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 32768];
-  const int bseq = blockIdx.z, h = blockIdx.y;
+  const int bseq = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int n_rep = H / KV, g = h / n_rep;
+  const int n_rep = H / KV;
+  const int mqb = (b.max_q_len + 127) / 128;  // query blocks per head in the grid
+  int h, qbi;
+  if (order == 1) {
+    const int n = gridDim.x, x = blockIdx.x;  // n % 8 == 0 (launcher)
+    const int wg = (x & 7) * (n >> 3) + (x >> 3);
+    const int r = wg % n_rep, t = wg / n_rep;
+    qbi = t % mqb;
+    h = (t / mqb) * n_rep + r;
+  } else {
+    h = blockIdx.x / mqb;
+    qbi = blockIdx.x % mqb;
+  }
+  const int g = h / n_rep;
   const int t0 = b.seq_start[bseq];
   const int T = b.seq_start[bseq + 1] - t0;
-  const int qb0 = blockIdx.x * 128;
-  if (qb0 >= T) return;  // uniform over the workgroup
+  const int nqb = (T + 127) / 128;
+  // heaviest (latest) query blocks first
+  const int qb = mqb - 1 - qbi;
+  if (qb >= nqb) return;  // uniform over the workgroup
+  const int qb0 = qb * 128;
   bf16x8 qf[2][4];
   int lim[2], tokrow[2];
   bool valid[2];
@@ -868,6 +889,9 @@ void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, 
                        b, H, KV, scale * LOG2E, out);
     return;
   }
-  hipLaunchKernelGGL(attn_prefill_kernel, dim3((b.max_q_len + 127) / 128, H, b.B), dim3(256), 0, s, q, kv_layer, b,
-                     H, KV, scale * LOG2E, out);
+  const int n = (b.max_q_len + 127) / 128 * H;
+  const char* e = getenv("INFERD_ATTN_ORDER");
+  const int order = (e && *e) ? atoi(e) : (n % 8 == 0 ? 1 : 0);
+  hipLaunchKernelGGL(attn_prefill_kernel, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out,
+                     (order == 1 && n % 8 == 0) ? 1 : 0);
 }
