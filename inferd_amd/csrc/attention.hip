@@ -700,15 +700,30 @@ __global__ __launch_bounds__(512, 1) void attn_prefill8_kernel(const u16* __rest
   // K slots 0-3, V slots 4-7, then this sequence's block table (read with ds_read so that no
   // vector load -- whose wait would drain the in-flight LDS-DMA -- sits in the loop)
   __shared__ __attribute__((aligned(16))) char lds[8 * 16384 + PREFILL8_MAX_PAGES * 4];
-  const int bseq = blockIdx.z, h = blockIdx.y;
+  // block order as attn_prefill_kernel (mode 1 when the grid is a multiple of 8)
+  const int bseq = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int hf = wave >> 2, kw = wave & 3;
-  const int n_rep = H / KV, g = h / n_rep;
+  const int n_rep = H / KV;
+  const int mqb = (b.max_q_len + 255) / 256;
+  int h, qbi;
+  if (gridDim.x % 8 == 0) {
+    const int n = gridDim.x, x = blockIdx.x;
+    const int wg = (x & 7) * (n >> 3) + (x >> 3);
+    const int r = wg % n_rep, t = wg / n_rep;
+    qbi = t % mqb;
+    h = (t / mqb) * n_rep + r;
+  } else {
+    h = blockIdx.x / mqb;
+    qbi = blockIdx.x % mqb;
+  }
+  const int g = h / n_rep;
   const int t0 = b.seq_start[bseq];
   const int T = b.seq_start[bseq + 1] - t0;
   const int nqb = (T + 255) / 256;
-  if ((int)blockIdx.x >= nqb) return;  // uniform over the workgroup
-  const int qb0 = (nqb - 1 - (int)blockIdx.x) * 256;  // heaviest blocks dispatch first
+  const int qbk = mqb - 1 - qbi;  // heaviest blocks dispatch first
+  if (qbk >= nqb) return;  // uniform over the workgroup
+  const int qb0 = qbk * 256;
   const int row0 = qb0 + kw * 64 + hf * 32;
   bf16x8 qf[2][4];
   int lim[2], tokrow[2];
@@ -885,7 +900,7 @@ void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, 
   // the 4-wave kernel is the default (faster on the box: 712 vs 578 TF/s at 32B / 8k).
   const int variant = env_int("INFERD_ATTN_PREFILL");
   if (variant == 8 && b.max_ctx <= PREFILL8_MAX_PAGES * KV_PAGE) {
-    hipLaunchKernelGGL(attn_prefill8_kernel, dim3((b.max_q_len + 255) / 256, H, b.B), dim3(512), 0, s, q, kv_layer,
+    hipLaunchKernelGGL(attn_prefill8_kernel, dim3((b.max_q_len + 255) / 256 * H, b.B), dim3(512), 0, s, q, kv_layer,
                        b, H, KV, scale * LOG2E, out);
     return;
   }
