@@ -126,6 +126,42 @@ __device__ __forceinline__ void qkv8(const DecodeFuse& f, int M, int tok, int co
   }
 }
 
+// The Qwen3 q-norm + RoPE of one query head in the S^T fragment layout: lane l holds dims
+// 8(l>>4) + 32 ks + j (ks = 0..3, j = 0..7) of query row `tok`, head `hq`; the RMS sum
+// reduces over the head's 4 lanes, the RoPE partner dim d +- 64 is fragment ks +- 2 of the
+// same lane.  Same per-element rounding points as qk_norm_rope_kv_kernel.
+__device__ __forceinline__ void q_norm_rope_frags(const DecodeFuse& fz, int M, int tok, int pos, int hq, int lane,
+                                                  bf16x8 (&qf)[4]) {
+  const int d0 = 8 * (lane >> 4);
+  const int qcol = hq * HEAD_DIM + d0;
+  float x[4][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qkv8(fz, M, tok, qcol + ks * 32, x[ks]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += x[ks][j] * x[ks][j];
+  }
+  const float inv = 1.0f / sqrtf(sum_q4(ss) / 128.0f + fz.eps);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const u16x8 wv = *(const u16x8*)(fz.qn_w + d0 + ks * 32);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[ks][j] = rbf(bf2f(wv[j]) * rbf(x[ks][j] * inv));
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int dc = d0 + (ks & 1) * 32;  // dim mod 64 of element 0
+    const u16x8 cv = *(const u16x8*)(fz.cos_t + (int64_t)pos * 64 + dc);
+    const u16x8 sv = *(const u16x8*)(fz.sin_t + (int64_t)pos * 64 + dc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float rot = ks < 2 ? -x[ks + 2][j] : x[ks - 2][j];
+      qf[ks][j] = (__bf16)(rbf(x[ks][j] * bf2f(cv[j])) + rbf(rot * bf2f(sv[j])));
+    }
+  }
+}
+
 // K/V of the decode token `tok` for kv head g -> cache (lanes 0-15 K, 16-31 V; all 64 lanes
 // run the arithmetic so the 16-wide shuffles see full groups)
 __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __restrict__ kv, const AttnBatch& b,
@@ -243,35 +279,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
   bf16x8 qf[4];
   if constexpr (FUSED) {
     const int hh = hn < n_rep ? hn : 0;
-    const int d0 = 8 * (lane >> 4);
-    const int qcol = (g * n_rep + hh) * HEAD_DIM + d0;
-    float x[4][8];
-    float ss = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      qkv8(fz, b.M, tok, qcol + ks * 32, x[ks]);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss += x[ks][j] * x[ks][j];
-    }
-    const float inv = 1.0f / sqrtf(sum_q4(ss) / 128.0f + fz.eps);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const u16x8 wv = *(const u16x8*)(fz.qn_w + d0 + ks * 32);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[ks][j] = rbf(bf2f(wv[j]) * rbf(x[ks][j] * inv));
-    }
-    const int pos = b.positions[tok];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int dc = d0 + (ks & 1) * 32;  // dim mod 64 of element 0
-      const u16x8 cv = *(const u16x8*)(fz.cos_t + (int64_t)pos * 64 + dc);
-      const u16x8 sv = *(const u16x8*)(fz.sin_t + (int64_t)pos * 64 + dc);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float rot = ks < 2 ? -x[ks + 2][j] : x[ks - 2][j];
-        qf[ks][j] = (__bf16)(rbf(x[ks][j] * bf2f(cv[j])) + rbf(rot * bf2f(sv[j])));
-      }
-    }
+    q_norm_rope_frags(fz, b.M, tok, b.positions[tok], g * n_rep + hh, lane, qf);
   } else {
     const int hh = hn < n_rep ? hn : 0;
     const u16* qp = q + ((int64_t)tok * H + g * n_rep + hh) * HEAD_DIM + 8 * (lane >> 4);
@@ -586,7 +594,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
                                                            const u16* __restrict__ kv,
                                                            AttnBatch b, int H, int KV,
                                                            float scale_log2,
-                                                           u16* __restrict__ out, int order) {
+                                                           u16* __restrict__ out, int order, DecodeFuse fz) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 32768];
   const int bseq = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -620,9 +628,13 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
     valid[nb] = row < T;
     tokrow[nb] = t0 + (valid[nb] ? row : T - 1);
     lim[nb] = b.positions[tokrow[nb]];
-    const u16* qp = q + ((int64_t)tokrow[nb] * H + h) * HEAD_DIM + 8 * (lane >> 4);
+    if (fz.qkv) {  // q-norm + RoPE from the raw q/k/v row (the separate kernel did K/V only)
+      q_norm_rope_frags(fz, b.M, tokrow[nb], lim[nb], h, lane, qf[nb]);
+    } else {
+      const u16* qp = q + ((int64_t)tokrow[nb] * H + h) * HEAD_DIM + 8 * (lane >> 4);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
+      for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
+    }
   }
   // pages: up to the workgroup's last row; a wave computes up to its own last row and
   // masks only pages that reach past its smallest row limit
@@ -895,11 +907,12 @@ __global__ __launch_bounds__(512, 1) void attn_prefill8_kernel(const u16* __rest
 }
 
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
-                         float scale, u16* out, hipStream_t s) {
-  // INFERD_ATTN_PREFILL=8 selects the 8-wave staggered kernel (tools/attn_bench.py A/B);
-  // the 4-wave kernel is the default (faster on the box: 712 vs 578 TF/s at 32B / 8k).
+                         float scale, u16* out, hipStream_t s, const u16* qkv, int64_t ldqkv, const u16* qn_w,
+                         const u16* cos_t, const u16* sin_t, float eps) {
+  // INFERD_ATTN_PREFILL=8 selects the 8-wave staggered kernel (tools/attn_bench.py A/B; it
+  // takes pre-normed q only); the 4-wave kernel is the default.
   const int variant = env_int("INFERD_ATTN_PREFILL");
-  if (variant == 8 && b.max_ctx <= PREFILL8_MAX_PAGES * KV_PAGE) {
+  if (variant == 8 && !qkv && b.max_ctx <= PREFILL8_MAX_PAGES * KV_PAGE) {
     hipLaunchKernelGGL(attn_prefill8_kernel, dim3((b.max_q_len + 255) / 256 * H, b.B), dim3(512), 0, s, q, kv_layer,
                        b, H, KV, scale * LOG2E, out);
     return;
@@ -907,6 +920,7 @@ void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, 
   const int n = (b.max_q_len + 127) / 128 * H;
   const char* e = getenv("INFERD_ATTN_ORDER");
   const int order = (e && *e) ? atoi(e) : (n % 8 == 0 ? 1 : 0);
+  const DecodeFuse fz = {qkv, ldqkv, qn_w, nullptr, cos_t, sin_t, eps, nullptr, nullptr, 0, 0};
   hipLaunchKernelGGL(attn_prefill_kernel, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out,
-                     (order == 1 && n % 8 == 0) ? 1 : 0);
+                     (order == 1 && n % 8 == 0) ? 1 : 0, fz);
 }

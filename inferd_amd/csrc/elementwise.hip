@@ -200,9 +200,9 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
     const u16* __restrict__ qkv, int64_t ldqkv, const int32_t* __restrict__ positions,
     const int32_t* __restrict__ slots, const u16* __restrict__ qn_w, const u16* __restrict__ kn_w,
     const u16* __restrict__ cos_t, const u16* __restrict__ sin_t, u16* __restrict__ q_out,
-    u16* __restrict__ kv_layer, int H, int KV, float eps) {
+    u16* __restrict__ kv_layer, int H, int KV, float eps, int head0) {
   int tok = blockIdx.y;
-  int hh = blockIdx.x * 16 + (threadIdx.x >> 4);
+  int hh = head0 + blockIdx.x * 16 + (threadIdx.x >> 4);
   int c = threadIdx.x & 15;  // dims 8c .. 8c+7
   int nheads = H + 2 * KV;
   bool active = hh < nheads;
@@ -269,11 +269,13 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
 void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positions,
                             const int32_t* slots, const u16* qn_w, const u16* kn_w,
                             const u16* cos_t, const u16* sin_t, u16* q_out, u16* kv_layer, int M,
-                            int H, int KV, float eps, hipStream_t s) {
-  int nheads = H + 2 * KV;
+                            int H, int KV, float eps, hipStream_t s, bool skip_q) {
+  // skip_q: K and V heads only (the prefill attention normalises and rotates q itself)
+  const int head0 = skip_q ? H : 0;
+  const int nheads = H + 2 * KV - head0;
   dim3 g((nheads + 15) / 16, M);
   hipLaunchKernelGGL(qk_norm_rope_kv_kernel, g, dim3(256), 0, s, qkv, ldqkv, positions, slots,
-                     qn_w, kn_w, cos_t, sin_t, q_out, kv_layer, H, KV, eps);
+                     qn_w, kn_w, cos_t, sin_t, q_out, kv_layer, H, KV, eps, head0);
 }
 
 // ------------------------------------------------------------------ embedding gather

@@ -646,10 +646,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
       __builtin_amdgcn_global_load_lds((const void*)(src + 512), (void*)(base + 1024), 16, 0, 0);
     }
   };
-  auto issue_s = [&](int s) {
-    int slot = s % RING_SLOTS;
-    issue(s & 3, s >> 2, slot);
-  };
+
 
   f32x4 acc[8][4];
 #pragma unroll

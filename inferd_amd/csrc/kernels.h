@@ -25,7 +25,7 @@ void launch_rope_table(const float* inv_freq, int max_pos, u16* cos_t, u16* sin_
 void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positions,
                             const int32_t* slots, const u16* qn_w, const u16* kn_w,
                             const u16* cos_t, const u16* sin_t, u16* q_out, u16* kv_layer, int M,
-                            int H, int KV, float eps, hipStream_t s);
+                            int H, int KV, float eps, hipStream_t s, bool skip_q = false);
 void launch_embed(const int32_t* ids, const u16* table, int M, int N, int vocab, u16* out,
                   int32_t* err, hipStream_t s);
 void launch_argmax_decode(const unsigned long long* keys, int B, int32_t* ids, hipStream_t s);
@@ -81,5 +81,9 @@ void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, co
                               float scale, u16* out, float* ws, hipStream_t s, const float* part = nullptr,
                               const float* ssq = nullptr, int ksl = 0, int K = 0);
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx);
+// With qkv non-null the kernel applies the q-norm + RoPE itself from the raw q/k/v rows
+// (qkv [M][ldqkv], q ignored); launch_qk_norm_rope_kv then only needs skip_q = true.
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
-                         float scale, u16* out, hipStream_t s);
+                         float scale, u16* out, hipStream_t s, const u16* qkv = nullptr, int64_t ldqkv = 0,
+                         const u16* qn_w = nullptr, const u16* cos_t = nullptr, const u16* sin_t = nullptr,
+                         float eps = 0.f);

@@ -287,3 +287,28 @@ def test_config5_q32b_layer_prefill_vs_oracle():
         e = rel_err(out, oracle.forward_cached("p", xd)[0])
         print(f"32B layer decode {step}: rel err {e:.2e}")
         assert e < TOL_REL
+
+
+def test_prefill_fused_q_rope_matches_separate(monkeypatch):
+    """INFERD_FUSE_PREFILL_ROPE=1 (q-norm + RoPE inside the prefill attention, K/V-only norm
+    kernel) against the default separate kernel: one Qwen3-8B-dims layer, two ragged
+    prompts with a cached prefix, then a decode step."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["qwen3-8b"]
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("INFERD_FUSE_PREFILL_ROPE", fused)
+        s = SpanRuntime(d, 3, 1, has_embed=False, has_lm_head=False, device=DEV, max_positions=1024,
+                        kv_pages=32, max_tokens=512, max_seqs=4)
+        s.init_synthetic(SEED)
+        g = torch.Generator().manual_seed(4)
+        x0 = (torch.randn(200 + 77, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+        x1 = (torch.randn(150, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+        x2 = (torch.randn(2, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+        h0 = s.forward([("a", 200), ("b", 77)], x=x0, want_hidden=True)["hidden"].cpu()
+        h1 = s.forward([("a", 150)], x=x1, want_hidden=True)["hidden"].cpu()
+        h2 = s.forward([("a", 1), ("b", 1)], x=x2, want_hidden=True)["hidden"].cpu()
+        outs.append(torch.cat([h0, h1, h2]))
+    e = rel_err(outs[0], outs[1])
+    print(f"fused vs separate prefill q-norm/rope: rel err {e:.2e}")
+    assert e < 2e-2
