@@ -48,7 +48,7 @@ def classify(name):
         if not m:
             return "gemm_decode"
         epi = int(m.group(1).split(",")[5])  # <MT, S, NW, TW, D, EPI, NORM>
-        return {0: "qkv_gemm", 1: "resid_gemm", 2: "gateup_gemm", 3: "lm_head_argmax"}[epi]
+        return {0: "qkv_gemm", 1: "resid_gemm", 2: "gateup_gemm", 3: "lm_head_argmax", 4: "qkv_gemm"}[epi]
     for key, cls in (("attn_decode_kernel", "attention"), ("qk_norm_rope_kv", "qk_norm_rope_kv"),
                      ("rmsnorm", "rmsnorm"), ("argmax_reduce", "lm_head_argmax")):
         if key in name:
