@@ -212,8 +212,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
         o = v[0][r];
       } else if constexpr (EPI == EPI_RESID) {
         o = rbf(v[0][r]) + bf2f(g.R[(int64_t)row * g.ldr + col]);
-      } else {  // EPI_SILU
-        o = rbf(silu_f(rbf(v[0][r]))) * rbf(v[1][r]);
+      } else if constexpr (EPI == EPI_SILU) {
+        o = rbf(silu_f(rbf(v[0][r]))) * rbf(v[S - 1][r]);
+      } else {
+        o = 0.f;  // EPI_PARTIAL returns above
       }
       g.C[(int64_t)row * g.ldc + col] = f2bf(o);
     }
@@ -871,11 +873,6 @@ static int gemm_tile_variant() {
 // Tail-split plan for `tiles` 256x256 tiles of nK K-steps on 8 XCDs x 32 CUs (one 512-thread
 // workgroup per CU).  INFERD_GEMM_SPLIT=0 disables it.  The fp32 partial workspace and the
 // counters are allocated once (zeroed) and grown on demand; never inside a graph capture.
-static float* g_split_ws = nullptr;
-static size_t g_split_ws_bytes = 0;
-static unsigned* g_split_cnt = nullptr;
-static int g_split_cnt_n = 0;
-
 static int env_or(const char* name, int dflt) {
   const char* e = getenv(name);
   return e && *e ? atoi(e) : dflt;
@@ -893,6 +890,17 @@ static void ring_launch(bool keepb, int grid, hipStream_t s, const u16* A, int64
                        ldr, M, rs, gm, gn, st);
 }
 
+// Per device (a process may drive several GPUs); grown on demand, never inside a graph
+// capture, not thread-safe (one host thread per device, like the span API).
+#define SPLIT_MAX_DEVICES 16
+struct SplitWs {
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  unsigned* cnt = nullptr;
+  int cnt_n = 0;
+};
+static SplitWs g_split[SPLIT_MAX_DEVICES];
+
 static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
   SplitTail st = {1, 0, 0, 0, nullptr, nullptr};
   const char* e = getenv("INFERD_GEMM_SPLIT");
@@ -904,28 +912,31 @@ static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
   if (split > 8 || nK % split || nK / split < 3) return st;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return st;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= SPLIT_MAX_DEVICES) return st;
+  SplitWs& w = g_split[dev];
   const size_t bytes = (size_t)8 * rem * split * 65536 * sizeof(float);
-  if (bytes > g_split_ws_bytes) {
-    if (g_split_ws) (void)hipFree(g_split_ws);
-    g_split_ws = nullptr;
-    g_split_ws_bytes = 0;
-    if (hipMalloc((void**)&g_split_ws, bytes) != hipSuccess) return st;
-    g_split_ws_bytes = bytes;
+  if (bytes > w.ws_bytes) {
+    if (w.ws) (void)hipFree(w.ws);
+    w.ws = nullptr;
+    w.ws_bytes = 0;
+    if (hipMalloc((void**)&w.ws, bytes) != hipSuccess) return st;
+    w.ws_bytes = bytes;
   }
-  if (2 * 8 * rem > g_split_cnt_n) {
-    if (g_split_cnt) (void)hipFree(g_split_cnt);
-    g_split_cnt = nullptr;
-    g_split_cnt_n = 0;
-    if (hipMalloc((void**)&g_split_cnt, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
-    if (hipMemset(g_split_cnt, 0, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
-    g_split_cnt_n = 2 * 8 * rem;
+  if (2 * 8 * rem > w.cnt_n) {
+    if (w.cnt) (void)hipFree(w.cnt);
+    w.cnt = nullptr;
+    w.cnt_n = 0;
+    if (hipMalloc((void**)&w.cnt, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
+    if (hipMemset(w.cnt, 0, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
+    w.cnt_n = 2 * 8 * rem;
   }
   st.split = split;
   st.tiles_per_xcd = per;
   st.full_per_xcd = per - rem;
   st.units_per_xcd = per - rem + rem * split;
-  st.ws = g_split_ws;
-  st.cnt = g_split_cnt;
+  st.ws = w.ws;
+  st.cnt = w.cnt;
   return st;
 }
 
