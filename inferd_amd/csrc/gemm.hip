@@ -572,6 +572,36 @@ struct SplitTail {
   unsigned* cnt;        // [2][8 * rem] arrival tickets, done counters (zero between launches)
 };
 
+// XCD-aware tile order (bijective for any grid size): blocks that share an XCD get
+// consecutive tiles, grouped GM row-blocks deep; with a tail split, each XCD's last tiles
+// are cut into K-slices (SplitTail)
+__device__ __forceinline__ void tile_order(const SplitTail& st, int grid_m, int grid_n, int& bm, int& bn,
+                                           int& slice, int& nsl, int& sidx) {
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  int tile = wg;
+  if (st.split > 1) {  // grid = 8 * units_per_xcd
+    const int x = wg / st.units_per_xcd, li = wg - x * st.units_per_xcd;
+    if (li < st.full_per_xcd) {
+      tile = x * st.tiles_per_xcd + li;
+    } else {
+      const int j = li - st.full_per_xcd;
+      tile = x * st.tiles_per_xcd + st.full_per_xcd + j / st.split;
+      slice = j % st.split;
+      nsl = st.split;
+      sidx = x * (st.tiles_per_xcd - st.full_per_xcd) + j / st.split;
+    }
+  }
+  constexpr int GM = 8;
+  const int group = tile / (GM * grid_n);
+  const int first_m = group * GM;
+  const int gsz = min(grid_m - first_m, GM);
+  const int in = tile - group * GM * grid_n;
+  bm = first_m + in % gsz;
+  bn = in / gsz;
+}
+
 template <int EPI, bool KEEPB>
 __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
@@ -580,33 +610,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
   __shared__ __attribute__((aligned(16))) char lds[RING_SLOTS * 16384];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 2, wc = wave & 3;
-  // ---- XCD-aware tile order (bijective for any grid size)
   int bm, bn, slice = 0, nsl = 1, sidx = 0;
-  {
-    const int nwg = gridDim.x, orig = blockIdx.x;
-    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
-    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-    int tile = wg;
-    if (st.split > 1) {  // grid = 8 * units_per_xcd
-      const int x = wg / st.units_per_xcd, li = wg - x * st.units_per_xcd;
-      if (li < st.full_per_xcd) {
-        tile = x * st.tiles_per_xcd + li;
-      } else {
-        const int j = li - st.full_per_xcd;
-        tile = x * st.tiles_per_xcd + st.full_per_xcd + j / st.split;
-        slice = j % st.split;
-        nsl = st.split;
-        sidx = x * (st.tiles_per_xcd - st.full_per_xcd) + j / st.split;
-      }
-    }
-    constexpr int GM = 8;
-    const int group = tile / (GM * grid_n);
-    const int first_m = group * GM;
-    const int gsz = min(grid_m - first_m, GM);
-    const int in = tile - group * GM * grid_n;
-    bm = first_m + in % gsz;
-    bn = in / gsz;
-  }
+  tile_order(st, grid_m, grid_n, bm, bn, slice, nsl, sidx);
   const int m0 = bm * 256;
   const int n0 = bn * ((EPI == EPI_SILU) ? 128 : 256);
   const int nK = KT / 2 / nsl;  // 64-deep K-steps of this slice
@@ -861,12 +866,275 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
   }
 }
 
+// ============================================================ 4-wave 256x256 prefill GEMM
+// gemm_w4_kernel: the same 256x256 output tile and K-step 64, on FOUR waves of 128x128
+// (8x8 accumulator tiles = 256 AGPRs each, one wave per SIMD).  Per K-step a wave issues
+// 128 MFMAs against 32 ds_read_b128 (0.25 LDS reads per MFMA; the 8-wave ring needs 0.375)
+// and 3 barriers instead of 8, and its MFMA stream never waits for a partner wave.
+//  * LDS: two K-step buffers of 64 KiB (A image [256 rows][128 B], XOR-swizzled 16-B
+//    chunks; B image [16 n-tiles][2 k-halves][1 KiB] fragment-packed, lane-linear).
+//  * Registers: F0 = the k-half-0 fragments (8 A + 8 B) of the current step, F1 = k-half 1.
+//  * Iteration t (buffer c = t & 1): [A] MFMAs on F0 (rows 0-63) while F1 is read from c;
+//    lgkmcnt(0) + barrier (every wave is done with c); [B] MFMAs on F0 (rows 64-127) and F1
+//    (rows 0-63) while the 16 LDS-DMA pieces of step t+2 are issued into c; counted vmcnt
+//    (step t+1's pieces landed) + barrier; [C] MFMAs on F1 (rows 64-127) while F0 of step
+//    t+1 is read from c ^ 1.  Step t+1's pieces have one full iteration to land.
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
+    const float* __restrict__ rs, int grid_m, int grid_n, SplitTail st) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 65536];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  int bm, bn, slice = 0, nsl = 1, sidx = 0;
+  tile_order(st, grid_m, grid_n, bm, bn, slice, nsl, sidx);
+  const int m0 = bm * 256;
+  const int n0 = bn * ((EPI == EPI_SILU) ? 128 : 256);
+  const int nK = KT / 2 / nsl;  // 64-deep K-steps of this slice (>= 2)
+  const int k0 = slice * nK;
+
+  // ---- LDS-DMA sources: wave-uniform (SGPR) bases + per-lane 32-bit byte offsets, so
+  // each piece is one global_load_lds with saddr: this wave's 8 A pieces (8 image rows
+  // each) and 8 B pieces (one 1 KiB fragment tile each)
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const char* a_base = (const char*)(A + (int64_t)m0 * lda + k0 * 64);
+  unsigned a_voff[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int i = 64 * wave + 8 * p + (lane >> 3);  // image row 0..255
+    const int rr = (m0 + i < M ? i : M - 1 - m0);
+    const int chunk = (lane & 7) ^ ((i >> 1) & 7);
+    a_voff[p] = (unsigned)(rr * lda * 2 + chunk * 16);
+  }
+  // B piece q = 8 * wave + p: image n-tile j = q >> 1, k-half q & 1
+  int64_t b_soff[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int q = 8 * wv + p;
+    const int j = q >> 1;
+    int gnt;
+    if constexpr (EPI == EPI_SILU) {  // wave column w: gate tiles 4w..4w+3, then the same up tiles
+      const int w = j >> 3, jj = j & 7;
+      gnt = (jj < 4 ? 0 : n_tiles_w / 2) + n0 / 16 + 4 * w + (jj & 3);
+    } else {
+      gnt = n0 / 16 + j;
+    }
+    b_soff[p] = ((int64_t)gnt * KT + 2 * k0 + (q & 1)) * 1024;
+  }
+  const unsigned b_voff = lane * 16;
+  auto issue = [&](int p, int t, int buf) {  // piece p (0-7 A, 8-15 B) of K-step t into buffer buf
+    char* base = lds + buf * 65536;
+    if (p < 8)
+      __builtin_amdgcn_global_load_lds((const void*)(a_base + t * 128 + a_voff[p]),
+                                       (void*)(base + (8 * wv + p) * 1024), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)((const char*)Wp + b_soff[p - 8] + (int64_t)t * 2048 + b_voff),
+                                       (void*)(base + 32768 + (8 * wv + p - 8) * 1024), 16, 0, 0);
+  };
+
+  // ---- fragment reads: A rows wr*128 + mt*16 + (lane & 15), swizzle depends on lane only
+  const int arow = wr * 128 + (lane & 15);
+  const int a_off0 = arow * 128 + 16 * ((lane >> 4) ^ ((arow >> 1) & 7));
+  const int a_off1 = arow * 128 + 16 * ((4 + (lane >> 4)) ^ ((arow >> 1) & 7));
+  const int b_off = 32768 + (8 * wc) * 2048 + lane * 16;
+  bf16x8 fa[2][8], fb[2][8];  // [k-half][tile]
+  auto read_a = [&](int kh, int mt, int buf) {
+    fa[kh][mt] = *(const bf16x8*)(lds + buf * 65536 + (kh ? a_off1 : a_off0) + mt * 2048);
+  };
+  auto read_b = [&](int kh, int nt, int buf) {
+    fb[kh][nt] = *(const bf16x8*)(lds + buf * 65536 + b_off + nt * 2048 + kh * 1024);
+  };
+  // The 256 accumulators live in AGPRs through inline-asm MFMAs ("+a"): with the builtin,
+  // hipcc's allocator rotates part of them through VGPRs inside the loop (copies per MFMA).
+  // Hazards hipcc cannot see (cdna_hip_programming.md §5.7 item 2) are padded by hand:
+  // zeroing -> first MFMA (acc_fence below), last MFMA -> first compiler read of a result.
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto acc_fence = [&]() {  // 16 wait states, then every accumulator is redefined after them
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i == 0)
+        asm volatile("s_nop 7\n\ts_nop 7" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
+                     "+a"(acc[i][4]), "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+      else
+        asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                     "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+    }
+  };
+  acc_fence();
+  auto mf = [&](int kh, int mt, int nt) {
+    asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[mt][nt]) : "v"(fb[kh][nt]), "v"(fa[kh][mt]));
+  };
+
+  // MODE 0: steady (issue step t+2, wait for t+1, read F0 of t+1); 1: t = nK-2 (no issue,
+  // wait 0, read); 2: t = nK-1 (no issue, no wait, no read)
+  auto iter = [&](auto MODE, int t) {
+    constexpr int mode = decltype(MODE)::value;
+    const int c = t & 1;
+    // [A] 32 MFMAs on F0 rows 0-63, 16 reads of F1 from c
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      if (g < 8) read_b(1, g, c); else read_a(1, g - 8, c);
+      mf(0, g >> 2, (g & 3) * 2);
+      mf(0, g >> 2, (g & 3) * 2 + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    // [B] 64 MFMAs (F0 rows 64-127, F1 rows 0-63), 16 LDS-DMA pieces of step t+2 into c
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      if constexpr (mode == 0) issue(g, t + 2, c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int x = 4 * g + u;  // 0..63
+        if (x < 32) mf(0, 4 + (x >> 3), x & 7); else mf(1, (x - 32) >> 3, x & 7);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (mode == 0) {
+      vm_wait<16>();
+    } else if constexpr (mode == 1) {
+      vm_wait<0>();
+    }
+    raw_barrier();
+    // [C] 32 MFMAs on F1 rows 64-127, 16 reads of F0 of step t+1 from c ^ 1
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      if constexpr (mode != 2) {
+        if (g < 8) read_b(0, g, c ^ 1); else read_a(0, g - 8, c ^ 1);
+      }
+      mf(1, 4 + (g >> 2), (g & 3) * 2);
+      mf(1, 4 + (g >> 2), (g & 3) * 2 + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // prologue: steps 0 and 1 in flight, wait for step 0, read its F0
+#pragma unroll
+  for (int p = 0; p < 16; ++p) issue(p, 0, 0);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) issue(p, 1, 1);
+  vm_wait<16>();
+  raw_barrier();
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    read_b(0, g, 0);
+    read_a(0, g, 0);
+  }
+  int t = 0;
+  for (; t < nK - 2; ++t) iter(std::integral_constant<int, 0>{}, t);
+  iter(std::integral_constant<int, 1>{}, t);
+  iter(std::integral_constant<int, 2>{}, t + 1);
+  acc_fence();
+
+  if (nsl > 1) {  // ---- tail split: publish or combine (as gemm_ring256_kernel)
+    __syncthreads();
+    unsigned* ticket_lds = (unsigned*)lds;
+    unsigned* cnt = st.cnt + sidx;
+    unsigned* done = st.cnt + 8 * (st.tiles_per_xcd - st.full_per_xcd) + sidx;
+    if (threadIdx.x == 0) ticket_lds[0] = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned ticket = ticket_lds[0];
+    float* part = st.ws + (size_t)sidx * nsl * 65536;
+    if (ticket + 1 < (unsigned)nsl) {
+      unsigned long long* dst = (unsigned long long*)(part + (size_t)slice * 65536);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const unsigned long long v = ((unsigned long long)__float_as_uint(acc[i][j][2 * hh + 1]) << 32) |
+                                         __float_as_uint(acc[i][j][2 * hh]);
+            __hip_atomic_store(dst + (((i * 8 + j) * 2 + hh) * 256 + threadIdx.x), v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (threadIdx.x == 0) {
+      while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 < (unsigned)nsl)
+        __builtin_amdgcn_s_sleep(2);
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          float v0 = 0.f, v1 = 0.f;
+          for (int sl = 0; sl < nsl; ++sl) {
+            if (sl == slice) {
+              v0 += acc[i][j][2 * hh];
+              v1 += acc[i][j][2 * hh + 1];
+            } else {
+              const unsigned long long* src = (const unsigned long long*)(part + (size_t)sl * 65536);
+              const unsigned long long v = __hip_atomic_load(src + ((i * 8 + j) * 2 + hh) * 256 + threadIdx.x,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              v0 += __uint_as_float((unsigned)v);
+              v1 += __uint_as_float((unsigned)(v >> 32));
+            }
+          }
+          acc[i][j][2 * hh] = v0;
+          acc[i][j][2 * hh + 1] = v1;
+        }
+  }
+
+  // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = m0 + wr * 128 + i * 16 + (lane & 15);
+    if (row >= M) continue;
+    const float sc = rs ? rs[row] : 1.0f;
+    if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int col = n0 + wc * 64 + nt * 16 + 4 * (lane >> 4);
+        u16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float gg = rbf(acc[i][nt][r] * sc);
+          const float uu = rbf(acc[i][4 + nt][r] * sc);
+          v[r] = f2bf(rbf(silu_f(gg)) * uu);
+        }
+        *(u16x4*)(C + (int64_t)row * ldc + col) = v;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = n0 + wc * 128 + j * 16 + 4 * (lane >> 4);
+        u16x4 v;
+        u16x4 rr;
+        if constexpr (EPI == EPI_RESID) rr = *(const u16x4*)(R + (int64_t)row * ldr + col);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float o = acc[i][j][r] * sc;
+          if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(rr[r]);
+          v[r] = f2bf(o);
+        }
+        *(u16x4*)(C + (int64_t)row * ldc + col) = v;
+      }
+    }
+  }
+}
+
 // INFERD_GEMM_TILE selects the prefill GEMM (read per call so one process can A/B them):
-// "ring" (default) | "256" | "128"
+// "w4" (default) | "ring" | "256" | "128"
 static int gemm_tile_variant() {
   const char* e = getenv("INFERD_GEMM_TILE");
-  if (!e || !*e) return 0;
+  if (!e || !*e) return 4;
   if (e[0] == 'r') return 0;
+  if (e[0] == 'w') return 4;
   return atoi(e);
 }
 
@@ -941,7 +1209,8 @@ static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
 }
 
 static bool use_ring256(int M, int N, int K, int epi) {
-  if (gemm_tile_variant() != 0 || M < 512 || K < 192) return false;
+  const int v = gemm_tile_variant();
+  if ((v != 0 && v != 4) || M < 512 || K < 192) return false;
   return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
 }
 
@@ -974,6 +1243,23 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     const int grid = st.split > 1 ? 8 * st.units_per_xcd : gm * gn;
     // INFERD_GEMM_KEEPB=0 selects the look-ahead-6 schedule that re-reads B0 (A/B)
     const bool keepb = env_or("INFERD_GEMM_KEEPB", 1) != 0;
+    if (gemm_tile_variant() == 4) {
+      switch (epi) {
+        case EPI_NONE:
+          hipLaunchKernelGGL(gemm_w4_kernel<EPI_NONE>, dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                             ldr, M, rs, gm, gn, st);
+          break;
+        case EPI_RESID:
+          hipLaunchKernelGGL(gemm_w4_kernel<EPI_RESID>, dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                             ldr, M, rs, gm, gn, st);
+          break;
+        default:
+          hipLaunchKernelGGL(gemm_w4_kernel<EPI_SILU>, dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                             ldr, M, rs, gm, gn, st);
+          break;
+      }
+      return;
+    }
     switch (epi) {
       case EPI_NONE:
         ring_launch<EPI_NONE>(keepb, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);

@@ -2,7 +2,8 @@
 projection shapes (BASELINE config 5, M = 8192 prompt rows), interleaved rounds in ONE
 process (cdna_hip_programming.md §5.4 rule 24), uniform random operands (rule 25).
 
-usage: python tools/gemm_bench.py [--m 8192] [--rounds 5] [--variants ring,256]
+usage: python tools/gemm_bench.py [--m 8192] [--rounds 5] [--variants ring,256,torch]
+("torch" times torch.matmul = hipBLASLt on the same operands, no epilogue: the library ceiling.)
 """
 import argparse
 import os
@@ -43,20 +44,24 @@ def main():
         w = ((torch.rand(rows, k, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
         wp = torch.empty_like(w)
         _lib.check(L.inferd_pack_weight(w.data_ptr(), rows, k, wp.data_ptr(), st))
-        del w
+        if "torch" not in args.variants.split(","):
+            w = None
         c = torch.empty(M, n, dtype=torch.bfloat16, device=dev)
         r = (torch.rand(M, n, device=dev) * 2 - 1).to(torch.bfloat16) if epi == 1 else None
-        bufs[name] = (a, wp, c, r, n, k, epi)
+        bufs[name] = (a, wp, c, r, n, k, epi, w)
     torch.cuda.synchronize()
     variants = args.variants.split(",")
     times = {(s, v): [] for s in bufs for v in variants}
     outs = {}
     for rnd in range(args.rounds):
-        for name, (a, wp, c, r, n, k, epi) in bufs.items():
+        for name, (a, wp, c, r, n, k, epi, w) in bufs.items():
             for v in variants:
-                os.environ[args.env_name] = v
-                call = lambda: _lib.check(L.inferd_gemm(a.data_ptr(), wp.data_ptr(), c.data_ptr(),  # noqa: E731
-                                                        None if r is None else r.data_ptr(), M, n, k, epi, st))
+                if v == "torch":  # hipBLASLt through torch.matmul: plain GEMM, no epilogue (ceiling probe)
+                    call = lambda: torch.matmul(a, w.t())  # noqa: E731
+                else:
+                    os.environ[args.env_name] = v
+                    call = lambda: _lib.check(L.inferd_gemm(a.data_ptr(), wp.data_ptr(), c.data_ptr(),  # noqa: E731
+                                                            None if r is None else r.data_ptr(), M, n, k, epi, st))
                 call()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -65,10 +70,10 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 times[(name, v)].append(e0.elapsed_time(e1) / args.reps)
-                if rnd == 0:
+                if rnd == 0 and v != "torch":
                     outs[(name, v)] = c.clone()
         print(f"round {rnd} done", flush=True)
-    for name, (a, wp, c, r, n, k, epi) in bufs.items():
+    for name, (a, wp, c, r, n, k, epi, w) in bufs.items():
         fl = 2.0 * M * n * k * (2 if epi == 2 else 1)
         line = [f"{name:7s} M={M} N={n} K={k}"]
         for v in variants:
@@ -77,6 +82,8 @@ def main():
             line.append(f"{v}: {med * 1e3:8.1f} us {fl / med / 1e9:7.1f} TF/s (min {fl / t[0] / 1e9:7.1f})")
         base = outs[(name, variants[0])]
         for v in variants[1:]:
+            if v == "torch":
+                continue
             d = (outs[(name, v)].float() - base.float()).abs().max().item()
             line.append(f"maxdiff[{v}]={d:.3g}")
         print(" | ".join(line), flush=True)
