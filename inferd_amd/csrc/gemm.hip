@@ -879,7 +879,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
 //    (rows 0-63) while the 16 LDS-DMA pieces of step t+2 are issued into c; counted vmcnt
 //    (step t+1's pieces landed) + barrier; [C] MFMAs on F1 (rows 64-127) while F0 of step
 //    t+1 is read from c ^ 1.  Step t+1's pieces have one full iteration to land.
-template <int EPI>
+template <int EPI, int ORD>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
     u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
@@ -923,14 +923,29 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     b_soff[p] = ((int64_t)gnt * KT + 2 * k0 + (q & 1)) * 1024;
   }
   const unsigned b_voff = lane * 16;
+  // ORD & 2: buffer_load_dwordx4 ... lds with the per-piece and per-step offsets in SGPRs
+  // (soffset) instead of a 64-bit VGPR address per piece
+  const __amdgpu_buffer_rsrc_t a_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a_base, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, 0, 0x7fffffff, 0x00020000);
   auto issue = [&](int p, int t, int buf) {  // piece p (0-7 A, 8-15 B) of K-step t into buffer buf
     char* base = lds + buf * 65536;
-    if (p < 8)
-      __builtin_amdgcn_global_load_lds((const void*)(a_base + t * 128 + a_voff[p]),
-                                       (void*)(base + (8 * wv + p) * 1024), 16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds((const void*)((const char*)Wp + b_soff[p - 8] + (int64_t)t * 2048 + b_voff),
-                                       (void*)(base + 32768 + (8 * wv + p - 8) * 1024), 16, 0, 0);
+    if constexpr ((ORD & 2) != 0) {
+      typedef __attribute__((address_space(3))) void* lds_ptr;
+      if (p < 8)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr)(base + (8 * wv + p) * 1024), 16, a_voff[p], t * 128,
+                                                 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr)(base + 32768 + (8 * wv + p - 8) * 1024), 16, b_voff,
+                                                 (int)(b_soff[p - 8] + (int64_t)t * 2048), 0, 0);
+    } else {
+      if (p < 8)
+        __builtin_amdgcn_global_load_lds((const void*)(a_base + t * 128 + a_voff[p]),
+                                         (void*)(base + (8 * wv + p) * 1024), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)((const char*)Wp + b_soff[p - 8] + (int64_t)t * 2048 + b_voff),
+                                         (void*)(base + 32768 + (8 * wv + p - 8) * 1024), 16, 0, 0);
+    }
   };
 
   // ---- fragment reads: A rows wr*128 + mt*16 + (lane & 15), swizzle depends on lane only
@@ -972,44 +987,58 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
 
   // MODE 0: steady (issue step t+2, wait for t+1, read F0 of t+1); 1: t = nK-2 (no issue,
   // wait 0, read); 2: t = nK-1 (no issue, no wait, no read)
+  // MFMA x of a K-step (0..127) in issue order: [A] F0 rows 0-63, [B] F0 rows 64-127 then F1
+  // rows 0-63, [C] F1 rows 64-127; ORD & 1 = nt-major inside each group of 32
+  auto mfx = [&](int x) {
+    const int kh = (x >= 64) ? 1 : 0;
+    const int q = x & 31, half = (x >> 5) & 1;  // group of 32: rows 64 * half + ...
+    if constexpr ((ORD & 1) == 0)
+      mf(kh, 4 * half + (q >> 3), q & 7);
+    else
+      mf(kh, 4 * half + (q & 3), q >> 2);
+  };
+  // Every barrier is straddled by MFMAs (the last one before it is issued after the wait),
+  // so the matrix pipe stays busy while the waves meet.
   auto iter = [&](auto MODE, int t) {
     constexpr int mode = decltype(MODE)::value;
     const int c = t & 1;
-    // [A] 32 MFMAs on F0 rows 0-63, 16 reads of F1 from c
+    // [A] 32 MFMAs; the 16 F1 reads from c ride the first 16
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      if (g < 8) read_b(1, g, c); else read_a(1, g - 8, c);
-      mf(0, g >> 2, (g & 3) * 2);
-      mf(0, g >> 2, (g & 3) * 2 + 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    raw_barrier();
-    // [B] 64 MFMAs (F0 rows 64-127, F1 rows 0-63), 16 LDS-DMA pieces of step t+2 into c
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      if constexpr (mode == 0) issue(g, t + 2, c);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int x = 4 * g + u;  // 0..63
-        if (x < 32) mf(0, 4 + (x >> 3), x & 7); else mf(1, (x - 32) >> 3, x & 7);
+    for (int x = 0; x < 32; ++x) {
+      if (x == 31) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to hipcc's bookkeeping
+      mfx(x);
+      if (x < 16) {
+        if (x < 8) read_b(1, x, c); else read_a(1, x - 8, c);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (mode == 0) {
-      vm_wait<16>();
-    } else if constexpr (mode == 1) {
-      vm_wait<0>();
-    }
-    raw_barrier();
-    // [C] 32 MFMAs on F1 rows 64-127, 16 reads of F0 of step t+1 from c ^ 1
+    raw_barrier();  // every wave is done reading c
+    // [B] 64 MFMAs; the 16 LDS-DMA pieces of step t+2 into c, one after every 4th MFMA
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
+    for (int x = 32; x < 96; ++x) {
+      if (x == 95) {
+        if constexpr (mode == 0) {
+          vm_wait<16>();  // step t+1 landed (16 younger pieces in flight)
+        } else if constexpr (mode == 1) {
+          vm_wait<0>();
+        }
+      }
+      mfx(x);
+      if constexpr (mode == 0) {
+        if ((x & 3) == 0) issue((x - 32) >> 2, t + 2, c);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    raw_barrier();  // step t+1 is visible in c ^ 1
+    // [C] 32 MFMAs; F0 of step t+1 read from c ^ 1 during the first 16
+#pragma unroll
+    for (int x = 96; x < 128; ++x) {
+      mfx(x);
       if constexpr (mode != 2) {
-        if (g < 8) read_b(0, g, c ^ 1); else read_a(0, g - 8, c ^ 1);
+        if (x < 112) {
+          if (x < 104) read_b(0, x - 96, c ^ 1); else read_a(0, x - 104, c ^ 1);
+        }
       }
-      mf(1, 4 + (g >> 2), (g & 3) * 2);
-      mf(1, 4 + (g >> 2), (g & 3) * 2 + 1);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -1129,12 +1158,16 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
 }
 
 // INFERD_GEMM_TILE selects the prefill GEMM (read per call so one process can A/B them):
-// "w4" (default) | "ring" | "256" | "128"
+// "w4" (default; "w4m" / "w4g" / "w4mg" its A/B arms) | "ring" | "256" | "128"
 static int gemm_tile_variant() {
   const char* e = getenv("INFERD_GEMM_TILE");
-  if (!e || !*e) return 4;
+  if (!e || !*e) return 7;
   if (e[0] == 'r') return 0;
-  if (e[0] == 'w') return 4;
+  if (e[0] == 'w') {  // "w4" = "w4nb" (default) | "w4m": mt-major MFMA order | "w4g": global_load_lds
+    int v = 7;
+    for (const char* c = e + 2; *c; ++c) v &= (*c == 'm') ? ~1 : (*c == 'g') ? ~2 : ~0;
+    return v;
+  }
   return atoi(e);
 }
 
@@ -1156,6 +1189,26 @@ static void ring_launch(bool keepb, int grid, hipStream_t s, const u16* A, int64
   else
     hipLaunchKernelGGL((gemm_ring256_kernel<EPI, false>), dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
                        ldr, M, rs, gm, gn, st);
+}
+
+template <int ORD>
+static void w4_launch(int epi, int grid, hipStream_t s, const u16* A, int64_t lda, const u16* Wp, int KT, int ntw,
+                      u16* C, int64_t ldc, const u16* R, int64_t ldr, int M, const float* rs, int gm, int gn,
+                      const SplitTail& st) {
+  switch (epi) {
+    case EPI_NONE:
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE, ORD>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                         ldr, M, rs, gm, gn, st);
+      break;
+    case EPI_RESID:
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI_RESID, ORD>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc,
+                         R, ldr, M, rs, gm, gn, st);
+      break;
+    default:
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI_SILU, ORD>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc,
+                         R, ldr, M, rs, gm, gn, st);
+      break;
+  }
 }
 
 // Per device (a process may drive several GPUs); grown on demand, never inside a graph
@@ -1210,7 +1263,7 @@ static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
 
 static bool use_ring256(int M, int N, int K, int epi) {
   const int v = gemm_tile_variant();
-  if ((v != 0 && v != 4) || M < 512 || K < 192) return false;
+  if ((v != 0 && (v < 4 || v > 7)) || M < 512 || K < 192) return false;
   return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
 }
 
@@ -1243,20 +1296,12 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     const int grid = st.split > 1 ? 8 * st.units_per_xcd : gm * gn;
     // INFERD_GEMM_KEEPB=0 selects the look-ahead-6 schedule that re-reads B0 (A/B)
     const bool keepb = env_or("INFERD_GEMM_KEEPB", 1) != 0;
-    if (gemm_tile_variant() == 4) {
-      switch (epi) {
-        case EPI_NONE:
-          hipLaunchKernelGGL(gemm_w4_kernel<EPI_NONE>, dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                             ldr, M, rs, gm, gn, st);
-          break;
-        case EPI_RESID:
-          hipLaunchKernelGGL(gemm_w4_kernel<EPI_RESID>, dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                             ldr, M, rs, gm, gn, st);
-          break;
-        default:
-          hipLaunchKernelGGL(gemm_w4_kernel<EPI_SILU>, dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                             ldr, M, rs, gm, gn, st);
-          break;
+    if (gemm_tile_variant() >= 4 && gemm_tile_variant() <= 7) {
+      switch (gemm_tile_variant()) {
+        case 4: w4_launch<0>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
+        case 5: w4_launch<1>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
+        case 6: w4_launch<2>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
+        default: w4_launch<3>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
       }
       return;
     }

@@ -20,6 +20,9 @@ SHAPES = {  # name: (N_out, K, epilogue)
     "o": (5120, 8192, 1),
     "gateup": (25600, 5120, 2),
     "down": (5120, 25600, 1),
+    # K sweep on the qkv shape: time(K) = per-tile overhead + K-proportional main loop
+    "qkv_k1": (10240, 1024, 0),
+    "qkv_k2": (10240, 2048, 0),
 }
 
 
