@@ -575,9 +575,8 @@ struct SplitTail {
 // XCD-aware tile order (bijective for any grid size): blocks that share an XCD get
 // consecutive tiles, grouped GM row-blocks deep; with a tail split, each XCD's last tiles
 // are cut into K-slices (SplitTail)
-__device__ __forceinline__ void tile_order(const SplitTail& st, int grid_m, int grid_n, int& bm, int& bn,
-                                           int& slice, int& nsl, int& sidx) {
-  const int nwg = gridDim.x, orig = blockIdx.x;
+__device__ __forceinline__ void tile_order_v(const SplitTail& st, int grid_m, int grid_n, int orig, int nwg, int& bm,
+                                             int& bn, int& slice, int& nsl, int& sidx) {
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   int tile = wg;
@@ -600,6 +599,11 @@ __device__ __forceinline__ void tile_order(const SplitTail& st, int grid_m, int 
   const int in = tile - group * GM * grid_n;
   bm = first_m + in % gsz;
   bn = in / gsz;
+}
+
+__device__ __forceinline__ void tile_order(const SplitTail& st, int grid_m, int grid_n, int& bm, int& bn,
+                                           int& slice, int& nsl, int& sidx) {
+  tile_order_v(st, grid_m, grid_n, blockIdx.x, gridDim.x, bm, bn, slice, nsl, sidx);
 }
 
 template <int EPI, bool KEEPB>
@@ -1157,12 +1161,270 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   }
 }
 
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// ============================================================ persistent 4-wave GEMM
+// gemm_w4p_kernel: gemm_w4_kernel's K-loop, but one workgroup per CU walks the units
+// v = blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8, so every unit keeps the XCD
+// that tile_order gives it), and the next unit's K-steps 0 and 1 are issued into the LDS
+// buffers as soon as the current unit's last two steps free them (phase B of its last two
+// iterations), i.e. BEFORE the epilogue: the next tile's HBM latency overlaps the store
+// tail instead of following it.  The first K-step of a unit starts its accumulators with a
+// zero C operand (no zeroing pass).  Buffer of step t = (t + par) & 1, par carried across
+// units.  Whole tiles only: grids that need the tail split run gemm_w4_kernel.
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
+    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
+    const float* __restrict__ rs, int grid_m, int grid_n, SplitTail st, int nunits) {
+  __shared__ __attribute__((aligned(16))) char lds[2 * 65536 + 16];  // + the split ticket
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  // vector-memory operations per wave in one epilogue (+8 row-scale loads when rs)
+  constexpr int EPI_OPS = EPI == EPI_SILU ? 32 : EPI == EPI_RESID ? 128 : 64;
+  const __amdgpu_buffer_rsrc_t c_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)((int64_t)M * ldc * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)R, 0, R ? (int)((int64_t)M * ldr * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)rs, 0, rs ? M * 4 : 0, 0x00020000);
+
+  struct Unit {
+    int m0, n0, nK, slice, nsl, sidx;
+  };
+  // LDS-DMA sources of the unit being loaded: buffer descriptors + per-piece offsets
+  __amdgpu_buffer_rsrc_t src_a, src_b;
+  unsigned a_voff[8];
+  int b_soff[8];
+  auto unit_of = [&](int v) {
+    Unit u;
+    int bm, bn;
+    u.slice = 0;
+    u.nsl = 1;
+    u.sidx = 0;
+    tile_order_v(st, grid_m, grid_n, v, nunits, bm, bn, u.slice, u.nsl, u.sidx);
+    u.m0 = bm * 256;
+    u.n0 = bn * ((EPI == EPI_SILU) ? 128 : 256);
+    u.nK = KT / 2 / u.nsl;
+    return u;
+  };
+  auto gnt_of = [&](const Unit& u, int p) {  // B piece q = 8 * wave + p: n-tile j = q >> 1, k-half q & 1
+    const int j = (8 * wv + p) >> 1;
+    if constexpr (EPI == EPI_SILU) {  // wave column w: gate tiles 4w..4w+3, then the same up tiles
+      const int w = j >> 3, jj = j & 7;
+      return (jj < 4 ? 0 : n_tiles_w / 2) + u.n0 / 16 + 4 * w + (jj & 3);
+    } else {
+      return u.n0 / 16 + j;
+    }
+  };
+  auto src_of = [&](const Unit& u) {
+    const int k0 = u.slice * u.nK;
+    src_a = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)u.m0 * lda + k0 * 64), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int i = 64 * wave + 8 * p + (lane >> 3);  // image row 0..255
+      const int rr = (u.m0 + i < M ? i : M - 1 - u.m0);
+      const int chunk = (lane & 7) ^ ((i >> 1) & 7);
+      a_voff[p] = (unsigned)(rr * lda * 2 + chunk * 16);
+    }
+    const int g0 = gnt_of(u, 0);
+    src_b = __builtin_amdgcn_make_buffer_rsrc((void*)(Wp + ((int64_t)g0 * KT + 2 * k0) * 512), 0, 0x7fffffff,
+                                             0x00020000);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) b_soff[p] = ((gnt_of(u, p) - g0) * KT + (p & 1)) * 1024;
+  };
+  auto issue = [&](int p, int t, int buf) {  // piece p (0-7 A, 8-15 B) of K-step t
+    char* base = lds + buf * 65536;
+    if (p < 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(src_a, (lds_ptr)(base + (8 * wv + p) * 1024), 16, a_voff[p],
+                                               t * 128, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(src_b, (lds_ptr)(base + 32768 + (8 * wv + p - 8) * 1024), 16,
+                                               lane * 16, b_soff[p - 8] + t * 2048, 0, 0);
+  };
+
+  const int arow = wr * 128 + (lane & 15);
+  const int a_off0 = arow * 128 + 16 * ((lane >> 4) ^ ((arow >> 1) & 7));
+  const int a_off1 = arow * 128 + 16 * ((4 + (lane >> 4)) ^ ((arow >> 1) & 7));
+  const int b_off = 32768 + (8 * wc) * 2048 + lane * 16;
+  bf16x8 fa[2][8], fb[2][8];  // [k-half][tile]
+  auto read_a = [&](int kh, int mt, int buf) {
+    fa[kh][mt] = *(const bf16x8*)(lds + buf * 65536 + (kh ? a_off1 : a_off0) + mt * 2048);
+  };
+  auto read_b = [&](int kh, int nt, int buf) {
+    fb[kh][nt] = *(const bf16x8*)(lds + buf * 65536 + b_off + nt * 2048 + kh * 1024);
+  };
+  f32x4 acc[8][8];
+  auto acc_fence = [&]() {  // 16 wait states after the last MFMA, then every accumulator redefined
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i == 0)
+        asm volatile("s_nop 7\n\ts_nop 7" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
+                     "+a"(acc[i][4]), "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+      else
+        asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]), "+a"(acc[i][4]),
+                     "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+    }
+  };
+  // MFMA x of a K-step (0..127), nt-major inside each group of 32 (see gemm_w4_kernel);
+  // ZERO: the unit's first K-step, k-half 0 starts the accumulator from 0
+  auto mfx = [&](bool zero, int x) {  // zero: compile-time after inlining
+    const int kh = (x >= 64) ? 1 : 0;
+    const int q = x & 31, half = (x >> 5) & 1;
+    const int mt = 4 * half + (q & 3), nt = q >> 2;
+    if (zero && kh == 0)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc[mt][nt]) : "v"(fb[0][nt]), "v"(fa[0][mt]));
+    else
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[mt][nt]) : "v"(fb[kh][nt]), "v"(fa[kh][mt]));
+  };
+  using ZF = std::integral_constant<bool, false>;
+  using ZT = std::integral_constant<bool, true>;
+  // MODE 0: issue step t+2, wait for t+1, read F0 of t+1; 1 (t = nK-2): issue the next
+  // unit's step 0 (if any), wait for t+1, read; 2 (t = nK-1): issue the next unit's step 1
+  auto iter = [&](auto MODE, auto ZERO, int t, int par, bool has_next) {
+    constexpr int mode = decltype(MODE)::value;
+    const int c = (t + par) & 1;
+#pragma unroll
+    for (int x = 0; x < 32; ++x) {
+      if (x == 31) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      mfx(decltype(ZERO)::value, x);
+      if (x < 16) {
+        if (x < 8) read_b(1, x, c); else read_a(1, x - 8, c);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    raw_barrier();  // every wave is done reading buffer c
+#pragma unroll
+    for (int x = 32; x < 96; ++x) {
+      if (x == 95) {
+        if constexpr (mode == 0) {
+          vm_wait<16>();
+        } else if constexpr (mode == 1) {
+          if (has_next) vm_wait<16>(); else vm_wait<0>();
+        }
+      }
+      mfx(decltype(ZERO)::value, x);
+      if ((x & 3) == 0) {
+        if constexpr (mode == 0) {
+          issue((x - 32) >> 2, t + 2, c);
+        } else {
+          if (has_next) issue((x - 32) >> 2, mode == 1 ? 0 : 1, c);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    raw_barrier();  // step t+1 visible in buffer c ^ 1
+#pragma unroll
+    for (int x = 96; x < 128; ++x) {
+      mfx(decltype(ZERO)::value, x);
+      if constexpr (mode != 2) {
+        if (x < 112) {
+          if (x < 104) read_b(0, x - 96, c ^ 1); else read_a(0, x - 104, c ^ 1);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  int v = blockIdx.x;
+  Unit u = unit_of(v);
+  src_of(u);
+  int par = 0;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) issue(p, 0, 0);
+#pragma unroll
+  for (int p = 0; p < 16; ++p) issue(p, 1, 1);
+  bool first = true;
+  for (;;) {
+    // step 0 landed: younger than its pieces are step 1's 16 and, after the first unit, the
+    // previous epilogue's EPI_OPS (fewer only when a split slice drained with vmcnt(0))
+    if (first) {
+      vm_wait<16>();
+    } else if (rs) {
+      vm_wait<(16 + EPI_OPS + 8 < 63 ? 16 + EPI_OPS + 8 : 63)>();
+    } else {
+      vm_wait<(16 + EPI_OPS < 63 ? 16 + EPI_OPS : 63)>();
+    }
+    first = false;
+    raw_barrier();
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      read_b(0, g, par);
+      read_a(0, g, par);
+    }
+    iter(std::integral_constant<int, 0>{}, ZT{}, 0, par, false);
+    for (int t = 1; t < u.nK - 2; ++t) iter(std::integral_constant<int, 0>{}, ZF{}, t, par, false);
+    // this unit's loads are all issued: cur now describes the next unit
+    const int vn = v + gridDim.x;
+    const bool has_next = vn < nunits;
+    Unit un = u;
+    if (has_next) {
+      un = unit_of(vn);
+      src_of(un);
+    }
+    iter(std::integral_constant<int, 1>{}, ZF{}, u.nK - 2, par, has_next);
+    iter(std::integral_constant<int, 2>{}, ZF{}, u.nK - 1, par, has_next);
+    acc_fence();
+
+    {  // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
+      // buffer loads/stores: rows >= M are issued and dropped by the range check, so the
+      // epilogue's vector-memory count is fixed (EPI_OPS) and the next unit's wait is exact
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = u.m0 + wr * 128 + i * 16 + (lane & 15);
+        float sc = 1.0f;
+        if (rs) sc = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_rsrc, row * 4, 0, 0));
+        if constexpr (EPI == EPI_SILU) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const int col = u.n0 + wc * 64 + nt * 16 + 4 * (lane >> 4);
+            u16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float gg = rbf(acc[i][nt][r] * sc);
+              const float uu = rbf(acc[i][4 + nt][r] * sc);
+              o[r] = f2bf(rbf(silu_f(gg)) * uu);
+            }
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), c_rsrc, (row * (int)ldc + col) * 2, 0,
+                                                  0);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int col = u.n0 + wc * 128 + j * 16 + 4 * (lane >> 4);
+            u16x4 o;
+            u16x4 rr;
+            if constexpr (EPI == EPI_RESID)
+              rr = __builtin_bit_cast(u16x4, __builtin_amdgcn_raw_buffer_load_b64(r_rsrc, (row * (int)ldr + col) * 2,
+                                                                                   0, 0));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float x = acc[i][j][r] * sc;
+              if constexpr (EPI == EPI_RESID) x = rbf(x) + bf2f(rr[r]);
+              o[r] = f2bf(x);
+            }
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), c_rsrc, (row * (int)ldc + col) * 2, 0,
+                                                  0);
+          }
+        }
+      }
+    }
+    if (!has_next) break;
+    par = (par + u.nK) & 1;
+    u = un;
+    v = vn;
+  }
+}
+
 // INFERD_GEMM_TILE selects the prefill GEMM (read per call so one process can A/B them):
-// "w4" (default; "w4m" / "w4g" / "w4mg" its A/B arms) | "ring" | "256" | "128"
+// "w4p" (default: persistent w4, w4 where the grid needs a tail split) | "w4" ("w4m" / "w4g" /
+// "w4mg" its A/B arms) | "ring" | "256" | "128"
 static int gemm_tile_variant() {
   const char* e = getenv("INFERD_GEMM_TILE");
-  if (!e || !*e) return 7;
+  if (!e || !*e) return 8;
   if (e[0] == 'r') return 0;
+  if (e[0] == 'w' && e[2] == 'p') return 8;  // "w4p": persistent
   if (e[0] == 'w') {  // "w4" = "w4nb" (default) | "w4m": mt-major MFMA order | "w4g": global_load_lds
     int v = 7;
     for (const char* c = e + 2; *c; ++c) v &= (*c == 'm') ? ~1 : (*c == 'g') ? ~2 : ~0;
@@ -1191,6 +1453,7 @@ static void ring_launch(bool keepb, int grid, hipStream_t s, const u16* A, int64
                        ldr, M, rs, gm, gn, st);
 }
 
+#define SPLIT_MAX_DEVICES_ 16
 template <int ORD>
 static void w4_launch(int epi, int grid, hipStream_t s, const u16* A, int64_t lda, const u16* Wp, int KT, int ntw,
                       u16* C, int64_t ldc, const u16* R, int64_t ldr, int M, const float* rs, int gm, int gn,
@@ -1209,6 +1472,21 @@ static void w4_launch(int epi, int grid, hipStream_t s, const u16* A, int64_t ld
                          R, ldr, M, rs, gm, gn, st);
       break;
   }
+}
+
+// persistent grid: one workgroup per CU, a multiple of 8 (units keep their XCD), <= units
+static int w4p_grid(int units) {
+  static int ncu[SPLIT_MAX_DEVICES_] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= SPLIT_MAX_DEVICES_) dev = 0;
+  if (ncu[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    ncu[dev] = n;
+  }
+  const int cap = env_or("INFERD_W4P_GRID", 0) > 0 ? env_or("INFERD_W4P_GRID", 0) : ncu[dev];
+  if (units <= cap) return units;
+  return cap & ~7;
 }
 
 // Per device (a process may drive several GPUs); grown on demand, never inside a graph
@@ -1263,7 +1541,7 @@ static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
 
 static bool use_ring256(int M, int N, int K, int epi) {
   const int v = gemm_tile_variant();
-  if ((v != 0 && (v < 4 || v > 7)) || M < 512 || K < 192) return false;
+  if ((v != 0 && (v < 4 || v > 8)) || M < 512 || K < 192) return false;
   return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
 }
 
@@ -1296,7 +1574,27 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     const int grid = st.split > 1 ? 8 * st.units_per_xcd : gm * gn;
     // INFERD_GEMM_KEEPB=0 selects the look-ahead-6 schedule that re-reads B0 (A/B)
     const bool keepb = env_or("INFERD_GEMM_KEEPB", 1) != 0;
-    if (gemm_tile_variant() >= 4 && gemm_tile_variant() <= 7) {
+    // w4p addresses C / R through 32-bit buffer offsets
+    const bool fits32 = (int64_t)(M + 256) * ldc * 2 < 0x7fffffff && (!R || (int64_t)(M + 256) * ldr * 2 < 0x7fffffff);
+    if (gemm_tile_variant() == 8 && fits32 && st.split == 1) {
+      const int g = w4p_grid(grid);
+      switch (epi) {
+        case EPI_NONE:
+          hipLaunchKernelGGL(gemm_w4p_kernel<EPI_NONE>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
+                             M, rs, gm, gn, st, grid);
+          break;
+        case EPI_RESID:
+          hipLaunchKernelGGL(gemm_w4p_kernel<EPI_RESID>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
+                             M, rs, gm, gn, st, grid);
+          break;
+        default:
+          hipLaunchKernelGGL(gemm_w4p_kernel<EPI_SILU>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
+                             M, rs, gm, gn, st, grid);
+          break;
+      }
+      return;
+    }
+    if (gemm_tile_variant() >= 4 && gemm_tile_variant() <= 8) {  // w4p with a tail split: w4
       switch (gemm_tile_variant()) {
         case 4: w4_launch<0>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
         case 5: w4_launch<1>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;

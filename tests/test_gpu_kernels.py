@@ -137,7 +137,7 @@ def test_gemm_swiglu(lib, M, K):
     assert (bf16_ulp_diff(c.cpu(), ref.cpu()) > 2).float().mean() < 2e-3
 
 
-@pytest.mark.parametrize("variant", ["ring", "w4", "w4mg", "256", "128"])
+@pytest.mark.parametrize("variant", ["ring", "w4", "w4mg", "w4p", "256", "128"])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 192), (777, 768, 1088), (2048, 1024, 4096), (1300, 256, 640),
                                    (4096, 2048, 1024)])
 def test_gemm_prefill_variants(lib, monkeypatch, variant, M, N, K):
