@@ -139,10 +139,12 @@ def test_gemm_swiglu(lib, M, K):
 
 @pytest.mark.parametrize("variant", ["ring", "w4", "w4mg", "w4p", "256", "128"])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 192), (777, 768, 1088), (2048, 1024, 4096), (1300, 256, 640),
-                                   (4096, 2048, 1024)])
+                                   (4096, 2048, 1024), (8092, 4096, 448)])
 def test_gemm_prefill_variants(lib, monkeypatch, variant, M, N, K):
     """Every prefill GEMM body (INFERD_GEMM_TILE) on ragged M, short and long K, all epilogues.
-    (2048, 1024, 4096) and (4096, 2048, 1024) run the ring kernel's tail split (K cut 8 / 2 ways)."""
+    (2048, 1024, 4096) and (4096, 2048, 1024) run the tail split (K cut 8 / 2 ways);
+    (8092, 4096, 448): 512 whole tiles, so the persistent w4p walks two tiles per workgroup
+    (ragged last row block, cross-tile prefetch, exact-count epilogue waits)."""
     monkeypatch.setenv("INFERD_GEMM_TILE", variant)
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
