@@ -128,6 +128,15 @@ class PipelineStage:
 
     def _exchange(self, send=None, send_to=None, recv=None, recv_from=None):
         import torch.distributed as dist
+        # gloo (CPU-rank tests, or GPU ranks rehearsing without RCCL): device tensors are
+        # staged through host memory; RCCL moves them GPU to GPU
+        staged = dist.get_backend(self.group) == "gloo"
+        dst = None
+        if staged:
+            if send is not None and send.is_cuda:
+                send = send.cpu()
+            if recv is not None and recv.is_cuda:
+                dst, recv = recv, torch.empty(recv.shape, dtype=recv.dtype)
         ops = []
         if send is not None:
             ops.append(dist.P2POp(dist.isend, send, send_to, self.group))
@@ -136,6 +145,8 @@ class PipelineStage:
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+        if dst is not None:
+            dst.copy_(recv)
 
     # ------------------------------------------------------------------ prefill
     @torch.no_grad()

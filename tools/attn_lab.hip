@@ -30,6 +30,65 @@ __global__ void fill_kernel(u16* p, size_t n, uint64_t seed) {
   }
 }
 
+// Control: the decode kernel's exact read pattern (grid (nc, KV, B), each workgroup's pages,
+// 32-token half-page items dealt over NW waves, 16 B per lane) with no compute -- the
+// achievable rate of this access pattern.  DEPTH items in flight per wave.
+template <int NW, int DEPTH>
+__global__ __launch_bounds__(NW * 64) void stream_kv_kernel(const u16* __restrict__ kv, AttnBatch b, int KV, int nc,
+                                                            unsigned* __restrict__ sink) {
+  const int c = blockIdx.x, g = blockIdx.y, s = blockIdx.z;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int np = (b.ctx_lens[s] + KV_PAGE - 1) / KV_PAGE;
+  const int p0 = c * np / nc, p1 = (c + 1) * np / nc;
+  const int* bt = b.block_table + (int64_t)s * b.max_pages;
+  unsigned x = 0;
+  const int n_items = 2 * (p1 - p0);
+  for (int u0 = wave; u0 < n_items; u0 += NW * DEPTH) {
+    bf16x8 r[DEPTH][16];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const int u = u0 + d * NW;
+      if (u >= n_items) break;
+      const int phys = bt[p0 + (u >> 1)];
+      const u16* kb = kv + ((int64_t)(phys * 2 + 0) * KV + g) * KV_BLOCK_ELEMS + (u & 1) * (KV_BLOCK_ELEMS / 2);
+      const u16* vb = kv + ((int64_t)(phys * 2 + 1) * KV + g) * KV_BLOCK_ELEMS + (u & 1) * (KV_BLOCK_ELEMS / 2);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[d][i] = *(const bf16x8*)(kb + i * 512 + lane * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[d][8 + i] = *(const bf16x8*)(vb + i * 512 + lane * 8);
+    }
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        const u32x4_t w = __builtin_bit_cast(u32x4_t, r[d][i]);
+        x ^= w[0] ^ w[1] ^ w[2] ^ w[3];
+      }
+  }
+  if (x == 0x12345u) sink[0] = x;
+}
+
+// Control 2: a flat read of the same number of bytes (contiguous, grid-stride, 16 B per lane,
+// UNROLL loads in flight per lane) -- the floor for a one-shot ~134 MB read.
+template <int UNROLL>
+__global__ __launch_bounds__(256) void flat_read_kernel(const bf16x8* __restrict__ p, size_t n, unsigned* sink) {
+  unsigned x = 0;
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride * UNROLL) {
+    bf16x8 r[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) r[u] = (i + u * stride < n) ? p[i + u * stride] : bf16x8{};
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      const u32x4_t w = __builtin_bit_cast(u32x4_t, r[u]);
+      x ^= w[0] ^ w[1] ^ w[2] ^ w[3];
+    }
+  }
+  if (x == 0x12345u) sink[0] = x;
+}
+
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 16;
   const int ctx = argc > 2 ? atoi(argv[2]) : 2100;
@@ -112,6 +171,45 @@ int main(int argc, char** argv) {
     const double us = ms * 1e3 / iters;
     printf("  %-26s %8.2f us  %7.0f GB/s  maxdiff %.3e\n", name, us, bytes / (us * 1e-6) / 1e9, md);
   };
+  unsigned* sink;
+  CHECK(hipMalloc(&sink, 64));
+  auto control = [&](const char* name, auto launch) {  // time only
+    for (int it = 0; it < R; ++it) launch(pools[it % R]);
+    const int iters = 6 * R;
+    CHECK(hipEventRecord(e0));
+    for (int it = 0; it < iters; ++it) launch(pools[it % R]);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / iters;
+    printf("  %-26s %8.2f us  %7.0f GB/s  (read-only control)\n", name, us, bytes / (us * 1e-6) / 1e9);
+  };
+  const size_t nvec = (size_t)(bytes / 16);
+  control("flat read 1024 WG x8", [&](u16* kvp) {
+    hipLaunchKernelGGL((flat_read_kernel<8>), dim3(1024), dim3(256), 0, 0, (const bf16x8*)kvp, nvec, sink);
+  });
+  control("flat read 2048 WG x4", [&](u16* kvp) {
+    hipLaunchKernelGGL((flat_read_kernel<4>), dim3(2048), dim3(256), 0, 0, (const bf16x8*)kvp, nvec, sink);
+  });
+  control("flat read 4096 WG x4", [&](u16* kvp) {
+    hipLaunchKernelGGL((flat_read_kernel<4>), dim3(4096), dim3(256), 0, 0, (const bf16x8*)kvp, nvec, sink);
+  });
+  control("stream nw8 nc2 depth2", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_kv_kernel<8, 2>), dim3(2, KV, B), dim3(512), 0, 0, kvp, ab, KV, 2, sink);
+  });
+  control("stream nw8 nc2 depth4", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_kv_kernel<8, 4>), dim3(2, KV, B), dim3(512), 0, 0, kvp, ab, KV, 2, sink);
+  });
+  control("stream nw8 nc4 depth2", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_kv_kernel<8, 2>), dim3(4, KV, B), dim3(512), 0, 0, kvp, ab, KV, 4, sink);
+  });
+  control("stream nw4 nc4 depth4", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_kv_kernel<4, 4>), dim3(4, KV, B), dim3(256), 0, 0, kvp, ab, KV, 4, sink);
+  });
+  control("stream nw16 nc1 depth2", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_kv_kernel<16, 2>), dim3(1, KV, B), dim3(1024), 0, 0, kvp, ab, KV, 1, sink);
+  });
   run("engine default shape", [&](u16* kvp) {
     launch_attn_decode(q, kvp, ab, H, KV, 1.0f / sqrtf(128.f), out, ws, 0);
   });
