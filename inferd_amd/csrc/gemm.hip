@@ -1163,6 +1163,124 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
+
+// EPI_QKV epilogue of one wave's 128 x 128 block = one head (q, k or v) of 128 rows: the
+// arithmetic of qk_norm_rope_kv_kernel (elementwise.hip) on the accumulators.  Lane l holds
+// rows row0 + 16 i + (l & 15), dims d = 16 nt + 4 (l >> 4) + r; the 4 lanes of a row (l,
+// l^16, l^32, l^48) hold all 128 dims, and dims d and d + 64 (RoPE's rotate_half pair) sit
+// in the same lane (nt and nt + 4).
+__device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const QkvEpilogue& e, int row0, int hd, int M,
+                                             const float* __restrict__ rs, int lane) {
+  const int q4 = lane >> 4;  // dims 4*q4 .. 4*q4+3 of every 16-dim tile
+  if (hd < e.H + e.KV) {
+    const bool isq = hd < e.H;
+    const u16* nw = isq ? e.qn_w : e.kn_w;
+    u16x4 wv[8];
+#pragma unroll
+    for (int nt = 0; nt < 8; ++nt) wv[nt] = *(const u16x4*)(nw + 16 * nt + 4 * q4);
+    // per-row operands up front, the cos/sin rows two-deep: the loads of row i+1 are in
+    // flight while row i computes (dependent per-row loads were the epilogue's cost)
+    int pos[8], slot[8];
+    float scv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = row0 + 16 * i + (lane & 15);
+      const int rowc = row < M ? row : M - 1;
+      pos[i] = e.positions[rowc];
+      slot[i] = isq ? 0 : e.slots[rowc];
+      scv[i] = rs ? rs[rowc] : 1.0f;
+    }
+    u16x4 cvb[2][4], svb[2][4];
+    auto load_cs = [&](int i, int bsel) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        cvb[bsel][nt] = *(const u16x4*)(e.cos_t + (int64_t)pos[i] * 64 + 16 * nt + 4 * q4);
+        svb[bsel][nt] = *(const u16x4*)(e.sin_t + (int64_t)pos[i] * 64 + 16 * nt + 4 * q4);
+      }
+    };
+    load_cs(0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i + 1 < 8) load_cs(i + 1, (i + 1) & 1);
+      const int row = row0 + 16 * i + (lane & 15);
+      const float sc = scv[i];
+      float x[8][4];
+      float ss = 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          x[nt][r] = rbf(acc[i][nt][r] * sc);  // the bf16 projection output
+          ss = fmaf(x[nt][r], x[nt][r], ss);
+        }
+      ss += __shfl_xor(ss, 16);
+      ss += __shfl_xor(ss, 32);
+      const float inv = 1.0f / sqrtf(ss / 128.0f + e.eps);
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[nt][r] = rbf(bf2f(wv[nt][r]) * rbf(x[nt][r] * inv));
+      u16x4 o[8];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const u16x4 cv = cvb[i & 1][nt], sv = svb[i & 1][nt];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float c = bf2f(cv[r]), sn = bf2f(sv[r]);
+          o[nt][r] = f2bf(rbf(x[nt][r] * c) + rbf(-x[nt + 4][r] * sn));
+          o[nt + 4][r] = f2bf(rbf(x[nt + 4][r] * c) + rbf(x[nt][r] * sn));
+        }
+      }
+      if (row >= M) continue;
+      if (isq) {
+        u16* qp = e.q_out + ((int64_t)row * e.H + hd) * HEAD_DIM + 4 * q4;
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) *(u16x4*)(qp + 16 * nt) = o[nt];
+      } else {
+        if (slot[i] < 0) continue;
+        const int page = slot[i] >> 6, s = slot[i] & 63, g = hd - e.H;
+        u16* blk = e.kv_layer + ((int64_t)(page * 2 + 0) * e.KV + g) * KV_BLOCK_ELEMS;
+#pragma unroll
+        for (int nt = 0; nt < 8; ++nt) {  // K tile layout: 8-dim chunk c8 = d >> 3, element d & 7
+          const int c8 = 2 * nt + (q4 >> 1);
+          const int ln = (s & 15) + 16 * (c8 & 3);
+          *(u16x4*)(blk + (((s >> 4) * 4 + (c8 >> 2)) * 64 + ln) * 8 + 4 * (q4 & 1)) = o[nt];
+        }
+      }
+    }
+  } else {  // v head: the bf16 projection output, scattered into the V^T tile layout
+    const int g = hd - e.H - e.KV;
+    int slots[8];
+    float scv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int rowc = min(row0 + 16 * i + (lane & 15), M - 1);
+      slots[i] = e.slots[rowc];
+      scv[i] = rs ? rs[rowc] : 1.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = row0 + 16 * i + (lane & 15);
+      if (row >= M) continue;
+      const int slot = slots[i];
+      if (slot < 0) continue;
+      const float sc = scv[i];
+      const int page = slot >> 6, s = slot & 63;
+      u16* blk = e.kv_layer + ((int64_t)(page * 2 + 1) * e.KV + g) * KV_BLOCK_ELEMS;
+      const int kt = s >> 5, tp = s & 31;
+      const int gg = tp < 16 ? (tp >> 2) : ((tp - 16) >> 2);
+      const int jj = tp < 16 ? (tp & 3) : 4 + ((tp - 16) & 3);
+#pragma unroll
+      for (int nt = 0; nt < 8; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ln = 4 * q4 + r + 16 * gg;  // d & 15 = 4 q4 + r, d >> 4 = nt
+          blk[((kt * 8 + nt) * 64 + ln) * 8 + jj] = f2bf(acc[i][nt][r] * sc);
+        }
+    }
+  }
+}
+
 // ============================================================ persistent 4-wave GEMM
 // gemm_w4p_kernel: gemm_w4_kernel's K-loop, but one workgroup per CU walks the units
 // v = blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8, so every unit keeps the XCD
@@ -1176,7 +1294,7 @@ template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
     u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    const float* __restrict__ rs, int grid_m, int grid_n, SplitTail st, int nunits) {
+    const float* __restrict__ rs, int grid_m, int grid_n, SplitTail st, int nunits, QkvEpilogue qe) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 65536 + 16];  // + the split ticket
   typedef __attribute__((address_space(3))) void* lds_ptr;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1339,7 +1457,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
   for (;;) {
     // step 0 landed: younger than its pieces are step 1's 16 and, after the first unit, the
     // previous epilogue's EPI_OPS (fewer only when a split slice drained with vmcnt(0))
-    if (first) {
+    if (first || EPI == EPI_QKV) {  // EPI_QKV: its epilogue's count varies by head kind
       vm_wait<16>();
     } else if (rs) {
       vm_wait<(16 + EPI_OPS + 8 < 63 ? 16 + EPI_OPS + 8 : 63)>();
@@ -1359,15 +1477,21 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     const int vn = v + gridDim.x;
     const bool has_next = vn < nunits;
     Unit un = u;
+    // EPI_QKV: no cross-tile prefetch -- its epilogue's own loads (positions, cos/sin,
+    // slots) would wait behind the next tile's 32 in-flight pieces (in-order vmcnt); the
+    // next tile's sources are then computed after the epilogue (fewer live registers in it)
+    constexpr bool XPF = EPI != EPI_QKV;
     if (has_next) {
       un = unit_of(vn);
-      src_of(un);
+      if constexpr (XPF) src_of(un);
     }
-    iter(std::integral_constant<int, 1>{}, ZF{}, u.nK - 2, par, has_next);
-    iter(std::integral_constant<int, 2>{}, ZF{}, u.nK - 1, par, has_next);
+    iter(std::integral_constant<int, 1>{}, ZF{}, u.nK - 2, par, XPF && has_next);
+    iter(std::integral_constant<int, 2>{}, ZF{}, u.nK - 1, par, XPF && has_next);
     acc_fence();
 
-    {  // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
+    if constexpr (EPI == EPI_QKV) {
+      qkv_epilogue(acc, qe, u.m0 + wr * 128, (u.n0 >> 7) + wc, M, rs, lane);
+    } else {  // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
       // buffer loads/stores: rows >= M are issued and dropped by the range check, so the
       // epilogue's vector-memory count is fixed (EPI_OPS) and the next unit's wait is exact
 #pragma unroll
@@ -1414,6 +1538,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     par = (par + u.nK) & 1;
     u = un;
     v = vn;
+    if constexpr (!XPF) {  // the next tile's steps 0 and 1, issued after the epilogue
+      src_of(u);
+#pragma unroll
+      for (int p = 0; p < 16; ++p) issue(p, 0, par);
+#pragma unroll
+      for (int p = 0; p < 16; ++p) issue(p, 1, par ^ 1);
+    }
   }
 }
 
@@ -1581,15 +1712,15 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
       switch (epi) {
         case EPI_NONE:
           hipLaunchKernelGGL(gemm_w4p_kernel<EPI_NONE>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
-                             M, rs, gm, gn, st, grid);
+                             M, rs, gm, gn, st, grid, QkvEpilogue{});
           break;
         case EPI_RESID:
           hipLaunchKernelGGL(gemm_w4p_kernel<EPI_RESID>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
-                             M, rs, gm, gn, st, grid);
+                             M, rs, gm, gn, st, grid, QkvEpilogue{});
           break;
         default:
           hipLaunchKernelGGL(gemm_w4p_kernel<EPI_SILU>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
-                             M, rs, gm, gn, st, grid);
+                             M, rs, gm, gn, st, grid, QkvEpilogue{});
           break;
       }
       return;
@@ -1710,4 +1841,36 @@ __global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long 
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M, int32_t* ids,
                           hipStream_t s) {
   hipLaunchKernelGGL(argmax_reduce_kernel, dim3(M), dim3(256), 0, s, partial, n_tiles, M, ids);
+}
+
+// ============================================================ fused prefill q/k/v projection
+// launch_gemm's persistent whole-tile path with the EPI_QKV epilogue: q/k RMSNorm + RoPE to
+// q_out and the K cache, V to the cache (what launch_qk_norm_rope_kv does from a stored q/k/v
+// row).  Needs that path: the 4-wave persistent kernel selected, no tail split, 32-bit C offsets
+// (C is unused here) and one head per wave column (N = (H + 2 KV) * 128).
+// INFERD_FUSE_QKV_EPI=0 keeps the two-kernel path (A/B).
+bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const RowNorm* norm,
+                           const QkvEpilogue& e, hipStream_t s) {
+  if (env_or("INFERD_FUSE_QKV_EPI", 1) == 0) return false;
+  if (gemm_tile_variant() != 8 || !gemm_uses_tiled(M, N, K, EPI_NONE) || !use_ring256(M, N, K, EPI_NONE)) return false;
+  if (N != (e.H + 2 * e.KV) * HEAD_DIM) return false;
+  const int gm = (M + 255) / 256, gn = N / 256;
+  const int tiles = gm * gn, nK = K / 64;
+  // the tail-split decision of plan_split_tail, without its workspace
+  if (tiles % 8 == 0) {
+    const int rem = (tiles / 8) % 32;
+    if (rem != 0 && 32 % rem == 0) {
+      const int split = 32 / rem;
+      if (split <= 8 && nK % split == 0 && nK / split >= 3) return false;
+    }
+  }
+  const float* rs = nullptr;
+  if (norm) {
+    launch_row_inv_rms(A, lda, M, K, norm->eps, norm->rs_ws, s);
+    rs = norm->rs_ws;
+  }
+  const SplitTail st = {1, 0, 0, 0, nullptr, nullptr};
+  hipLaunchKernelGGL(gemm_w4p_kernel<EPI_QKV>, dim3(w4p_grid(tiles)), dim3(256), 0, s, A, lda, Wp, K / 32, N / 16,
+                     (u16*)nullptr, (int64_t)0, (const u16*)nullptr, (int64_t)0, M, rs, gm, gn, st, tiles, e);
+  return true;
 }

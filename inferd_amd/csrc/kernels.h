@@ -12,6 +12,21 @@ enum GemmEpilogue {
   EPI_SILU = 2,    // C = bf16(bf16(silu(bf16(g))) * bf16(u)) with [gate; up] packed weight
   EPI_ARGMAX = 3,  // per-row partial argmax keys of bf16(acc) (+ optional bf16 logits in C)
   EPI_PARTIAL = 4, // internal: fp32 K-slice partials (+ row sums of squares), reduced by the consumer
+  EPI_QKV = 5,     // internal: prefill q/k/v projection with q/k RMSNorm + RoPE and the K/V cache write
+};
+
+// EPI_QKV epilogue operands (qk_norm_rope_kv_kernel's, applied to the GEMM's tile in registers)
+struct QkvEpilogue {
+  const int32_t* positions;
+  const int32_t* slots;
+  const u16* qn_w;
+  const u16* kn_w;
+  const u16* cos_t;
+  const u16* sin_t;
+  u16* q_out;
+  u16* kv_layer;
+  int H, KV;
+  float eps;
 };
 
 // elementwise.hip
@@ -49,6 +64,11 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
                  const RowNorm* norm = nullptr);
 // decode q/k/v with K split over `kslices` (M <= 16, NORM folded): part [kslices][M][N] fp32,
 // ssq [kslices][M] fp32; the fused decode attention reduces them
+// prefill q/k/v projection fused with q/k RMSNorm + RoPE and the K/V cache write (the
+// persistent GEMM's epilogue); returns false, launching nothing, where that body does not
+// apply (the caller then runs launch_gemm + launch_qk_norm_rope_kv)
+bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const RowNorm* norm,
+                           const QkvEpilogue& e, hipStream_t s);
 void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
                                 float* part, float* ssq, float eps, hipStream_t s);
 // rs[row] = 1 / sqrt(mean(x[row][:K]^2) + eps)

@@ -429,10 +429,19 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     const bool fused = b->decode && fuse_decode_rope();
     const int ksl = (fused && M <= 16) ? qkv_split(h) : 1;
     pe = s->prof_begin(PROF_QKV, st);
-    if (ksl > 1)
+    // prefill: q/k norm + RoPE and the K/V cache write in the projection's epilogue when
+    // the persistent GEMM runs it (else the separate qk_norm_rope_kv launch below)
+    bool qkv_done = false;
+    if (ksl > 1) {
       launch_gemm_decode_partial(x, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, s->qkv_ssq, c.rms_eps, st);
-    else
-      launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &rn);
+    } else {
+      if (!b->decode && !fuse_prefill_rope()) {
+        const QkvEpilogue qe = {b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t, s->sin_t, s->q, kv_l,
+                                H, KV, c.rms_eps};
+        qkv_done = launch_gemm_qkv_fused(x, h, W.qkv, M, qkvN, h, &rn, qe, st);
+      }
+      if (!qkv_done) launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &rn);
+    }
     s->prof_end(pe, st);
     if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
@@ -447,10 +456,12 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       // prefill: the attention kernel applies the q-norm + RoPE itself; this launch then
       // only normalises / rotates K and writes K/V to the cache
       const bool fq = !b->decode && fuse_prefill_rope();
-      pe = s->prof_begin(PROF_ROPE, st);
-      launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
-                             s->sin_t, s->q, kv_l, M, H, KV, c.rms_eps, st, fq);
-      s->prof_end(pe, st);
+      if (!qkv_done) {
+        pe = s->prof_begin(PROF_ROPE, st);
+        launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
+                               s->sin_t, s->q, kv_l, M, H, KV, c.rms_eps, st, fq);
+        s->prof_end(pe, st);
+      }
       pe = s->prof_begin(PROF_ATTN, st);
       if (b->decode)
         launch_attn_decode(s->q, kv_l, ab, H, KV, scale, s->attn, s->attn_ws, st);
