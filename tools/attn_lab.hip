@@ -185,6 +185,26 @@ int main(int argc, char** argv) {
     const double us = ms * 1e3 / iters;
     printf("  %-26s %8.2f us  %7.0f GB/s  (read-only control)\n", name, us, bytes / (us * 1e-6) / 1e9);
   };
+  // flat one-shot read floors at the decode step's per-kernel byte counts (Qwen3-8B B=16:
+  // o 33.5, q/k/v 50.3, down 100.7, attention 134.2, gate/up 201.3 MB)
+  for (double mb : {33.5, 50.3, 100.7, 134.2, 201.3}) {
+    const size_t nv = (size_t)(mb * 1e6 / 16);
+    if (nv * 16 > pool_bytes) continue;
+    for (int wg : {1024, 2048, 4096}) {
+      for (int it = 0; it < R; ++it)
+        hipLaunchKernelGGL((flat_read_kernel<4>), dim3(wg), dim3(256), 0, 0, (const bf16x8*)pools[it % R], nv, sink);
+      const int iters = 6 * R;
+      CHECK(hipEventRecord(e0));
+      for (int it = 0; it < iters; ++it)
+        hipLaunchKernelGGL((flat_read_kernel<4>), dim3(wg), dim3(256), 0, 0, (const bf16x8*)pools[it % R], nv, sink);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1e3 / iters;
+      printf("  flat read %6.1f MB  %4d WG  %8.2f us  %7.0f GB/s\n", mb, wg, us, mb * 1e6 / (us * 1e-6) / 1e9);
+    }
+  }
   const size_t nvec = (size_t)(bytes / 16);
   control("flat read 1024 WG x8", [&](u16* kvp) {
     hipLaunchKernelGGL((flat_read_kernel<8>), dim3(1024), dim3(256), 0, 0, (const bf16x8*)kvp, nvec, sink);
