@@ -163,7 +163,10 @@ int inferd_span_error_flags(InferdSpan* span, int32_t* flags);
 int inferd_span_profile_start(InferdSpan* span, int32_t max_pairs);
 int inferd_span_profile_stop(InferdSpan* span, double* total_ms, int32_t* counts, int32_t n_classes);
 
-/* Device base pointer of one layer's KV pool ([pages][K|V][kv_heads][64*128] bf16). */
+/* Device base pointer of one layer's KV pool: bf16
+ * [pages / 16][kv_heads][pages % 16][K|V][64*128] (super-pages of 16 pages; a pool spans
+ * whole super-pages, so callers of the single-op entry points below round their pool up to a
+ * multiple of 16 pages). */
 int inferd_span_kv_layer(InferdSpan* span, int32_t layer, void** out);
 /* Zero the KV pool. */
 int inferd_span_kv_clear(InferdSpan* span, void* stream);

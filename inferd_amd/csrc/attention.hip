@@ -195,7 +195,7 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
     ko[j] = f2bf(rbf(x[j] * bf2f(cv[j])) + rbf(rot * bf2f(sv[j])));
   }
   if (lane < 16) {
-    u16* blk = kv + ((int64_t)(page * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
+    u16* blk = kv + kv_block(page, 0, g, KV);
     const int tb = s >> 4, ks = c >> 2, ln = (s & 15) + 16 * (c & 3);
     *(u16x8*)(blk + ((tb * 4 + ks) * 64 + ln) * 8) = ko;
   } else if (lane < 32) {
@@ -204,7 +204,7 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
     u16x8 vraw;
 #pragma unroll
     for (int j = 0; j < 8; ++j) vraw[j] = f2bf(vx[j]);
-    u16* blk = kv + ((int64_t)(page * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
+    u16* blk = kv + kv_block(page, 1, g, KV);
     const int kt = s >> 5, tp = s & 31;
     const int gg = tp < 16 ? (tp >> 2) : ((tp - 16) >> 2);
     const int jj = tp < 16 ? (tp & 3) : 4 + ((tp - 16) & 3);
@@ -247,10 +247,10 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
   int u = u_begin + wave;
   const bool has_item = u < u_end;
   auto kaddr = [&](int uu) {
-    return (const bf16x8*)(kv + ((int64_t)(bt[uu >> 1] * 2 + 0) * KV + g) * KV_BLOCK_ELEMS) + (uu & 1) * 512 + lane;
+    return (const bf16x8*)(kv + kv_block(bt[uu >> 1], 0, g, KV)) + (uu & 1) * 512 + lane;
   };
   auto vaddr = [&](int uu) {
-    return (const bf16x8*)(kv + ((int64_t)(bt[uu >> 1] * 2 + 1) * KV + g) * KV_BLOCK_ELEMS) + (uu & 1) * 512 + lane;
+    return (const bf16x8*)(kv + kv_block(bt[uu >> 1], 1, g, KV)) + (uu & 1) * 512 + lane;
   };
   // The first two items' K/V loads (a 2-deep register ring: item j+2 is issued as soon as
   // item j's registers are consumed, so each wave always has two half pages in flight) are
@@ -648,8 +648,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
   auto stage = [&](int buf, int pi) {
     const int phys = bt[pi];
-    const u16* kblk = kv + ((int64_t)(phys * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
-    const u16* vblk = kv + ((int64_t)(phys * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
+    const u16* kblk = kv + kv_block(phys, 0, g, KV);
+    const u16* vblk = kv + kv_block(phys, 1, g, KV);
     char* base = lds + buf * 32768;
 #pragma unroll
     for (int pc = 0; pc < 8; ++pc) {
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(512, 1) void attn_prefill8_kernel(const u16* __rest
   auto issue = [&](int kind, int j) {  // kind 0 = K, 1 = V
     if (j >= n_pages) return;
     const int phys = __builtin_amdgcn_readfirstlane(tab[j]);
-    const u16* blk = kv + ((int64_t)(phys * 2 + kind) * KV + g) * KV_BLOCK_ELEMS + wave * 1024 + lane * 8;
+    const u16* blk = kv + kv_block(phys, kind, g, KV) + wave * 1024 + lane * 8;
     char* dst = lds + (kind * 4 + (j & 3)) * 16384 + wave * 2048;
     __builtin_amdgcn_global_load_lds((const void*)blk, (void*)dst, 16, 0, 0);
     __builtin_amdgcn_global_load_lds((const void*)(blk + 512), (void*)(dst + 1024), 16, 0, 0);

@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
       } else if (slot >= 0) {
         int g = hsafe - H;
         int page = slot >> 6, s = slot & 63;
-        u16* blk = kv_layer + ((int64_t)(page * 2 + 0) * KV + g) * KV_BLOCK_ELEMS;
+        u16* blk = kv_layer + kv_block(page, 0, g, KV);
         int tb = s >> 4, ks = c >> 2, lane = (s & 15) + 16 * (c & 3);
         *(u16x8*)(blk + ((tb * 4 + ks) * 64 + lane) * 8) = o;
       }
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
   } else if (active && slot >= 0) {  // v head: scatter into the V^T tile layout
     int g = hsafe - H - KV;
     int page = slot >> 6, s = slot & 63;
-    u16* blk = kv_layer + ((int64_t)(page * 2 + 1) * KV + g) * KV_BLOCK_ELEMS;
+    u16* blk = kv_layer + kv_block(page, 1, g, KV);
     int kt = s >> 5, tp = s & 31;
     int gg = tp < 16 ? (tp >> 2) : ((tp - 16) >> 2);
     int jj = tp < 16 ? (tp & 3) : 4 + ((tp - 16) & 3);

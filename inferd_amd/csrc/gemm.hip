@@ -1239,7 +1239,7 @@ __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const Qkv
       } else {
         if (slot[i] < 0) continue;
         const int page = slot[i] >> 6, s = slot[i] & 63, g = hd - e.H;
-        u16* blk = e.kv_layer + ((int64_t)(page * 2 + 0) * e.KV + g) * KV_BLOCK_ELEMS;
+        u16* blk = e.kv_layer + kv_block(page, 0, g, e.KV);
 #pragma unroll
         for (int nt = 0; nt < 8; ++nt) {  // K tile layout: 8-dim chunk c8 = d >> 3, element d & 7
           const int c8 = 2 * nt + (q4 >> 1);
@@ -1266,7 +1266,7 @@ __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const Qkv
       if (slot < 0) continue;
       const float sc = scv[i];
       const int page = slot >> 6, s = slot & 63;
-      u16* blk = e.kv_layer + ((int64_t)(page * 2 + 1) * e.KV + g) * KV_BLOCK_ELEMS;
+      u16* blk = e.kv_layer + kv_block(page, 1, g, e.KV);
       const int kt = s >> 5, tp = s & 31;
       const int gg = tp < 16 ? (tp >> 2) : ((tp - 16) >> 2);
       const int jj = tp < 16 ? (tp & 3) : 4 + ((tp - 16) & 3);

@@ -198,7 +198,8 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
     launch_rope_table(dinv, c.max_positions, s->cos_t, s->sin_t, 0);
   }
   // KV pool
-  s->kv_layer_elems = (size_t)c.kv_pages * 2 * KV * KV_BLOCK_ELEMS;
+  // whole super-pages (common.h: KV_SUPER)
+  s->kv_layer_elems = (size_t)((c.kv_pages + KV_SUPER - 1) / KV_SUPER * KV_SUPER) * 2 * KV * KV_BLOCK_ELEMS;
   if (c.n_layers > 0) {
     SALLOC(s->kv_pool, s->kv_layer_elems * c.n_layers * 2);
     if (hipMemset(s->kv_pool, 0, s->kv_layer_elems * c.n_layers * 2) != hipSuccess)

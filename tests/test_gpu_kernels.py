@@ -182,7 +182,8 @@ def test_qk_norm_rope_golden_and_cache(lib):
     lib.check(L.inferd_rope_table(d.rope_theta, 128, 40960, cos_t.data_ptr(), sin_t.data_ptr(), lib.stream_ptr()))
     pages = [3, 1, 5]
     slots = torch.tensor([pages[(100 + i) // 64] * 64 + (100 + i) % 64 for i in range(T)], dtype=torch.int32, device=DEV)
-    kv = torch.zeros(8 * 2 * d.kv_heads * 64 * 128, dtype=torch.bfloat16, device=DEV)
+    from kv_layout import pool_elems
+    kv = torch.zeros(pool_elems(8, d.kv_heads), dtype=torch.bfloat16, device=DEV)
     q_out = torch.empty(T, d.heads, 128, dtype=torch.bfloat16, device=DEV)
     qn_d, kn_d = W["q_norm"].to(DEV), W["k_norm"].to(DEV)
     lib.check(L.inferd_qk_norm_rope_kv(qkv.data_ptr(), pos.data_ptr(), slots.data_ptr(), qn_d.data_ptr(),
@@ -223,13 +224,12 @@ def test_rope_table_matches_hf(lib):
 def _attn_case(lib, H, KV, q_lens, past_lens, seed=0):
     """Random bf16 q/K/V; K/V written into shuffled pages; compare with fp32 SDPA."""
     from inferd_amd.runtime import PagePool, SeqState, build_batch
-    from kv_layout import K_IDX, V_IDX
+    from kv_layout import K_IDX, V_IDX, block, pool_elems
     torch.manual_seed(seed)
     L = lib.load()
     pool = PagePool(256)
     pool._free = list(np.random.default_rng(seed).permutation(256))
-    kv = torch.zeros(256 * 2 * KV * 64 * 128, dtype=torch.bfloat16)
-    blocks = kv.view(256, 2, KV, 64 * 128)
+    kv = torch.zeros(pool_elems(256, KV), dtype=torch.bfloat16)
     seqs, Ks, Vs, Qs = [], [], [], []
     for T, P in zip(q_lens, past_lens):
         st = SeqState()
@@ -244,8 +244,8 @@ def _attn_case(lib, H, KV, q_lens, past_lens, seed=0):
             m = min(64, n - pi * 64)
             kk[:, :m] = K[:, pi * 64: pi * 64 + m]
             vv[:, :m] = V[:, pi * 64: pi * 64 + m]
-            blocks[p, 0][:, K_IDX.reshape(-1)] = kk.reshape(KV, -1)
-            blocks[p, 1][:, V_IDX.reshape(-1)] = vv.reshape(KV, -1)
+            block(kv, KV, p, 0)[:, K_IDX.reshape(-1)] = kk.reshape(KV, -1)
+            block(kv, KV, p, 1)[:, V_IDX.reshape(-1)] = vv.reshape(KV, -1)
         seqs.append((st, T))
         Ks.append(K)
         Vs.append(V)

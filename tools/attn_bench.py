@@ -46,7 +46,8 @@ def main():
         st.length = P
         seqs.append((st, T))
     batch, keep = build_batch(seqs, dev)
-    kv = (torch.rand(B * pages_per * 2 * KV * 64 * 128, device=dev) * 2 - 1).to(torch.bfloat16)
+    pool_pages = (B * pages_per + 15) // 16 * 16  # whole KV super-pages (common.h KV_SUPER)
+    kv = (torch.rand(pool_pages * 2 * KV * 64 * 128, device=dev) * 2 - 1).to(torch.bfloat16)
     q = (torch.rand(B * T, H, 128, device=dev) * 4 - 2).to(torch.bfloat16)
     out = torch.empty(B * T, H * 128, dtype=torch.bfloat16, device=dev)
     ws_bytes = L.inferd_attention_workspace_bytes(B, H, n)

@@ -50,8 +50,46 @@ __global__ __launch_bounds__(NW * 64) void stream_kv_kernel(const u16* __restric
       const int u = u0 + d * NW;
       if (u >= n_items) break;
       const int phys = bt[p0 + (u >> 1)];
-      const u16* kb = kv + ((int64_t)(phys * 2 + 0) * KV + g) * KV_BLOCK_ELEMS + (u & 1) * (KV_BLOCK_ELEMS / 2);
-      const u16* vb = kv + ((int64_t)(phys * 2 + 1) * KV + g) * KV_BLOCK_ELEMS + (u & 1) * (KV_BLOCK_ELEMS / 2);
+      const u16* kb = kv + kv_block(phys, 0, g, KV) + (u & 1) * (KV_BLOCK_ELEMS / 2);
+      const u16* vb = kv + kv_block(phys, 1, g, KV) + (u & 1) * (KV_BLOCK_ELEMS / 2);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[d][i] = *(const bf16x8*)(kb + i * 512 + lane * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[d][8 + i] = *(const bf16x8*)(vb + i * 512 + lane * 8);
+    }
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+        const u32x4_t w = __builtin_bit_cast(u32x4_t, r[d][i]);
+        x ^= w[0] ^ w[1] ^ w[2] ^ w[3];
+      }
+  }
+  if (x == 0x12345u) sink[0] = x;
+}
+
+// Control 1b: the same work split (grid (nc, KV, B), 32-token items over NW waves) but
+// every workgroup's pages contiguous in memory (a head-major KV layout): what the page
+// layout costs the decode read.
+template <int NW, int DEPTH>
+__global__ __launch_bounds__(NW * 64) void stream_contig_kernel(const u16* __restrict__ kv, int np, int nc,
+                                                                unsigned* __restrict__ sink) {
+  const int c = blockIdx.x, g = blockIdx.y, s = blockIdx.z;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int p0 = c * np / nc, p1 = (c + 1) * np / nc;
+  // region of (s, g): np pages x (K 16 KiB + V 16 KiB), contiguous
+  const u16* base = kv + ((int64_t)(s * gridDim.y + g) * np) * 2 * KV_BLOCK_ELEMS;
+  unsigned x = 0;
+  const int n_items = 2 * (p1 - p0);
+  for (int u0 = wave; u0 < n_items; u0 += NW * DEPTH) {
+    bf16x8 r[DEPTH][16];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const int u = u0 + d * NW;
+      if (u >= n_items) break;
+      const u16* kb = base + (int64_t)(p0 + (u >> 1)) * 2 * KV_BLOCK_ELEMS + (u & 1) * (KV_BLOCK_ELEMS / 2);
+      const u16* vb = kb + KV_BLOCK_ELEMS;
 #pragma unroll
       for (int i = 0; i < 8; ++i) r[d][i] = *(const bf16x8*)(kb + i * 512 + lane * 8);
 #pragma unroll
@@ -94,7 +132,7 @@ int main(int argc, char** argv) {
   const int ctx = argc > 2 ? atoi(argv[2]) : 2100;
   const int H = 32, KV = 8;
   const int np = (ctx + 63) / 64;
-  const size_t pool_elems = (size_t)B * np * 2 * KV * KV_BLOCK_ELEMS;
+  const size_t pool_elems = (size_t)((B * np + KV_SUPER - 1) / KV_SUPER * KV_SUPER) * 2 * KV * KV_BLOCK_ELEMS;
   const size_t pool_bytes = pool_elems * 2;
   const int R = (int)((1536ull << 20) / pool_bytes) + 1;
   std::vector<u16*> pools(R);
@@ -214,6 +252,12 @@ int main(int argc, char** argv) {
   });
   control("flat read 4096 WG x4", [&](u16* kvp) {
     hipLaunchKernelGGL((flat_read_kernel<4>), dim3(4096), dim3(256), 0, 0, (const bf16x8*)kvp, nvec, sink);
+  });
+  control("contig nw8 nc2 depth2", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_contig_kernel<8, 2>), dim3(2, KV, B), dim3(512), 0, 0, kvp, np, 2, sink);
+  });
+  control("contig nw8 nc4 depth2", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_contig_kernel<8, 2>), dim3(4, KV, B), dim3(512), 0, 0, kvp, np, 4, sink);
   });
   control("stream nw8 nc2 depth2", [&](u16* kvp) {
     hipLaunchKernelGGL((stream_kv_kernel<8, 2>), dim3(2, KV, B), dim3(512), 0, 0, kvp, ab, KV, 2, sink);
