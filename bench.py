@@ -6,8 +6,10 @@ Workload (BASELINE.json configs[2], the metric's config): Qwen3-8B, batch 16 dec
 microbatch of 16 sequences through all 36 layers + final norm + lm_head + greedy argmax.
 
   N = 1 : the whole model is one span on one GPU.
-  N > 1 : the 36 layers are split into N even spans, one per GPU/rank ([5,5,5,5,4,4,4,4]
-          at N = 8); N microbatches of 16 sequences are in flight; hidden states move
+  N > 1 : the 36 layers are split into N spans, one per GPU/rank, balanced by each stage's
+          algorithmic decode bytes (the last stage also streams the 1.24 GB lm_head, ~2.4
+          layers' worth): [19,17], [9,10,10,7], [4,5,5,5,5,5,5,2] at N = 2/4/8 (`--split even`
+          gives [18,18] ... [5,5,5,5,4,4,4,4]); N microbatches of 16 sequences are in flight; hidden states move
           stage -> stage with RCCL send/recv over xGMI, greedy ids return last -> first.
           Per-GPU work is fixed as N grows ("scaling": "weak").
 
@@ -35,6 +37,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+from inferd_amd.pipeline import balanced_split, even_split  # noqa: E402  (host logic only, no GPU)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFLOPS = 2500.0
@@ -56,7 +59,10 @@ def parse():
     p.add_argument("--profile-steps", type=int, default=8, help="eager event-instrumented decode steps")
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
     p.add_argument("--spans", default="", help="comma-separated layers per stage (BASELINE config 4: an uneven, "
-                                                "balance.py-like split, e.g. 5,27,4); default: even split")
+                                                "balance.py-like split, e.g. 5,27,4); overrides --split")
+    p.add_argument("--split", choices=("balanced", "even"), default="balanced",
+                   help="stage layer counts: balanced = min-max of per-stage decode bytes (lm_head priced "
+                        "on the last stage), even = counts differing by at most one")
     p.add_argument("--mode", choices=("decode", "prefill"), default="decode",
                    help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline)")
     p.add_argument("--prefill-layers", type=int, default=8)
@@ -114,11 +120,15 @@ def run_prefill(args):
         "kernels": kernels}), flush=True)
 
 
-def even_split(n_layers: int, n: int):
-    base, extra = divmod(n_layers, n)
-    sizes = [base + (1 if i < extra else 0) for i in range(n)]
-    starts = [sum(sizes[:i]) for i in range(n)]
-    return list(zip(starts, sizes))
+def stage_split(d, n: int, B: int, ctx: int, how: str = "balanced"):
+    """Layer ranges per stage.  "balanced" (default): inferd_amd.pipeline.balanced_split with
+    each stage priced by its algorithmic decode bytes (HBM-bound), so the last stage, which
+    also streams the 1.24 GB lm_head, gets fewer layers; "even": layer counts differing by
+    at most one."""
+    if how == "even":
+        return even_split(d.layers, n)
+    kb = kernel_bytes(d, B, ctx)
+    return balanced_split(d.layers, n, step_bytes(d, 1, B, ctx, False), kb["lm_head_argmax"])
 
 
 # ------------------------------------------------------------------ algorithmic traffic
@@ -220,7 +230,7 @@ def main():
         assert len(sizes) == world and sum(sizes) == d.layers, f"--spans {args.spans}: need {world} stages, {d.layers} layers"
         spans = [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
     else:
-        spans = even_split(d.layers, world)
+        spans = stage_split(d, world, B, ctx, args.split)
     first, n_layers = spans[rank]
     n_mb = world                                   # microbatches in flight
     st = P.PipelineStage(d, rank, world, first, n_layers, device=dev, seed=args.seed,

@@ -31,6 +31,48 @@ import torch
 from .runtime import KV_PAGE, DecodeGraph, ModelDims, SeqState, SpanRuntime, build_batch
 
 
+def even_split(n_layers: int, n: int):
+    """[(first layer, layer count)] per stage, counts differing by at most one."""
+    base, extra = divmod(n_layers, n)
+    sizes = [base + (1 if i < extra else 0) for i in range(n)]
+    return [(sum(sizes[:i]), k) for i, k in enumerate(sizes)]
+
+
+def balanced_split(n_layers: int, n: int, layer_cost: float, head_cost: float = 0.0, embed_cost: float = 0.0):
+    """[(first layer, layer count)] per stage minimising the slowest stage's cost, where a
+    stage costs layer_cost per layer plus embed_cost on stage 0 and head_cost (final norm +
+    lm_head + argmax) on the last stage; ties go to the split with the smallest sum of
+    squared stage costs.  Every stage keeps at least one layer.
+
+    A lockstep pipeline ticks at its slowest stage, so the even split that split_model.py's
+    hand-written layer ranges would give (split_model.py:92-108, inferd.yaml) leaves every
+    other stage idle for the lm_head's share of the last stage: at Qwen3-8B decode the
+    lm_head reads V*h*2 = 1.24 GB, about 2.4 layers' worth of weights + KV."""
+    assert 1 <= n <= n_layers
+    INF = (float("inf"), float("inf"))
+    # best[s][l]: (max cost, sum of squares) of stages 0..s-1 covering layers 0..l-1
+    best = [[INF] * (n_layers + 1) for _ in range(n + 1)]
+    cut = [[0] * (n_layers + 1) for _ in range(n + 1)]
+    best[0][0] = (0.0, 0.0)
+    for s in range(1, n + 1):
+        for l in range(s, n_layers - (n - s) + 1):
+            for j in range(s - 1, l):
+                mx, sq = best[s - 1][j]
+                if mx == float("inf"):
+                    continue
+                c = (l - j) * layer_cost + (embed_cost if s == 1 else 0.0) + (head_cost if s == n else 0.0)
+                cand = (max(mx, c), sq + c * c)
+                if cand < best[s][l]:
+                    best[s][l], cut[s][l] = cand, j
+    sizes, l = [], n_layers
+    for s in range(n, 0, -1):
+        j = cut[s][l]
+        sizes.append(l - j)
+        l = j
+    sizes.reverse()
+    return [(sum(sizes[:i]), k) for i, k in enumerate(sizes)]
+
+
 class SpanExecutor:
     """Runs one span's compute for pipeline items on this rank's GPU."""
 

@@ -137,3 +137,40 @@ def test_weightgen_numpy_known_values():
     assert int(z[0]) == 0xE220A8397B1DCDAF
     v = wg.uniform_fp32(1234, 7, 5, 1.0)
     assert v.dtype == np.float32 and np.all(np.abs(v) <= 1.0)
+
+
+def _brute_split(n_layers, n, lc, hc):
+    """All compositions of n_layers into n positive parts; (max, sum sq) optimum."""
+    import itertools
+    best = None
+    for cuts in itertools.combinations(range(1, n_layers), n - 1):
+        b = (0,) + cuts + (n_layers,)
+        sizes = [b[i + 1] - b[i] for i in range(n)]
+        costs = [k * lc + (hc if i == n - 1 else 0.0) for i, k in enumerate(sizes)]
+        key = (max(costs), sum(c * c for c in costs))
+        if best is None or key < best[0]:
+            best = (key, sizes)
+    return best
+
+
+@pytest.mark.parametrize("n_layers,n,hc", [(12, 3, 2.4), (12, 4, 0.0), (10, 2, 5.0), (9, 9, 1.0), (13, 5, 3.3)])
+def test_balanced_split_is_min_max(n_layers, n, hc):
+    from inferd_amd.pipeline import balanced_split
+    spans = balanced_split(n_layers, n, 1.0, hc)
+    sizes = [k for _, k in spans]
+    assert sum(sizes) == n_layers and min(sizes) >= 1
+    assert [f for f, _ in spans] == [sum(sizes[:i]) for i in range(n)]
+    costs = [k + (hc if i == n - 1 else 0.0) for i, k in enumerate(sizes)]
+    (bmax, bsq), _ = _brute_split(n_layers, n, 1.0, hc)
+    assert max(costs) == pytest.approx(bmax) and sum(c * c for c in costs) == pytest.approx(bsq)
+
+
+def test_bench_stage_split_qwen3_8b():
+    """bench.py's default stage split at the headline config prices the lm_head on the last
+    stage: its slowest stage is 5 layers at N = 8 where the even split's is 4 layers + lm_head."""
+    import bench
+    from inferd_amd.runtime import MODELS
+    d = MODELS["qwen3-8b"]
+    assert [k for _, k in bench.stage_split(d, 8, 16, 2048)] == [4, 5, 5, 5, 5, 5, 5, 2]
+    assert [k for _, k in bench.stage_split(d, 8, 16, 2048, "even")] == [5, 5, 5, 5, 4, 4, 4, 4]
+    assert [k for _, k in bench.stage_split(d, 1, 16, 2048)] == [36]
