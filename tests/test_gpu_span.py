@@ -351,3 +351,45 @@ def test_prefill_qkv_epilogue_matches_separate(monkeypatch):
     # row per prompt on the box); the extension and decode rows read the cache both wrote
     assert n_rows <= 0.005 * 932, n_rows
     assert e < 1e-2
+
+
+def test_config3_q8b_layer_b16_ctx2048_decode_graph():
+    """BASELINE config 3 at its full size, on the exact bench path: one Qwen3-8B layer,
+    16 sequences prefilled with 2048 tokens each (two sequences per call, as bench.py does),
+    then 3 decode steps as replays of the captured decode graph (split-K q/k/v GEMV, fused
+    norm/RoPE/cache-write attention over 2k of paged context, o/gate-up/down GEMVs), each
+    compared per sequence with the oracle's cached forward (bf16, SDPA) on the same inputs."""
+    from inferd_amd.runtime import DecodeGraph
+    d = R.CONFIGS["qwen3-8b"]
+    B, T, steps, layer = 16, 2048, 3, 5
+    s = span("qwen3-8b", layer, 1, False, False, kv_pages=B * (T // 64 + 2) + 4, max_tokens=2 * T,
+             max_seqs=B, max_positions=T + 64)
+    oracle = R.RefSpan(d, SEED, layer, layer, False, False, torch.bfloat16, "sdpa")
+    gen = torch.Generator().manual_seed(77)
+    x = (torch.randn(B, T, d.hidden, generator=gen) * 0.5).to(torch.bfloat16)
+    sess = [f"c3_{b}" for b in range(B)]
+    worst = 0.0
+    for b0 in range(0, B, 2):
+        out = s.forward([(sid, T) for sid in sess[b0:b0 + 2]], x=x[b0:b0 + 2].reshape(2 * T, -1).to(DEV))["hidden"]
+        for j in range(2):
+            ref = oracle.forward_cached(sess[b0 + j], x[b0 + j:b0 + j + 1])[0]
+            e = rel_err(out[j * T:(j + 1) * T], ref)
+            worst = max(worst, e)
+            assert e < TOL_REL, (b0 + j, e)
+    print(f"prefill B={B} T={T}: worst rel err {worst:.2e}")
+    xin = torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV)
+    hout = torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV)
+    g = DecodeGraph(s, sess, steps, x=xin, hidden_out=hout)
+    for k in range(steps):
+        xs = (torch.randn(B, d.hidden, generator=gen) * 0.5).to(torch.bfloat16)
+        xin.copy_(xs.to(DEV))
+        g.launch()
+        torch.cuda.synchronize()
+        got = hout.cpu()
+        worst = 0.0
+        for b in range(B):
+            ref = oracle.forward_cached(sess[b], xs[b].reshape(1, 1, -1))[0, 0]
+            e = rel_err(got[b], ref)
+            worst = max(worst, e)
+            assert e < TOL_REL, (k, b, e)
+        print(f"decode step {k} (ctx {T + k + 1}): worst rel err {worst:.2e}")
