@@ -16,6 +16,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -82,22 +83,28 @@ def build_batch(seqs, device):
     B = len(seqs)
     M = sum(n for _, n in seqs)
     max_pages = max(1, max(len(st.pages) for st, _ in seqs))
-    seq_start, positions, slots, ctx = [0], [], [], []
-    for st, n in seqs:
-        for i in range(n):
-            p = st.length + i
-            positions.append(p)
-            slots.append(st.pages[p // KV_PAGE] * KV_PAGE + p % KV_PAGE)
-        seq_start.append(seq_start[-1] + n)
-        ctx.append(st.length + n)
-    table = []
-    for st, _ in seqs:
-        table.extend(st.pages + [0] * (max_pages - len(st.pages)))
-    host = torch.tensor(seq_start + positions + slots + ctx + table, dtype=torch.int32)
-    dev = host.to(device)
+    # one int32 host array [seq_start | positions | slots | ctx_lens | block_table], filled
+    # with vectorised numpy (a prefill of 8k tokens is 8k positions and slots)
+    host = np.zeros(B + 1 + 2 * M + B + B * max_pages, dtype=np.int32)
+    lens = np.array([n for _, n in seqs], dtype=np.int64)
+    host[1:B + 1] = np.cumsum(lens)
+    pos_v = host[B + 1:B + 1 + M]
+    slot_v = host[B + 1 + M:B + 1 + 2 * M]
+    ctx_v = host[B + 1 + 2 * M:B + 1 + 2 * M + B]
+    tab_v = host[B + 1 + 2 * M + B:].reshape(B, max_pages)
+    o = 0
+    for i, (st, n) in enumerate(seqs):
+        pages = np.asarray(st.pages, dtype=np.int64)
+        p = np.arange(st.length, st.length + n, dtype=np.int64)
+        pos_v[o:o + n] = p
+        slot_v[o:o + n] = pages[p // KV_PAGE] * KV_PAGE + p % KV_PAGE
+        ctx_v[i] = st.length + n
+        tab_v[i, :len(st.pages)] = pages
+        o += n
+    dev = torch.from_numpy(host).to(device)
     o = [0, B + 1, B + 1 + M, B + 1 + 2 * M, B + 1 + 2 * M + B]
     base = dev.data_ptr()
-    b = _lib.Batch(n_seqs=B, n_tokens=M, max_q_len=max(n for _, n in seqs), max_ctx_len=max(ctx),
+    b = _lib.Batch(n_seqs=B, n_tokens=M, max_q_len=int(lens.max()), max_ctx_len=int(ctx_v.max()),
                    max_pages=max_pages, decode=int(all(n == 1 for _, n in seqs)),
                    seq_start=base + 4 * o[0], positions=base + 4 * o[1], slots=base + 4 * o[2],
                    ctx_lens=base + 4 * o[3], block_table=base + 4 * o[4])
