@@ -37,7 +37,7 @@ struct DecodeArgs {
   int64_t ldc;
   const u16* R;
   int64_t ldr;
-  unsigned long long* keys;  // EPI_ARGMAX partial keys [n_tiles][M]
+  unsigned long long* keys;  // EPI_ARGMAX partial keys [M][n_tiles]
   float eps;                 // NORM: RMSNorm epsilon
   // EPI_PARTIAL (K split over gridDim.y slices, reduced by the consumer): slice y covers
   // k-tiles [y * KT / gridDim.y, (y + 1) * KT / gridDim.y); it writes its fp32 accumulator
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
         key = other > key ? other : key;
       }
       if (row < M) {
-        if ((ln & 15) == 0) g.keys[(int64_t)nt * M + row] = key;
+        if ((ln & 15) == 0) g.keys[(int64_t)row * g.n_tiles + nt] = key;  // [M][n_tiles]
         if (g.C) g.C[(int64_t)row * g.ldc + col] = f2bf(lv);
       }
     } else if (row < M) {
@@ -1814,15 +1814,22 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
   }
 }
 
-// per-row max over n_tiles partial keys -> token id (lowest index among equal maxima)
-__global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long long* __restrict__ partial,
-                                                            int n_tiles, int M, int32_t* __restrict__ ids) {
-  __shared__ unsigned long long red[4];
+// Greedy id per row from the lm_head GEMV's per-tile keys (layout [M][n_tiles], so a
+// row's keys are contiguous): one 1024-thread workgroup per row, four independent
+// coalesced loads in flight per thread, max over (value key << 32 | ~col) = the first
+// maximal column, as torch.argmax.
+__global__ __launch_bounds__(1024) void argmax_reduce_kernel(const unsigned long long* __restrict__ partial,
+                                                             int n_tiles, int32_t* __restrict__ ids) {
+  __shared__ unsigned long long red[16];
   const int row = blockIdx.x;
+  const unsigned long long* p = partial + (int64_t)row * n_tiles;
   unsigned long long best = 0;
-  for (int t = threadIdx.x; t < n_tiles; t += 256) {
-    unsigned long long k = partial[(int64_t)t * M + row];
-    best = k > best ? k : best;
+  for (int t = threadIdx.x; t < n_tiles; t += 4 * 1024) {
+    unsigned long long k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = (t + u * 1024 < n_tiles) ? p[t + u * 1024] : 0ull;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) best = k[u] > best ? k[u] : best;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1833,14 +1840,14 @@ __global__ __launch_bounds__(256) void argmax_reduce_kernel(const unsigned long 
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long b = red[0];
-    for (int w = 1; w < 4; ++w) b = red[w] > b ? red[w] : b;
+    for (int w = 1; w < 16; ++w) b = red[w] > b ? red[w] : b;
     ids[row] = (int32_t)(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull));
   }
 }
 
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M, int32_t* ids,
                           hipStream_t s) {
-  hipLaunchKernelGGL(argmax_reduce_kernel, dim3(M), dim3(256), 0, s, partial, n_tiles, M, ids);
+  hipLaunchKernelGGL(argmax_reduce_kernel, dim3(M), dim3(1024), 0, s, partial, n_tiles, ids);
 }
 
 // ============================================================ fused prefill q/k/v projection
