@@ -108,6 +108,16 @@ def run_prefill(args):
     prof = span.profile_stop()
     kernels = {k: {"launches": n, "avg_ms": round(ms / max(n, 1), 3)} for k, (ms, n) in prof.items() if n}
     tf = fl / t / 1e12
+    # PMC-measured L2-to-fabric bytes per launch of the dominant kernel class
+    # (tools/pmc_prefill.sh -> profiles/traffic_prefill_r01.json; MALL hits are counted too)
+    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_prefill_r01.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tr = json.load(f)
+        if tr.get("workload") == f"{d.name}-prefill-{L}layers-T{T}" and B == 1:
+            traffic = tr["per_launch_bytes"].get(dom)
     print(json.dumps({
         "metric": "prefill tokens/sec, Qwen3-32B 8-layer span (one of 8 pipeline stages)",
         "value": round(B * T / t, 1), "unit": "tokens/s", "n_gpus": 1, "steps": args.steps,
@@ -117,7 +127,8 @@ def run_prefill(args):
         "config": {"workload": f"qwen3-32b layers 8-{8 + L - 1}, prefill {B} x {T} tokens",
                    "global_batch": B, "seq_len": T, "parallelism": "pp-stage"},
         "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_kernel": dom,
                      "alg_flops_per_step": fl},
         "kernels": kernels}), flush=True)
 
