@@ -28,7 +28,7 @@ from __future__ import annotations
 
 import torch
 
-from .runtime import KV_PAGE, DecodeGraph, ModelDims, SeqState, SpanRuntime, build_batch
+from .runtime import KV_PAGE, DecodeGraph, ModelDims, SpanRuntime, build_batch
 
 
 def even_split(n_layers: int, n: int):
