@@ -217,16 +217,25 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
   }
 }
 
-template <int NW, bool FUSED>
-__global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restrict__ q, u16* __restrict__ kv,
-                                                      AttnBatch b, int H, int KV, int nc_req, float scale_log2,
-                                                      int n_chunks_max, unsigned* __restrict__ counters,
-                                                      float* __restrict__ part, u16* __restrict__ out,
-                                                      DecodeFuse fz) {
+template <bool WT>
+__device__ __forceinline__ void out_store(u16* p, u16 v) {
+  if constexpr (WT)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
+// WT: output stores write-through (agent-scope relaxed atomic stores, sc1), for the one-grid
+// attention + o_proj kernel whose o workgroups read them in the same launch.
+template <int NW, bool FUSED, bool WT = false>
+__device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16* __restrict__ kv, const AttnBatch& b,
+                                                 int H, int KV, int nc_req, float scale_log2, int n_chunks_max,
+                                                 unsigned* __restrict__ counters, float* __restrict__ part,
+                                                 u16* __restrict__ out, const DecodeFuse& fz, const int chunk,
+                                                 const int g, const int bseq) {
   __shared__ float sm_m[NW][16], sm_l[NW][16];
   __shared__ float sm_o[NW][16][HEAD_DIM + 4];
   __shared__ int sm_last;
-  const int chunk = blockIdx.x, g = blockIdx.y, bseq = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_rep = H / KV;
   const int ctx = b.ctx_lens[bseq];
@@ -388,7 +397,7 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
       L += sm_l[w][n] * f;
     }
     if (nc == 1) {
-      op[n * HEAD_DIM + d] = f2bf(acc / L);
+      out_store<WT>(op + n * HEAD_DIM + d, f2bf(acc / L));
     } else {
       float* pc = base + (int64_t)chunk * stride + n * PART_STRIDE;
       __hip_atomic_store(pc + d, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -428,8 +437,133 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
       L += __hip_atomic_load(pc + HEAD_DIM + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
       acc += __hip_atomic_load(pc + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
     }
-    op[n * HEAD_DIM + d] = f2bf(acc / L);
+    out_store<WT>(op + n * HEAD_DIM + d, f2bf(acc / L));
   }
+}
+
+template <int NW, bool FUSED>
+__global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restrict__ q, u16* __restrict__ kv,
+                                                      AttnBatch b, int H, int KV, int nc_req, float scale_log2,
+                                                      int n_chunks_max, unsigned* __restrict__ counters,
+                                                      float* __restrict__ part, u16* __restrict__ out,
+                                                      DecodeFuse fz) {
+  attn_decode_body<NW, FUSED>(q, kv, b, H, KV, nc_req, scale_log2, n_chunks_max, counters, part, out, fz,
+                              blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// ---------------------------------------------------------------- attention + o_proj, one grid
+// Decode attention (8 waves, fused q/k/v epilogue) and the o projection (+ residual) of the
+// same layer in ONE launch: workgroups [0, n_att) are the attention's (chunk, g, b) grid in
+// its own linear order; workgroups [n_att, n_att + N/16) are o-projection column tiles.
+// Workgroups dispatch in index order, so every attention workgroup is placed before any o
+// workgroup and none of them waits on an o workgroup.  An o workgroup streams its whole
+// 16-column weight tile (K/32/8 tiles per wave) into registers first, then waits for the
+// attention's done counter (each attention workgroup: write-through output stores,
+// vmcnt(0), barrier, one relaxed add), then thread 0 does one agent acquire and the
+// workgroup reads the attention-output fragments.  Same tile-to-wave assignment and
+// summation order as gemm_decode_kernel
+// <1, 1, 8, 4, 3, EPI_RESID> (wave w: batches w, w+8, ... of 4 k-tiles), so the result is
+// bit-identical to the separate o launch.  The poll is bounded: on expiry the workgroup
+// raises chain[2] and exits (wrong output, never a hang).
+// chain: [0] attention workgroups done, [1] o workgroups past the wait, [2] error flag;
+// the last o workgroup past the wait resets [0] and [1] for the next launch.
+struct OProj {
+  const u16* Wp;  // fragment-packed [N/16][K/32] tiles
+  int K;
+  u16* C;         // [M][N] = R + attn @ W^T
+  const u16* R;
+  int64_t ldc;
+  int n_tiles;
+};
+
+template <int TPW>
+__global__ __launch_bounds__(512) void attn_o_decode_kernel(u16* __restrict__ kv, AttnBatch b, int H, int KV, int nc,
+                                                             float scale_log2, unsigned* __restrict__ counters,
+                                                             float* __restrict__ part, u16* __restrict__ out,
+                                                             DecodeFuse fz, OProj op, unsigned* __restrict__ chain) {
+  const int n_att = nc * KV * b.B;
+  const int idx = blockIdx.x;
+  if (idx < n_att) {
+    attn_decode_body<8, true, true>(nullptr, kv, b, H, KV, nc, scale_log2, nc, counters, part, out, fz, idx % nc,
+                                    (idx / nc) % KV, idx / (nc * KV));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // write-through output stores landed
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&chain[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  __shared__ f32x4 red[8][64];
+  __shared__ int sm_ok;
+  const int nt = idx - n_att;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int KT = op.K / 32;
+  const int lda = H * HEAD_DIM;
+  const bf16x8* wb = (const bf16x8*)(op.Wp + (int64_t)nt * KT * 512) + lane;
+  bf16x8 wv[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW / 4; ++j)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wv[4 * j + u] = __builtin_nontemporal_load(wb + (4 * (wave + 8 * j) + u) * 64);
+  if (threadIdx.x == 0) {
+    int budget = 1 << 22;
+    while (__hip_atomic_load(&chain[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)n_att && --budget > 0)
+      __builtin_amdgcn_s_sleep(1);
+    sm_ok = budget > 0;
+    const unsigned prev = __hip_atomic_fetch_add(&chain[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)op.n_tiles - 1) {
+      __hip_atomic_store(&chain[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&chain[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!sm_ok) __hip_atomic_store(&chain[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1 (one invalidate per workgroup)
+  }
+  __syncthreads();
+  if (!sm_ok) return;
+  const int M = b.M;
+  int row = lane & 15;
+  row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
+  const u16* a = out + (int64_t)row * lda + 8 * (lane >> 4);
+  bf16x8 av[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW / 4; ++j)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) av[4 * j + u] = *(const bf16x8*)(a + (4 * (wave + 8 * j) + u) * 32);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) acc = mfma16(av[i], wv[i], acc);
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int ln = threadIdx.x;
+  f32x4 v = red[0][ln];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) v += red[w][ln];
+  const int col = nt * 16 + (ln & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = 4 * (ln >> 4) + r;
+    if (rr < M) op.C[(int64_t)rr * op.ldc + col] = f2bf(rbf(v[r]) + bf2f(op.R[(int64_t)rr * op.ldc + col]));
+  }
+}
+
+static void decode_shape(int B, int KV, int max_ctx, int* nw, int* nc);
+
+// Returns false (nothing launched) when the shapes are outside the one-grid kernel's scope.
+bool launch_attn_o_decode_fused(const u16* qn_w, const u16* kn_w, const u16* cos_t, const u16* sin_t, float eps,
+                                u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out, float* ws,
+                                const float* part, const float* ssq, int ksl, int K, int64_t ldqkv, const u16* Wo,
+                                int N, u16* C, const u16* R, unsigned* chain, hipStream_t s) {
+  int nw, nc;
+  decode_shape(b.B, KV, b.max_ctx, &nw, &nc);
+  const int Ko = H * HEAD_DIM;
+  if (nw != 8 || b.M > 16 || Ko != 4096 || N % 16 != 0) return false;  // TPW = 4096 / 32 / 8 = 16
+  const DecodeFuse fz = {nullptr, ldqkv, qn_w, kn_w, cos_t, sin_t, eps, part, ssq, ksl, K};
+  unsigned* counters = (unsigned*)ws;
+  float* pw = (float*)((char*)ws + DECODE_COUNTER_BYTES);
+  const OProj op = {Wo, Ko, C, R, (int64_t)N, N / 16};
+  const int n_att = nc * KV * b.B;
+  hipLaunchKernelGGL((attn_o_decode_kernel<16>), dim3(n_att + N / 16), dim3(512), 0, s, kv_layer, b, H, KV, nc,
+                     scale * LOG2E, counters, pw, out, fz, op, chain);
+  return true;
 }
 
 static int env_int(const char* name) {

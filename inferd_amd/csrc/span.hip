@@ -95,6 +95,7 @@ struct InferdSpan {
       *last = nullptr;
   float* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
+  unsigned* chain = nullptr;  // attn_o_decode_kernel counters (3 u32, zero between launches)
   float* rs_ws = nullptr;  // folded-norm row scales of the prefill GEMMs [max_tokens]
   float* qkv_part = nullptr;  // decode split-K q/k/v partials [QKV_KSL_MAX][16][qkv_rows]
   float* qkv_ssq = nullptr;   // and their row sums of squares [QKV_KSL_MAX][16]
@@ -217,6 +218,8 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
+  SALLOC(s->chain, 64);
+  if (hipMemset(s->chain, 0, 64) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
   SALLOC(s->rs_ws, (size_t)c.max_tokens * 4);
   SALLOC(s->qkv_part, (size_t)QKV_KSL_MAX * 16 * s->qkv_rows() * 4);
@@ -377,6 +380,12 @@ static bool fuse_prefill_rope() {
   return e && *e == '1';
 }
 
+// INFERD_FUSE_ATTN_O=1: decode attention and o_proj in one grid (attn_o_decode_kernel)
+static bool fuse_attn_o() {
+  const char* e = getenv("INFERD_FUSE_ATTN_O");
+  return e && *e == '1';
+}
+
 static bool fuse_decode_rope() {
   const char* e = getenv("INFERD_FUSE_DECODE_ROPE");
   return !(e && *e == '0');
@@ -444,9 +453,15 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       if (!qkv_done) launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &rn);
     }
     s->prof_end(pe, st);
+    bool o_done = false;
     if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
-      if (ksl > 1)
+      if (ksl > 1 && fuse_attn_o())
+        o_done = launch_attn_o_decode_fused(W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV, scale,
+                                            s->attn, s->attn_ws, s->qkv_part, s->qkv_ssq, ksl, h, qkvN, W.o, h,
+                                            s->h, x, s->chain, st);
+      if (o_done) {
+      } else if (ksl > 1)
         launch_attn_decode_fused(nullptr, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
                                  scale, s->attn, s->attn_ws, st, s->qkv_part, s->qkv_ssq, ksl, h);
       else
@@ -474,9 +489,11 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       s->prof_end(pe, st);
     }
     // h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
-    pe = s->prof_begin(PROF_O, st);
-    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);
-    s->prof_end(pe, st);
+    if (!o_done) {
+      pe = s->prof_begin(PROF_O, st);
+      launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);
+      s->prof_end(pe, st);
+    }
     pe = s->prof_begin(PROF_GATEUP, st);
     launch_gemm(s->h, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, &rn);
     s->prof_end(pe, st);
