@@ -545,13 +545,111 @@ __global__ __launch_bounds__(512) void attn_o_decode_kernel(u16* __restrict__ kv
   }
 }
 
+// Persistent variant (INFERD_FUSE_ATTN_O=2): grid = n_att = N/16 workgroups, one per CU,
+// all resident (the launcher checks the CU count).  Workgroup i first DMAs the first half
+// of o tile i's weights (its waves' batches j < TPW/8, 64 KB) into LDS, so they land while
+// the attention streams the KV cache; then runs attention item i, publishes (write-through
+// output, vmcnt(0), barrier, one add), issues the second half of the weights into
+// registers, waits for all n_att, one acquire, and computes o tile i in the same order as
+// above (bit-identical).
+template <int TPW>
+__global__ __launch_bounds__(512, 1) void attn_o_persist_kernel(u16* __restrict__ kv, AttnBatch b, int H, int KV,
+                                                                int nc, float scale_log2,
+                                                                unsigned* __restrict__ counters,
+                                                                float* __restrict__ part, u16* __restrict__ out,
+                                                                DecodeFuse fz, OProj op, unsigned* __restrict__ chain) {
+  constexpr int HALF = TPW / 2;  // tiles per wave staged in LDS
+  __shared__ __attribute__((aligned(16))) char wlds[8 * HALF * 1024];
+  __shared__ f32x4 red[8][64];
+  __shared__ int sm_ok;
+  const int n_att = nc * KV * b.B;
+  const int idx = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int KT = op.K / 32;
+  const u16* wsrc = op.Wp + (int64_t)idx * KT * 512;
+#pragma unroll
+  for (int jj = 0; jj < HALF / 4; ++jj)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int kt = 4 * (wave + 8 * jj) + u;
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc + kt * 512 + lane * 8),
+                                       (void*)(wlds + (wave * HALF + jj * 4 + u) * 1024), 16, 0, 0);
+    }
+  attn_decode_body<8, true, true>(nullptr, kv, b, H, KV, nc, scale_log2, nc, counters, part, out, fz, idx % nc,
+                                  (idx / nc) % KV, idx / (nc * KV));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // write-through output stores and weight DMA landed
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&chain[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bf16x8* wb = (const bf16x8*)wsrc + lane;
+  bf16x8 wv[HALF];
+#pragma unroll
+  for (int jj = HALF / 4; jj < TPW / 4; ++jj)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      wv[(jj - HALF / 4) * 4 + u] = __builtin_nontemporal_load(wb + (4 * (wave + 8 * jj) + u) * 64);
+  if (threadIdx.x == 0) {
+    int budget = 1 << 22;
+    while (__hip_atomic_load(&chain[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)n_att && --budget > 0)
+      __builtin_amdgcn_s_sleep(2);
+    sm_ok = budget > 0;
+    const unsigned prev = __hip_atomic_fetch_add(&chain[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned)n_att - 1) {
+      __hip_atomic_store(&chain[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&chain[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!sm_ok) __hip_atomic_store(&chain[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!sm_ok) return;
+  const int M = b.M;
+  int row = lane & 15;
+  row = row < M ? row : M - 1;
+  const u16* a = out + (int64_t)row * (H * HEAD_DIM) + 8 * (lane >> 4);
+  bf16x8 av[TPW];
+#pragma unroll
+  for (int j = 0; j < TPW / 4; ++j)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) av[4 * j + u] = *(const bf16x8*)(a + (4 * (wave + 8 * j) + u) * 32);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < HALF; ++i)
+    acc = mfma16(av[i], *(const bf16x8*)(wlds + (wave * HALF + i) * 1024 + lane * 16), acc);
+#pragma unroll
+  for (int i = HALF; i < TPW; ++i) acc = mfma16(av[i], wv[i - HALF], acc);
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int ln = threadIdx.x;
+  f32x4 v = red[0][ln];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) v += red[w][ln];
+  const int col = idx * 16 + (ln & 15);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = 4 * (ln >> 4) + r;
+    if (rr < M) op.C[(int64_t)rr * op.ldc + col] = f2bf(rbf(v[r]) + bf2f(op.R[(int64_t)rr * op.ldc + col]));
+  }
+}
+
 static void decode_shape(int B, int KV, int max_ctx, int* nw, int* nc);
+
+static int device_cus() {
+  static int n = -1;
+  if (n < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 0;
+  }
+  return n;
+}
 
 // Returns false (nothing launched) when the shapes are outside the one-grid kernel's scope.
 bool launch_attn_o_decode_fused(const u16* qn_w, const u16* kn_w, const u16* cos_t, const u16* sin_t, float eps,
                                 u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out, float* ws,
                                 const float* part, const float* ssq, int ksl, int K, int64_t ldqkv, const u16* Wo,
-                                int N, u16* C, const u16* R, unsigned* chain, hipStream_t s) {
+                                int N, u16* C, const u16* R, unsigned* chain, hipStream_t s, int mode) {
   int nw, nc;
   decode_shape(b.B, KV, b.max_ctx, &nw, &nc);
   const int Ko = H * HEAD_DIM;
@@ -561,6 +659,13 @@ bool launch_attn_o_decode_fused(const u16* qn_w, const u16* kn_w, const u16* cos
   float* pw = (float*)((char*)ws + DECODE_COUNTER_BYTES);
   const OProj op = {Wo, Ko, C, R, (int64_t)N, N / 16};
   const int n_att = nc * KV * b.B;
+  if (mode == 2) {
+    // one workgroup per CU, every one resident: needs n_att == N/16 <= CUs
+    if (n_att != N / 16 || n_att > device_cus()) return false;
+    hipLaunchKernelGGL((attn_o_persist_kernel<16>), dim3(n_att), dim3(512), 0, s, kv_layer, b, H, KV, nc,
+                       scale * LOG2E, counters, pw, out, fz, op, chain);
+    return true;
+  }
   hipLaunchKernelGGL((attn_o_decode_kernel<16>), dim3(n_att + N / 16), dim3(512), 0, s, kv_layer, b, H, KV, nc,
                      scale * LOG2E, counters, pw, out, fz, op, chain);
   return true;

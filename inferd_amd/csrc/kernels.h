@@ -97,12 +97,13 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 // With `part` non-null the q/k/v come from launch_gemm_decode_partial's fp32 K-slices
 // (part [ksl][M][ldqkv], ssq [ksl][M], K = hidden) instead of the bf16 rows `qkv`.
 // Decode attention (fused q/k/v epilogue, split-K partials) and o_proj + residual in one
-// grid (attention.hip attn_o_decode_kernel); false = shape not covered, nothing launched.
+// grid (attention.hip attn_o_decode_kernel; mode 2: attn_o_persist_kernel, one workgroup per
+// CU doing attention item i then o tile i); false = shape not covered, nothing launched.
 // chain: 3 zeroed u32 (done counters + error flag), left zero after every launch.
 bool launch_attn_o_decode_fused(const u16* qn_w, const u16* kn_w, const u16* cos_t, const u16* sin_t, float eps,
                                 u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out, float* ws,
                                 const float* part, const float* ssq, int ksl, int K, int64_t ldqkv, const u16* Wo,
-                                int N, u16* C, const u16* R, unsigned* chain, hipStream_t s);
+                                int N, u16* C, const u16* R, unsigned* chain, hipStream_t s, int mode);
 void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
                               const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
                               float scale, u16* out, float* ws, hipStream_t s, const float* part = nullptr,

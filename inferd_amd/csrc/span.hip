@@ -380,10 +380,11 @@ static bool fuse_prefill_rope() {
   return e && *e == '1';
 }
 
-// INFERD_FUSE_ATTN_O=1: decode attention and o_proj in one grid (attn_o_decode_kernel)
-static bool fuse_attn_o() {
+// INFERD_FUSE_ATTN_O=1: decode attention and o_proj in one grid (attn_o_decode_kernel);
+// =2: the persistent one-workgroup-per-CU form (attn_o_persist_kernel); 0 / unset: two launches
+static int fuse_attn_o() {
   const char* e = getenv("INFERD_FUSE_ATTN_O");
-  return e && *e == '1';
+  return e && (*e == '1' || *e == '2') ? *e - '0' : 0;
 }
 
 static bool fuse_decode_rope() {
@@ -459,7 +460,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       if (ksl > 1 && fuse_attn_o())
         o_done = launch_attn_o_decode_fused(W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV, scale,
                                             s->attn, s->attn_ws, s->qkv_part, s->qkv_ssq, ksl, h, qkvN, W.o, h,
-                                            s->h, x, s->chain, st);
+                                            s->h, x, s->chain, st, fuse_attn_o());
       if (o_done) {
       } else if (ksl > 1)
         launch_attn_decode_fused(nullptr, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
