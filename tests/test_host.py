@@ -174,3 +174,32 @@ def test_bench_stage_split_qwen3_8b():
     assert [k for _, k in bench.stage_split(d, 8, 16, 2048)] == [4, 5, 5, 5, 5, 5, 5, 2]
     assert [k for _, k in bench.stage_split(d, 8, 16, 2048, "even")] == [5, 5, 5, 5, 4, 4, 4, 4]
     assert [k for _, k in bench.stage_split(d, 1, 16, 2048)] == [36]
+
+
+def test_build_batch_descriptor_layout():
+    """runtime.build_batch (numpy-vectorised) against a per-token restatement of the
+    descriptor: seq_start | positions | slots (page * 64 + offset) | ctx_lens | block table."""
+    import random
+    from inferd_amd.runtime import KV_PAGE, SeqState, build_batch
+    rng = random.Random(0)
+    for _ in range(100):
+        seqs = []
+        for _b in range(rng.randint(1, 6)):
+            st = SeqState()
+            st.length, n = rng.randint(0, 300), rng.randint(1, 200)
+            st.pages = rng.sample(range(1000), (st.length + n + KV_PAGE - 1) // KV_PAGE + rng.randint(0, 2))
+            seqs.append((st, n))
+        batch, dev = build_batch(seqs, "cpu")
+        max_pages = max(len(st.pages) for st, _ in seqs)
+        start, pos, slots, ctx, table = [0], [], [], [], []
+        for st, n in seqs:
+            for i in range(n):
+                p = st.length + i
+                pos.append(p)
+                slots.append(st.pages[p // KV_PAGE] * KV_PAGE + p % KV_PAGE)
+            start.append(start[-1] + n)
+            ctx.append(st.length + n)
+            table += st.pages + [0] * (max_pages - len(st.pages))
+        assert dev.tolist() == start + pos + slots + ctx + table
+        assert batch.n_tokens == sum(n for _, n in seqs) and batch.max_ctx_len == max(ctx)
+        assert batch.max_q_len == max(n for _, n in seqs) and batch.max_pages == max_pages
