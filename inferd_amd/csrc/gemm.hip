@@ -15,9 +15,10 @@
 //    non-temporal: each byte is read once per step).  The NW partial accumulators reduce
 //    through LDS; the epilogue (residual add / SwiGLU / argmax keys) is fused.  No split-K:
 //    measured on the box, every in-launch K split cost more than the balance it bought.
-//  * gemm_tiled / gemm_tiled256: M > 64 rows (prefill).  128x128 (4 waves) or 256x256
-//    (8 waves) block tiles, A and B staged through double-buffered LDS with
-//    global_load_lds (A XOR-swizzled on the source address, B already fragment-ordered).
+//  * gemm_w4p / gemm_w4: >= 512 rows (prefill).  256x256x64 block tiles on four waves,
+//    LDS-DMA staged (see their section); gemm_tiled: 65..511 rows and odd shapes, 128x128
+//    tiles, double-buffered LDS with global_load_lds (A XOR-swizzled on the source address,
+//    B already fragment-ordered).
 #include <stdlib.h>
 
 #include <utility>
@@ -28,6 +29,15 @@
 __device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g)); }
 
 // ============================================================ decode (M <= 64) kernel
+// RMSNorm modes of the decode GEMV (NORM template argument, kernels.h DN_*):
+//  DN_NONE  A used as is;
+//  DN_FOLD  folded norm (INFERD_NORM_FOLD=1, A/B only): the norm weight was folded into the
+//           packed W at pack time; rsqrt(mean(A^2) + eps) (sums of squares from the A
+//           fragments) multiplies the fp32 accumulator;
+//  DN_EXACT Qwen3RMSNorm at the reference rounding points (qwen3_server_module.py:19-25):
+//           A' = bf16(w * bf16(A * r)), r = 1 / sqrt(sum_p ssq_in[p][row] / K + eps) from the
+//           per-tile sums of squares the producer wrote (ssq_out below), applied to each A
+//           fragment before its MFMA.
 struct DecodeArgs {
   const u16* A;
   int64_t lda;
@@ -41,18 +51,31 @@ struct DecodeArgs {
   float eps;                 // NORM: RMSNorm epsilon
   // EPI_PARTIAL (K split over gridDim.y slices, reduced by the consumer): slice y covers
   // k-tiles [y * KT / gridDim.y, (y + 1) * KT / gridDim.y); it writes its fp32 accumulator
-  // to part[y][row][col] (row stride ldp) and, with NORM, its rows' sums of squares to
+  // to part[y][row][col] (row stride ldp) and, with DN_FOLD, its rows' sums of squares to
   // ssq[y][row] -- both unscaled.
   float* part;
   int64_t ldp;
   float* ssq;
+  // DN_EXACT: producer partial sums of squares ssq_in[p * 64 + row], p < n_parts, and the
+  // norm weight [K]
+  const float* ssq_in;
+  int n_parts;
+  const u16* norm_w;
+  // EPI_RESID producer side: ssq_out[tile * 64 + row] = sum over the tile's 16 columns of
+  // the stored bf16 outputs squared (the next DN_EXACT consumer's ssq_in), or null
+  float* ssq_out;
 };
 
-template <int MT, int S, int NW, int TW, int D, int EPI, bool NORM>
+#define DECODE_NORM_MAXK 8192  // DN_EXACT: K of one workgroup (hidden <= 8192)
+
+template <int MT, int S, int NW, int TW, int D, int EPI, int NORM>
 __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
-  __shared__ float sm_ss[NORM ? NW : 1][MT * 16];
+  __shared__ float sm_ss[NORM == DN_FOLD ? NW : 1][MT * 16];
+  __shared__ float sm_r[NORM == DN_EXACT ? NW * 64 : 1];
+  // DN_EXACT: this workgroup's K range of the norm weight, staged once (<= 8192 columns)
+  __shared__ __attribute__((aligned(16))) u16 sm_w[NORM == DN_EXACT ? DECODE_NORM_MAXK : 8];
   const int M = g.M;
   const int nt = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -73,7 +96,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[s][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ssq[MT];  // NORM: this lane's share of sum(x^2) of row mt*16 + (lane & 15)
+  float ssq[MT];  // DN_FOLD: this lane's share of sum(x^2) of row mt*16 + (lane & 15)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) ssq[mt] = 0.f;
 
@@ -93,10 +116,33 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
       for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
   };
   if (b < nb) {
-    // prologue: stages 0..D-2
+    // prologue: stages 0..D-2 (the weight bytes are in flight while the row scales reduce)
     [&]<int... I>(std::integer_sequence<int, I...>) {
       ((b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
     }(std::make_integer_sequence<int, D - 1>{});
+  }
+  float rr[MT];  // DN_EXACT: r of row mt*16 + (lane & 15)
+  if constexpr (NORM == DN_EXACT) {
+    // ssq_in[p][row], p < n_parts: thread t sums rows (t % 64) over parts t/64, t/64 + NW, ...
+    // then the NW partial sums of a row add in fixed order (deterministic)
+    const int row = threadIdx.x & 63;
+    float t = 0.f;
+    if (row < M)
+      for (int p = threadIdx.x >> 6; p < g.n_parts; p += NW) t += g.ssq_in[p * 64 + row];
+    sm_r[threadIdx.x] = t;
+    for (int c = threadIdx.x; c < KT * 4; c += NW * 64)
+      *(u16x8*)(sm_w + c * 8) = *(const u16x8*)(g.norm_w + kt0 * 32 + c * 8);
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int rw = mt * 16 + (lane & 15);
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += sm_r[w * 64 + rw];
+      rr[mt] = 1.0f / sqrtf(s / (float)(g.KT * 32) + g.eps);
+    }
+  }
+  if (b < nb) {
     bool fin = false;
     while (!fin) {
       [&]<int... I>(std::integer_sequence<int, I...>) {
@@ -108,13 +154,27 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
           // keep the issued loads ahead of the MFMAs (the scheduler would otherwise
           // interleave them to save registers, leaving few loads in flight)
           __builtin_amdgcn_sched_barrier(0);
+          if constexpr (NORM == DN_EXACT) {
+#pragma unroll
+            for (int u = 0; u < TW; ++u) {
+              const u16x8 nv = *(const u16x8*)(sm_w + (b * TW + u) * 32 + 8 * (lane >> 4));
+#pragma unroll
+              for (int mt = 0; mt < MT; ++mt) {
+                const u16x8 xv = __builtin_bit_cast(u16x8, av[d][u][mt]);
+                bf16x8 y;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) y[j] = (__bf16)(bf2f(nv[j]) * rbf(bf2f(xv[j]) * rr[mt]));
+                av[d][u][mt] = y;
+              }
+            }
+          }
 #pragma unroll
           for (int u = 0; u < TW; ++u)
 #pragma unroll
             for (int s = 0; s < S; ++s)
 #pragma unroll
               for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[d][u][mt], wv[d][s][u], acc[s][mt]);
-          if constexpr (NORM) {
+          if constexpr (NORM == DN_FOLD) {
 #pragma unroll
             for (int u = 0; u < TW; ++u)
 #pragma unroll
@@ -136,7 +196,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) red[wave][(s * MT + mt) * 64 + lane] = acc[s][mt];
-  if constexpr (NORM) {
+  if constexpr (NORM == DN_FOLD) {
     // lanes l, l^16, l^32, l^48 hold the four k-quarters of row (l & 15)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -167,7 +227,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
       const int row = mt * 16 + 4 * (ln >> 4) + r;
       if (row >= M) continue;
       g.part[((int64_t)blockIdx.y * M + row) * g.ldp + col] = v[0][r];
-      if constexpr (NORM) {
+      if constexpr (NORM == DN_FOLD) {
         if (nt == 0 && (ln & 15) == 0) {
           float t = 0.f;
 #pragma unroll
@@ -178,14 +238,14 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
     }
     return;
   }
-  if constexpr (NORM) {
-    // folded RMSNorm: out = rsqrt(mean(x^2) + eps) * (x @ (W * w)^T)   
+  if constexpr (NORM == DN_FOLD) {
+    // folded RMSNorm: out = rsqrt(mean(x^2) + eps) * (x @ (W * w)^T)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int rr = mt * 16 + 4 * (ln >> 4) + r;
+      const int rr2 = mt * 16 + 4 * (ln >> 4) + r;
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) t += sm_ss[w][rr];
+      for (int w = 0; w < NW; ++w) t += sm_ss[w][rr2];
       const float inv = 1.0f / sqrtf(t / (float)(g.KT * 32) + g.eps);
 #pragma unroll
       for (int s = 0; s < S; ++s) v[s][r] *= inv;
@@ -206,12 +266,21 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
         if ((ln & 15) == 0) g.keys[(int64_t)row * g.n_tiles + nt] = key;  // [M][n_tiles]
         if (g.C) g.C[(int64_t)row * g.ldc + col] = f2bf(lv);
       }
+    } else if constexpr (EPI == EPI_RESID) {
+      // all lanes take part in the 16-lane ssq reduction: rows >= M contribute zero
+      const bool live = row < M;
+      const u16 ob = live ? f2bf(rbf(v[0][r]) + bf2f(g.R[(int64_t)row * g.ldr + col])) : (u16)0;
+      if (live) g.C[(int64_t)row * g.ldc + col] = ob;
+      if (g.ssq_out) {
+        float q = bf2f(ob) * bf2f(ob);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) q += __shfl_xor(q, o, 16);
+        if (live && (ln & 15) == 0) g.ssq_out[nt * 64 + row] = q;
+      }
     } else if (row < M) {
       float o;
       if constexpr (EPI == EPI_NONE) {
         o = v[0][r];
-      } else if constexpr (EPI == EPI_RESID) {
-        o = rbf(v[0][r]) + bf2f(g.R[(int64_t)row * g.ldr + col]);
       } else if constexpr (EPI == EPI_SILU) {
         o = rbf(silu_f(rbf(v[0][r]))) * rbf(v[S - 1][r]);
       } else {
@@ -230,7 +299,7 @@ struct DecodeCfg {
   static constexpr int D = (S == 1 && MT == 1) ? 3 : 2;
 };
 
-template <int MT, int EPI, bool NORM>
+template <int MT, int EPI, int NORM>
 static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   using C = DecodeCfg<MT, S>;
@@ -242,7 +311,7 @@ static void decode_launch(const DecodeArgs& a, hipStream_t s) {
                        s, a);
 }
 
-template <int EPI, bool NORM>
+template <int EPI, int NORM>
 static void decode_mt(const DecodeArgs& a, hipStream_t s) {
   if (a.M <= 16)
     decode_launch<1, EPI, NORM>(a, s);
@@ -255,10 +324,11 @@ static void decode_mt(const DecodeArgs& a, hipStream_t s) {
 }
 
 // q/k/v projection of a decode step with K split over `kslices` workgroup slices and the
-// reduction (+ folded-norm scale) left to the consumer (launch_attn_decode_fused): with
-// NW = 4 the 384 x 2 workgroups of Qwen3-8B sit 3 per CU, every CU streaming the same bytes.
+// reduction left to the consumer (launch_attn_decode_fused): with NW = 4 the 384 x 2
+// workgroups of Qwen3-8B sit 3 per CU, every CU streaming the same bytes.  `norm` selects
+// the RMSNorm mode: DN_EXACT (ssq_in / n_parts / norm_w), DN_FOLD (writes ssq) or none.
 void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
-                                float* part, float* ssq, float eps, hipStream_t s) {
+                                float* part, float* ssq, const DecodeNorm& norm, hipStream_t s) {
   DecodeArgs a = {};
   a.A = A;
   a.lda = lda;
@@ -266,12 +336,20 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
   a.KT = K / 32;
   a.n_tiles = N / 16;
   a.M = M;
-  a.eps = eps;
+  a.eps = norm.eps;
   a.part = part;
   a.ldp = N;
   a.ssq = ssq;
-  hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, true>), dim3(N / 16, kslices), dim3(256), 0, s,
-                     a);
+  a.ssq_in = norm.ssq_in;
+  a.n_parts = norm.n_parts;
+  a.norm_w = norm.w;
+  const dim3 grid(N / 16, kslices);
+  if (norm.mode == DN_EXACT)
+    hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT>), grid, dim3(256), 0, s, a);
+  else if (norm.mode == DN_FOLD)
+    hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_FOLD>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_NONE>), grid, dim3(256), 0, s, a);
 }
 
 // ============================================================ tiled (prefill) kernel
@@ -406,157 +484,6 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(
   }
 }
 
-// ============================================================ 256x256 tiled (large prefill)
-// 256x256x64 block tile, 8 waves as 2 (M) x 4 (N), each wave 128x64 = 8x4 MFMA tiles
-// (128 fp32 accumulator registers).  Per K-step the workgroup stages A (256 rows x 64 k,
-// 32 KiB, source-swizzled) and B (16 n-tiles x 2 k-tiles = 32 packed 1 KiB tiles) into one
-// of two 64 KiB LDS buffers with global_load_lds_dwordx4 (8 pieces per wave), overlapping
-// the next step's transfer with this step's 64 MFMAs per wave.  EPI_SILU: the B tile holds
-// 128 gate + 128 up columns of the same 128 outputs.
-template <int EPI>
-__global__ __launch_bounds__(512) void gemm_tiled256_kernel(
-    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
-    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    const float* __restrict__ rs) {
-  __shared__ __attribute__((aligned(16))) char lds[2 * 65536];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int m0 = blockIdx.y * 256;
-  const int ncols = (EPI == EPI_SILU) ? 128 : 256;
-  const int n0 = blockIdx.x * ncols;
-  const int nsteps = KT / 2;
-  // A pieces q = 0..31: rows 8q..8q+7; B pieces q = 0..31: local n-tile q/2, k-tile q%2
-  const u16* a_src[4];
-  const u16* b_src[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int q = wave * 4 + p;
-    const int r = 8 * q + (lane >> 3);
-    int grow = m0 + r;
-    grow = grow < M ? grow : M - 1;
-    const int chunk = (lane & 7) ^ ((r >> 1) & 7);
-    a_src[p] = A + (int64_t)grow * lda + chunk * 8;
-    const int j = q >> 1, kk = q & 1;
-    int gnt;
-    if (EPI == EPI_SILU)
-      gnt = (j < 8) ? (n0 / 16 + j) : (n_tiles_w / 2 + n0 / 16 + (j - 8));
-    else
-      gnt = n0 / 16 + j;
-    b_src[p] = Wp + ((int64_t)gnt * KT + kk) * 512 + lane * 8;
-  }
-  auto stage = [&](int buf, int step) {
-    char* base = lds + buf * 65536;
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[p] + step * 64), (void*)(base + (wave * 4 + p) * 1024),
-                                       16, 0, 0);
-#pragma unroll
-    for (int p = 0; p < 4; ++p)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src[p] + (int64_t)step * 1024),
-                                       (void*)(base + 32768 + (wave * 4 + p) * 1024), 16, 0, 0);
-  };
-  // local n-tiles of this wave (4 x 16 columns)
-  int bj[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (EPI == EPI_SILU)
-      bj[t] = (t < 2) ? (wc * 2 + t) : (8 + wc * 2 + (t - 2));
-    else
-      bj[t] = wc * 4 + t;
-  }
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  stage(0, 0);
-  __syncthreads();
-  for (int t = 0; t < nsteps; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nsteps) stage(cur ^ 1, t + 1);
-    const char* base = lds + cur * 65536;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 bfr[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) bfr[nt] = *(const bf16x8*)(base + 32768 + (bj[nt] * 2 + kk) * 1024 + lane * 16);
-#pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        const int r = wr * 128 + mt * 16 + (lane & 15);
-        const int c = kk * 4 + (lane >> 4);
-        const bf16x8 af = *(const bf16x8*)(base + r * 128 + 16 * (c ^ ((r >> 1) & 7)));
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16(af, bfr[nt], acc[mt][nt]);
-      }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int mt = 0; mt < 8; ++mt) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = m0 + wr * 128 + mt * 16 + 4 * (lane >> 4) + r;
-      if (row >= M) continue;
-      const float sc = rs ? rs[row] : 1.0f;  // folded RMSNorm row scale
-      if constexpr (EPI == EPI_SILU) {
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int col = n0 + wc * 32 + nt * 16 + (lane & 15);
-          const float gg = rbf(acc[mt][nt][r] * sc);
-          const float uu = rbf(acc[mt][nt + 2][r] * sc);
-          C[(int64_t)row * ldc + col] = f2bf(rbf(silu_f(gg)) * uu);
-        }
-      } else {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
-          float o = acc[mt][nt][r] * sc;
-          if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(R[(int64_t)row * ldr + col]);
-          C[(int64_t)row * ldc + col] = f2bf(o);
-        }
-      }
-    }
-  }
-}
-
-// ============================================================ ring-staged 256x256 (prefill)
-// Same 256x256x64 block tile and 2 (M) x 4 (N) wave grid as gemm_tiled256, but the
-// staging never drains (cdna_hip_programming.md §5 "Pipelining across barriers"):
-//  * LDS is a ring of 10 half-tile slots of 16 KiB (the whole 160 KiB).  A K-step's
-//    tile is four half-tiles consumed in this order: A0 (rows qr=0 of both wave rows),
-//    B0 (columns qc=0 of every wave column), B1, A1.  Half-tile s lives in slot s % 10.
-//  * One K-step = 4 phases, one per output quadrant of a wave (64 rows x 32 cols, 16
-//    MFMAs): (A0,B0) (A0,B1) (A1,B1) (A1,B0).  Phase P reads its register sub-tiles,
-//    issues half-tile P+6 (2 global_load_lds_dwordx4 per thread), waits with a COUNTED
-//    vmcnt for the half-tile phase P+1 reads (4 half-tiles stay in flight), passes a raw
-//    s_barrier, runs its 16 MFMAs at raised priority and passes a second s_barrier.
-//  * Waves 4-7 run one barrier behind waves 0-3 (each SIMD holds one wave of each half),
-//    so on every SIMD one wave is in its MFMA segment while its partner reads LDS.
-//  * Hazards (derived in DESIGN.md §4): a slot is re-filled only >= 2 phases after its
-//    last read, which bounds the look-ahead to ring - 4 = 6 half-tiles.
-//  * Operands are swapped (C^T = W * A^T) so each lane's 4 accumulator registers are 4
-//    consecutive output columns: the epilogue stores 8 bytes per lane.
-//  * blockIdx is remapped XCD-aware (blocks sharing an XCD get consecutive tiles) and
-//    grouped 8 row-blocks deep so an XCD's concurrent blocks share A rows and W columns.
-#define RING_SLOTS 10
-
-// vm_wait with a run-time count (even values 0..14; -1 = no wait); a constant argument
-// folds to the single s_waitcnt
-__device__ __forceinline__ void vm_wait_rt(int n) {
-  switch (n) {
-    case 0: vm_wait<0>(); break;
-    case 2: vm_wait<2>(); break;
-    case 4: vm_wait<4>(); break;
-    case 6: vm_wait<6>(); break;
-    case 8: vm_wait<8>(); break;
-    case 10: vm_wait<10>(); break;
-    case 12: vm_wait<12>(); break;
-    case 14: vm_wait<14>(); break;
-    default: break;
-  }
-}
-
-
 // Tail split (SplitTail): when the tile count leaves a partial last round on an XCD
 // (Qwen3-32B o/down: 640 tiles = 2.5 rounds of 256 CUs), each XCD's last `rem` tiles are
 // cut into `split` K-slices so the last round is full.  Slices publish fp32 partials
@@ -606,270 +533,6 @@ __device__ __forceinline__ void tile_order(const SplitTail& st, int grid_m, int 
   tile_order_v(st, grid_m, grid_n, blockIdx.x, gridDim.x, bm, bn, slice, nsl, sidx);
 }
 
-template <int EPI, bool KEEPB>
-__global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
-    const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
-    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    const float* __restrict__ rs, int grid_m, int grid_n, SplitTail st) {
-  __shared__ __attribute__((aligned(16))) char lds[RING_SLOTS * 16384];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wr = wave >> 2, wc = wave & 3;
-  int bm, bn, slice = 0, nsl = 1, sidx = 0;
-  tile_order(st, grid_m, grid_n, bm, bn, slice, nsl, sidx);
-  const int m0 = bm * 256;
-  const int n0 = bn * ((EPI == EPI_SILU) ? 128 : 256);
-  const int nK = KT / 2 / nsl;  // 64-deep K-steps of this slice
-  const int S = 4 * nK;         // half-tiles
-  const int k0 = slice * nK;    // first K-step
-
-  // ---- staging sources: this wave's two 1 KiB pieces of each half-tile kind
-  const u16* a_src[2][2];      // [half][piece]
-  const u16* b_src[2];         // [half] (the 2 pieces are the 2 consecutive k-tiles)
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      const int qp = 2 * wave + p;                 // piece 0..15: image rows 8qp..8qp+7
-      const int i = 8 * qp + (lane >> 3);          // image row 0..127
-      int grow = m0 + (i >> 6) * 128 + h * 64 + (i & 63);
-      grow = grow < M ? grow : M - 1;
-      const int chunk = (lane & 7) ^ ((i >> 1) & 7);
-      a_src[h][p] = A + (int64_t)grow * lda + chunk * 8 + k0 * 64;
-    }
-    // image n-tile nl = wave: wave column nl>>1, sub-tile nl&1
-    int gnt;
-    if constexpr (EPI == EPI_SILU)
-      gnt = (h == 0 ? 0 : n_tiles_w / 2) + n0 / 16 + (wave >> 1) * 2 + (wave & 1);
-    else
-      gnt = n0 / 16 + (wave >> 1) * 4 + h * 2 + (wave & 1);
-    b_src[h] = Wp + ((int64_t)gnt * KT + 2 * k0) * 512 + lane * 8;
-  }
-  // kind: 0 = A0, 1 = B0, 2 = B1, 3 = A1 (the consumption order within a K-step)
-  auto issue = [&](int kind, int t, int slot) {
-    char* base = lds + slot * 16384 + wave * 2048;
-    if (kind == 0 || kind == 3) {
-      const int h = kind == 0 ? 0 : 1;
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[h][0] + t * 64), (void*)base, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(a_src[h][1] + t * 64), (void*)(base + 1024), 16, 0, 0);
-    } else {
-      const u16* src = b_src[kind - 1] + (int64_t)t * 1024;
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)base, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(src + 512), (void*)(base + 1024), 16, 0, 0);
-    }
-  };
-
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // KEEPB: both B sub-tiles stay in registers for the whole K-step (B0 is not re-read by
-  // the last quadrant), so every slot's last read is no later than its own index and the
-  // look-ahead grows from ring - 4 to ring - 2 half-tiles.
-  constexpr int D = KEEPB ? RING_SLOTS - 2 : RING_SLOTS - 4;
-  bf16x8 areg[4][2], breg[2][2][2];  // breg[quadrant column][nt][ks]
-
-  auto read_a = [&](int slot) {
-    const char* base = lds + slot * 16384;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int i = wr * 64 + mt * 16 + (lane & 15);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int c = ks * 4 + (lane >> 4);
-        areg[mt][ks] = *(const bf16x8*)(base + i * 128 + 16 * (c ^ ((i >> 1) & 7)));
-      }
-    }
-  };
-  auto read_b = [&](auto QC, int slot) {
-    constexpr int qc = decltype(QC)::value;
-    const char* base = lds + slot * 16384 + lane * 16;
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) breg[qc][nt][ks] = *(const bf16x8*)(base + ((wc * 2 + nt) * 2 + ks) * 1024);
-  };
-  auto mfmas = [&](auto QR, auto QC) {
-    constexpr int qr = decltype(QR)::value, qc = decltype(QC)::value;
-    constexpr int bq = KEEPB ? qc : 0;  // without KEEPB one B register set is reused
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-          acc[qr * 4 + mt][qc * 2 + nt] = mfma16(breg[bq][nt][ks], areg[mt][ks], acc[qr * 4 + mt][qc * 2 + nt]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto wrap = [](int x) { return x >= RING_SLOTS ? x - RING_SLOTS : x; };
-  using Q0 = std::integral_constant<int, 0>;
-  using Q1 = std::integral_constant<int, 1>;
-
-  // One phase P = 4t + j: reads, issue of half-tile P + D (when it exists; its kind
-  // (j + D) & 3 is a compile-time constant), counted wait, barrier, MFMAs, barrier.
-  // VM >= 0: that constant wait; VM == -2: the run-time wait of wait_at(P) (tail steps).
-  auto wait_at = [&](int P) {  // what phase P+1 reads: half-tile P+2 (quadrants 0-2)
-    if (P >= S - 1 || ((P + 1) & 3) == 3) return -1;
-    const int last = P + D < S - 1 ? P + D : S - 1;
-    return 2 * (last - (P + 2));
-  };
-  auto phase = [&](auto J, auto VM, int t, int rb) {
-    constexpr int j = decltype(J)::value;
-    constexpr int vmc = decltype(VM)::value;
-    const int P = 4 * t + j;
-    if constexpr (j == 0) { read_a(rb); read_b(Q0{}, wrap(rb + 1)); }
-    if constexpr (j == 1) read_b(std::integral_constant<int, KEEPB ? 1 : 0>{}, wrap(rb + 2));
-    if constexpr (j == 2) read_a(wrap(rb + 3));
-    if constexpr (j == 3 && !KEEPB) read_b(Q0{}, wrap(rb + 1));
-    const int si = P + D;
-    if (vmc >= 0 || si < S) issue((j + D) & 3, si >> 2, si % RING_SLOTS);
-    if constexpr (vmc >= 0)
-      vm_wait<vmc>();
-    else
-      vm_wait_rt(wait_at(P));
-    raw_barrier();
-    if constexpr (j == 0) mfmas(Q0{}, Q0{});
-    if constexpr (j == 1) mfmas(Q0{}, Q1{});
-    if constexpr (j == 2) mfmas(Q1{}, Q1{});
-    if constexpr (j == 3) mfmas(Q1{}, Q0{});
-    raw_barrier();
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  using VSTEADY = std::integral_constant<int, 2 * (D - 2)>;
-  using VTAIL = std::integral_constant<int, -2>;
-
-  // prologue: half-tiles 0..D-1 in flight, wait for 0 and 1 (A0, B0 of step 0)
-#pragma unroll
-  for (int s = 0; s < D; ++s) issue(s & 3, s >> 2, s);
-  vm_wait<2 * (D - 2)>();
-  raw_barrier();
-  if (wr == 1) raw_barrier();  // stagger: waves 4-7 one barrier behind
-
-  int rb = 0;  // slot of the current step's A0 half-tile = (4t) % 10
-  int t = 0;
-  // steady state: all four phases issue (4t + 3 + D <= S - 1), constant wait
-  for (; 4 * t + 3 + D <= S - 1; ++t) {
-    phase(I0{}, VSTEADY{}, t, rb);
-    phase(I1{}, VSTEADY{}, t, rb);
-    phase(I2{}, VSTEADY{}, t, rb);
-    phase(I3{}, VSTEADY{}, t, rb);
-    rb = wrap(rb + 4);
-  }
-  // tail: the last (D + 3) / 4 steps issue what is left and drain with exact counts
-  for (; t < nK; ++t) {
-    phase(I0{}, VTAIL{}, t, rb);
-    phase(I1{}, VTAIL{}, t, rb);
-    phase(I2{}, VTAIL{}, t, rb);
-    phase(I3{}, VTAIL{}, t, rb);
-    rb = wrap(rb + 4);
-  }
-  if (wr == 0) raw_barrier();  // close the stagger
-
-  if (nsl > 1) {  // ---- tail split: publish or combine
-    __syncthreads();  // every wave is past its last LDS read: lds is free
-    unsigned* ticket_lds = (unsigned*)lds;
-    unsigned* cnt = st.cnt + sidx;
-    unsigned* done = st.cnt + 8 * (st.tiles_per_xcd - st.full_per_xcd) + sidx;
-    if (threadIdx.x == 0) ticket_lds[0] = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const unsigned ticket = ticket_lds[0];
-    float* part = st.ws + (size_t)sidx * nsl * 65536;
-    if (ticket + 1 < (unsigned)nsl) {  // not last: publish this slice's partial write-through
-      unsigned long long* dst = (unsigned long long*)(part + (size_t)slice * 65536);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const unsigned long long v = ((unsigned long long)__float_as_uint(acc[i][j][2 * hh + 1]) << 32) |
-                                         __float_as_uint(acc[i][j][2 * hh]);
-            __hip_atomic_store(dst + (((i * 4 + j) * 2 + hh) * 512 + threadIdx.x), v, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    // sc1 poll, then sc1 loads of the partials: no acquire fence (MI355X_MICROARCH.md,
-    // visibility "Valid forms" row 1: one workgroup per CU, drained sc1 stores, one add per
-    // storing workgroup behind its barrier; the other waves load after a barrier)
-    if (threadIdx.x == 0) {
-      while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1 < (unsigned)nsl)
-        __builtin_amdgcn_s_sleep(2);
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    // fixed slice order, in place (a second 128-register accumulator would spill)
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          float v0 = 0.f, v1 = 0.f;
-          for (int sl = 0; sl < nsl; ++sl) {
-            if (sl == slice) {
-              v0 += acc[i][j][2 * hh];
-              v1 += acc[i][j][2 * hh + 1];
-            } else {
-              const unsigned long long* src = (const unsigned long long*)(part + (size_t)sl * 65536);
-              const unsigned long long v = __hip_atomic_load(src + ((i * 4 + j) * 2 + hh) * 512 + threadIdx.x,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              v0 += __uint_as_float((unsigned)v);
-              v1 += __uint_as_float((unsigned)(v >> 32));
-            }
-          }
-          acc[i][j][2 * hh] = v0;
-          acc[i][j][2 * hh + 1] = v1;
-        }
-  }
-
-  // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + (lane & 15);
-    if (row >= M) continue;
-    const float sc = rs ? rs[row] : 1.0f;  // folded RMSNorm row scale
-    if constexpr (EPI == EPI_SILU) {
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int col = n0 + wc * 32 + nt * 16 + 4 * (lane >> 4);
-        u16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float gg = rbf(acc[i][nt][r] * sc);
-          const float uu = rbf(acc[i][2 + nt][r] * sc);
-          v[r] = f2bf(rbf(silu_f(gg)) * uu);
-        }
-        *(u16x4*)(C + (int64_t)row * ldc + col) = v;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int col = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + 4 * (lane >> 4);
-        u16x4 v;
-        u16x4 rr;
-        if constexpr (EPI == EPI_RESID) rr = *(const u16x4*)(R + (int64_t)row * ldr + col);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float o = acc[i][j][r] * sc;
-          if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(rr[r]);
-          v[r] = f2bf(o);
-        }
-        *(u16x4*)(C + (int64_t)row * ldc + col) = v;
-      }
-    }
-  }
-}
-
 // ============================================================ 4-wave 256x256 prefill GEMM
 // gemm_w4_kernel: the same 256x256 output tile and K-step 64, on FOUR waves of 128x128
 // (8x8 accumulator tiles = 256 AGPRs each, one wave per SIMD).  Per K-step a wave issues
@@ -883,7 +546,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ring256_kernel(
 //    (rows 0-63) while the 16 LDS-DMA pieces of step t+2 are issued into c; counted vmcnt
 //    (step t+1's pieces landed) + barrier; [C] MFMAs on F1 (rows 64-127) while F0 of step
 //    t+1 is read from c ^ 1.  Step t+1's pieces have one full iteration to land.
-template <int EPI, int ORD>
+template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
     u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
@@ -927,29 +590,20 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     b_soff[p] = ((int64_t)gnt * KT + 2 * k0 + (q & 1)) * 1024;
   }
   const unsigned b_voff = lane * 16;
-  // ORD & 2: buffer_load_dwordx4 ... lds with the per-piece and per-step offsets in SGPRs
-  // (soffset) instead of a 64-bit VGPR address per piece
+  // buffer_load_dwordx4 ... lds with the per-piece and per-step offsets in SGPRs (soffset)
+  // instead of a 64-bit VGPR address per piece
   const __amdgpu_buffer_rsrc_t a_rsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)a_base, 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, 0, 0x7fffffff, 0x00020000);
   auto issue = [&](int p, int t, int buf) {  // piece p (0-7 A, 8-15 B) of K-step t into buffer buf
     char* base = lds + buf * 65536;
-    if constexpr ((ORD & 2) != 0) {
-      typedef __attribute__((address_space(3))) void* lds_ptr;
-      if (p < 8)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr)(base + (8 * wv + p) * 1024), 16, a_voff[p], t * 128,
-                                                 0, 0);
-      else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr)(base + 32768 + (8 * wv + p - 8) * 1024), 16, b_voff,
-                                                 (int)(b_soff[p - 8] + (int64_t)t * 2048), 0, 0);
-    } else {
-      if (p < 8)
-        __builtin_amdgcn_global_load_lds((const void*)(a_base + t * 128 + a_voff[p]),
-                                         (void*)(base + (8 * wv + p) * 1024), 16, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds((const void*)((const char*)Wp + b_soff[p - 8] + (int64_t)t * 2048 + b_voff),
-                                         (void*)(base + 32768 + (8 * wv + p - 8) * 1024), 16, 0, 0);
-    }
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    if (p < 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a_rsrc, (lds_ptr)(base + (8 * wv + p) * 1024), 16, a_voff[p], t * 128,
+                                               0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b_rsrc, (lds_ptr)(base + 32768 + (8 * wv + p - 8) * 1024), 16, b_voff,
+                                               (int)(b_soff[p - 8] + (int64_t)t * 2048), 0, 0);
   };
 
   // ---- fragment reads: A rows wr*128 + mt*16 + (lane & 15), swizzle depends on lane only
@@ -992,14 +646,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   // MODE 0: steady (issue step t+2, wait for t+1, read F0 of t+1); 1: t = nK-2 (no issue,
   // wait 0, read); 2: t = nK-1 (no issue, no wait, no read)
   // MFMA x of a K-step (0..127) in issue order: [A] F0 rows 0-63, [B] F0 rows 64-127 then F1
-  // rows 0-63, [C] F1 rows 64-127; ORD & 1 = nt-major inside each group of 32
+  // rows 0-63, [C] F1 rows 64-127
   auto mfx = [&](int x) {
     const int kh = (x >= 64) ? 1 : 0;
     const int q = x & 31, half = (x >> 5) & 1;  // group of 32: rows 64 * half + ...
-    if constexpr ((ORD & 1) == 0)
-      mf(kh, 4 * half + (q >> 3), q & 7);
-    else
-      mf(kh, 4 * half + (q & 3), q >> 2);
+    mf(kh, 4 * half + (q & 3), q >> 2);  // nt-major inside each group of 32
   };
   // Every barrier is straddled by MFMAs (the last one before it is issued after the wait),
   // so the matrix pipe stays busy while the waves meet.
@@ -1065,7 +716,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   iter(std::integral_constant<int, 2>{}, t + 1);
   acc_fence();
 
-  if (nsl > 1) {  // ---- tail split: publish or combine (as gemm_ring256_kernel)
+  if (nsl > 1) {  // ---- tail split: publish or combine (tools/archive/gemm_superseded.hip had the same in the 8-wave ring)
     __syncthreads();
     unsigned* ticket_lds = (unsigned*)lds;
     unsigned* cnt = st.cnt + sidx;
@@ -1548,93 +1199,59 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
   }
 }
 
-// INFERD_GEMM_TILE selects the prefill GEMM (read per call so one process can A/B them):
-// "w4p" (default: persistent w4, w4 where the grid needs a tail split) | "w4" ("w4m" / "w4g" /
-// "w4mg" its A/B arms) | "ring" | "256" | "128"
-static int gemm_tile_variant() {
-  const char* e = getenv("INFERD_GEMM_TILE");
-  if (!e || !*e) return 8;
-  if (e[0] == 'r') return 0;
-  if (e[0] == 'w' && e[2] == 'p') return 8;  // "w4p": persistent
-  if (e[0] == 'w') {  // "w4" = "w4nb" (default) | "w4m": mt-major MFMA order | "w4g": global_load_lds
-    int v = 7;
-    for (const char* c = e + 2; *c; ++c) v &= (*c == 'm') ? ~1 : (*c == 'g') ? ~2 : ~0;
-    return v;
-  }
-  return atoi(e);
-}
-
-// Tail-split plan for `tiles` 256x256 tiles of nK K-steps on 8 XCDs x 32 CUs (one 512-thread
-// workgroup per CU).  INFERD_GEMM_SPLIT=0 disables it.  The fp32 partial workspace and the
-// counters are allocated once (zeroed) and grown on demand; never inside a graph capture.
 static int env_or(const char* name, int dflt) {
   const char* e = getenv(name);
   return e && *e ? atoi(e) : dflt;
 }
 
-template <int EPI>
-static void ring_launch(bool keepb, int grid, hipStream_t s, const u16* A, int64_t lda, const u16* Wp, int KT, int ntw,
-                        u16* C, int64_t ldc, const u16* R, int64_t ldr, int M, const float* rs, int gm, int gn,
-                        const SplitTail& st) {
-  if (keepb)
-    hipLaunchKernelGGL((gemm_ring256_kernel<EPI, true>), dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                       ldr, M, rs, gm, gn, st);
-  else
-    hipLaunchKernelGGL((gemm_ring256_kernel<EPI, false>), dim3(grid), dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                       ldr, M, rs, gm, gn, st);
-}
-
-#define SPLIT_MAX_DEVICES_ 16
-template <int ORD>
 static void w4_launch(int epi, int grid, hipStream_t s, const u16* A, int64_t lda, const u16* Wp, int KT, int ntw,
                       u16* C, int64_t ldc, const u16* R, int64_t ldr, int M, const float* rs, int gm, int gn,
                       const SplitTail& st) {
   switch (epi) {
     case EPI_NONE:
-      hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE, ORD>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                         ldr, M, rs, gm, gn, st);
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
+                         M, rs, gm, gn, st);
       break;
     case EPI_RESID:
-      hipLaunchKernelGGL((gemm_w4_kernel<EPI_RESID, ORD>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc,
-                         R, ldr, M, rs, gm, gn, st);
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI_RESID>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                         ldr, M, rs, gm, gn, st);
       break;
     default:
-      hipLaunchKernelGGL((gemm_w4_kernel<EPI_SILU, ORD>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc,
-                         R, ldr, M, rs, gm, gn, st);
+      hipLaunchKernelGGL((gemm_w4_kernel<EPI_SILU>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
+                         ldr, M, rs, gm, gn, st);
       break;
   }
 }
 
 // persistent grid: one workgroup per CU, a multiple of 8 (units keep their XCD), <= units
+#define W4P_MAX_DEVICES 16
 static int w4p_grid(int units) {
-  static int ncu[SPLIT_MAX_DEVICES_] = {0};
+  static int ncu[W4P_MAX_DEVICES] = {0};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= SPLIT_MAX_DEVICES_) dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= W4P_MAX_DEVICES) dev = 0;
   if (ncu[dev] == 0) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
     ncu[dev] = n;
   }
-  const int cap = env_or("INFERD_W4P_GRID", 0) > 0 ? env_or("INFERD_W4P_GRID", 0) : ncu[dev];
-  if (units <= cap) return units;
-  return cap & ~7;
+  if (units <= ncu[dev]) return units;
+  return ncu[dev] & ~7;
 }
 
-// Per device (a process may drive several GPUs); grown on demand, never inside a graph
-// capture, not thread-safe (one host thread per device, like the span API).
-#define SPLIT_MAX_DEVICES 16
-struct SplitWs {
-  float* ws = nullptr;
-  size_t ws_bytes = 0;
-  unsigned* cnt = nullptr;
-  int cnt_n = 0;
-};
-static SplitWs g_split[SPLIT_MAX_DEVICES];
+void gemm_ws_free(GemmWs* w) {
+  if (!w) return;
+  if (w->ws) (void)hipFree(w->ws);
+  if (w->cnt) (void)hipFree(w->cnt);
+  *w = GemmWs{};
+}
 
-static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
+// Tail-split plan for `tiles` 256x256 tiles of nK K-steps on 8 XCDs x 32 CUs (one workgroup
+// per CU), with its fp32 partials and tickets in the caller's (span's) workspace: allocated
+// zeroed and grown on demand, never inside a graph capture (no workspace, or capturing: no
+// split).  INFERD_GEMM_SPLIT=0 disables it (A/B).
+static SplitTail plan_split_tail(int tiles, int nK, GemmWs* w, hipStream_t s) {
   SplitTail st = {1, 0, 0, 0, nullptr, nullptr};
-  const char* e = getenv("INFERD_GEMM_SPLIT");
-  if (e && *e && atoi(e) == 0) return st;
+  if (!w || env_or("INFERD_GEMM_SPLIT", 1) == 0) return st;
   if (tiles % 8) return st;
   const int per = tiles / 8, rem = per % 32;
   if (rem == 0 || 32 % rem) return st;
@@ -1642,42 +1259,34 @@ static SplitTail plan_split_tail(int tiles, int nK, hipStream_t s) {
   if (split > 8 || nK % split || nK / split < 3) return st;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return st;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= SPLIT_MAX_DEVICES) return st;
-  SplitWs& w = g_split[dev];
   const size_t bytes = (size_t)8 * rem * split * 65536 * sizeof(float);
-  if (bytes > w.ws_bytes) {
-    if (w.ws) (void)hipFree(w.ws);
-    w.ws = nullptr;
-    w.ws_bytes = 0;
-    if (hipMalloc((void**)&w.ws, bytes) != hipSuccess) return st;
-    w.ws_bytes = bytes;
+  if (bytes > w->ws_bytes) {
+    if (w->ws) (void)hipFree(w->ws);
+    w->ws = nullptr;
+    w->ws_bytes = 0;
+    if (hipMalloc((void**)&w->ws, bytes) != hipSuccess) return st;
+    w->ws_bytes = bytes;
   }
-  if (2 * 8 * rem > w.cnt_n) {
-    if (w.cnt) (void)hipFree(w.cnt);
-    w.cnt = nullptr;
-    w.cnt_n = 0;
-    if (hipMalloc((void**)&w.cnt, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
-    if (hipMemset(w.cnt, 0, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
-    w.cnt_n = 2 * 8 * rem;
+  if (2 * 8 * rem > w->cnt_n) {
+    if (w->cnt) (void)hipFree(w->cnt);
+    w->cnt = nullptr;
+    w->cnt_n = 0;
+    if (hipMalloc((void**)&w->cnt, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
+    if (hipMemsetAsync(w->cnt, 0, 2 * 8 * rem * sizeof(unsigned), s) != hipSuccess) return st;
+    w->cnt_n = 2 * 8 * rem;
   }
   st.split = split;
   st.tiles_per_xcd = per;
   st.full_per_xcd = per - rem;
   st.units_per_xcd = per - rem + rem * split;
-  st.ws = w.ws;
-  st.cnt = w.cnt;
+  st.ws = w->ws;
+  st.cnt = w->cnt;
   return st;
 }
 
-static bool use_ring256(int M, int N, int K, int epi) {
-  const int v = gemm_tile_variant();
-  if ((v != 0 && (v < 4 || v > 8)) || M < 512 || K < 192) return false;
-  return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
-}
-
-static bool use_tiled256(int M, int N, int epi) {
-  if (gemm_tile_variant() == 128 || M < 512) return false;
+// the 256x256 four-wave bodies (gemm_w4p / gemm_w4): >= 512 rows, whole 256-column tiles
+static bool use_w4(int M, int N, int K, int epi) {
+  if (M < 512 || K < 192) return false;
   return (epi == EPI_SILU) ? (N % 128 == 0) : (N % 256 == 0);
 }
 
@@ -1689,25 +1298,24 @@ bool gemm_uses_tiled(int M, int N, int K, int epi) {
 
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
-                 const RowNorm* norm) {
+                 const RowNorm* fold, GemmWs* ws, const DecodeNorm* dn, float* ssq_out) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
+  const bool tiled = gemm_uses_tiled(M, N, K, epi);
   const float* rs = nullptr;
-  if (norm && gemm_uses_tiled(M, N, K, epi)) {
-    launch_row_inv_rms(A, lda, M, K, norm->eps, norm->rs_ws, s);
-    rs = norm->rs_ws;
+  if (fold && tiled) {
+    launch_row_inv_rms(A, lda, M, K, fold->eps, fold->rs_ws, s);
+    rs = fold->rs_ws;
   }
-  if (gemm_uses_tiled(M, N, K, epi) && use_ring256(M, N, K, epi)) {
+  if (tiled && use_w4(M, N, K, epi)) {
     const int ncols = (epi == EPI_SILU) ? 128 : 256;
     const int gm = (M + 255) / 256, gn = N / ncols;
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
-    const SplitTail st = plan_split_tail(gm * gn, K / 64, s);
+    const SplitTail st = plan_split_tail(gm * gn, K / 64, ws, s);
     const int grid = st.split > 1 ? 8 * st.units_per_xcd : gm * gn;
-    // INFERD_GEMM_KEEPB=0 selects the look-ahead-6 schedule that re-reads B0 (A/B)
-    const bool keepb = env_or("INFERD_GEMM_KEEPB", 1) != 0;
     // w4p addresses C / R through 32-bit buffer offsets
     const bool fits32 = (int64_t)(M + 256) * ldc * 2 < 0x7fffffff && (!R || (int64_t)(M + 256) * ldr * 2 < 0x7fffffff);
-    if (gemm_tile_variant() == 8 && fits32 && st.split == 1) {
+    if (fits32 && st.split == 1) {
       const int g = w4p_grid(grid);
       switch (epi) {
         case EPI_NONE:
@@ -1725,46 +1333,10 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
       }
       return;
     }
-    if (gemm_tile_variant() >= 4 && gemm_tile_variant() <= 8) {  // w4p with a tail split: w4
-      switch (gemm_tile_variant()) {
-        case 4: w4_launch<0>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
-        case 5: w4_launch<1>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
-        case 6: w4_launch<2>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
-        default: w4_launch<3>(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st); break;
-      }
-      return;
-    }
-    switch (epi) {
-      case EPI_NONE:
-        ring_launch<EPI_NONE>(keepb, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);
-        break;
-      case EPI_RESID:
-        ring_launch<EPI_RESID>(keepb, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);
-        break;
-      default:
-        ring_launch<EPI_SILU>(keepb, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);
-        break;
-    }
+    w4_launch(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);  // tail split
     return;
   }
-  if (gemm_uses_tiled(M, N, K, epi) && use_tiled256(M, N, epi)) {
-    const int ncols = (epi == EPI_SILU) ? 128 : 256;
-    dim3 g(N / ncols, (M + 255) / 256);
-    const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
-    switch (epi) {
-      case EPI_NONE:
-        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_NONE>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
-        break;
-      case EPI_RESID:
-        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_RESID>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
-        break;
-      default:
-        hipLaunchKernelGGL(gemm_tiled256_kernel<EPI_SILU>, g, dim3(512), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
-        break;
-    }
-    return;
-  }
-  if (gemm_uses_tiled(M, N, K, epi)) {
+  if (tiled) {
     const int ncols = (epi == EPI_SILU) ? 64 : 128;
     dim3 g(N / ncols, (M + TBM - 1) / TBM);
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
@@ -1781,7 +1353,10 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     }
     return;
   }
-  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail)
+  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail; the
+  // DN_EXACT norm and the ssq_out partials are defined for M <= 64 only)
+  const int mode = fold ? DN_FOLD : (dn ? dn->mode : DN_NONE);
+  if ((mode == DN_EXACT || ssq_out) && M > 64) return;
   for (int m0 = 0; m0 < M; m0 += 64) {
     DecodeArgs a = {};
     a.M = (M - m0) < 64 ? (M - m0) : 64;
@@ -1795,19 +1370,31 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     a.R = R ? R + (int64_t)m0 * ldr : nullptr;
     a.ldr = ldr;
     a.keys = keys;
-    a.eps = norm ? norm->eps : 0.f;
-    if (norm) {
+    a.eps = fold ? fold->eps : (dn ? dn->eps : 0.f);
+    a.ssq_out = (epi == EPI_RESID) ? ssq_out : nullptr;
+    if (mode == DN_EXACT) {
+      a.ssq_in = dn->ssq_in;
+      a.n_parts = dn->n_parts;
+      a.norm_w = dn->w;
+    }
+    if (mode == DN_FOLD) {
       switch (epi) {
-        case EPI_NONE: decode_mt<EPI_NONE, true>(a, s); break;
-        case EPI_SILU: decode_mt<EPI_SILU, true>(a, s); break;
+        case EPI_NONE: decode_mt<EPI_NONE, DN_FOLD>(a, s); break;
+        case EPI_SILU: decode_mt<EPI_SILU, DN_FOLD>(a, s); break;
         default: return;  // the span folds norms into the NONE (qkv) and SILU (gate/up) GEMMs only
+      }
+    } else if (mode == DN_EXACT) {
+      switch (epi) {
+        case EPI_NONE: decode_mt<EPI_NONE, DN_EXACT>(a, s); break;
+        case EPI_SILU: decode_mt<EPI_SILU, DN_EXACT>(a, s); break;
+        default: decode_mt<EPI_ARGMAX, DN_EXACT>(a, s); break;
       }
     } else {
       switch (epi) {
-        case EPI_NONE: decode_mt<EPI_NONE, false>(a, s); break;
-        case EPI_RESID: decode_mt<EPI_RESID, false>(a, s); break;
-        case EPI_SILU: decode_mt<EPI_SILU, false>(a, s); break;
-        default: decode_mt<EPI_ARGMAX, false>(a, s); break;
+        case EPI_NONE: decode_mt<EPI_NONE, DN_NONE>(a, s); break;
+        case EPI_RESID: decode_mt<EPI_RESID, DN_NONE>(a, s); break;
+        case EPI_SILU: decode_mt<EPI_SILU, DN_NONE>(a, s); break;
+        default: decode_mt<EPI_ARGMAX, DN_NONE>(a, s); break;
       }
     }
     if (epi == EPI_ARGMAX) break;  // argmax requires M <= 64 (checked by the caller)
@@ -1859,7 +1446,7 @@ void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
 bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const RowNorm* norm,
                            const QkvEpilogue& e, hipStream_t s) {
   if (env_or("INFERD_FUSE_QKV_EPI", 1) == 0) return false;
-  if (gemm_tile_variant() != 8 || !gemm_uses_tiled(M, N, K, EPI_NONE) || !use_ring256(M, N, K, EPI_NONE)) return false;
+  if (!gemm_uses_tiled(M, N, K, EPI_NONE) || !use_w4(M, N, K, EPI_NONE)) return false;
   if (N != (e.H + 2 * e.KV) * HEAD_DIM) return false;
   const int gm = (M + 255) / 256, gn = N / 256;
   const int tiles = gm * gn, nK = K / 64;

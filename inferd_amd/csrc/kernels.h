@@ -51,26 +51,52 @@ void launch_decode_advance(int32_t* positions, int32_t* slots, int32_t* ctx_lens
 // packed weight holds 2N rows ([gate; up]).  For EPI_ARGMAX `partial` receives
 // (N/16) x M keys and `amax_keys` the per-row reduction (M <= 64).
 bool gemm_uses_tiled(int M, int N, int K, int epi);
-// Folded RMSNorm (epi NONE / SILU): Wp was packed with the norm weight folded in
-// (W[n][k] * w[k]); the GEMM reads the RAW activations and scales each output row by
-// rsqrt(mean(A_row^2) + eps) -- computed in-kernel from the A fragments on the decode path,
-// by a row kernel into rs_ws [M] floats on the tiled (prefill) path.
+// Folded RMSNorm (INFERD_NORM_FOLD=1, kept for A/B against the exact path): Wp was packed with
+// the norm weight folded in (W[n][k] * w[k]); the GEMM reads the RAW activations and scales
+// each output row by rsqrt(mean(A_row^2) + eps) -- computed in-kernel from the A fragments on
+// the decode path, by a row kernel into rs_ws [M] floats on the tiled (prefill) path.
 struct RowNorm {
   float eps;
   float* rs_ws;
 };
+// RMSNorm modes of the decode (M <= 64) GEMV
+enum { DN_NONE = 0, DN_FOLD = 1, DN_EXACT = 2 };
+// DN_EXACT: Qwen3RMSNorm at the reference's rounding points applied to A inside the GEMV,
+// A' = bf16(w * bf16(A * r)), r = 1 / sqrt(sum_p ssq_in[p * 64 + row] / K + eps): the row sums
+// of squares come from the kernel that produced A (launch_gemm's ssq_out on an EPI_RESID
+// GEMV, one partial per 16-column tile, n_parts = K / 16)
+struct DecodeNorm {
+  int mode;
+  float eps;
+  const float* ssq_in;
+  int n_parts;
+  const u16* w;
+};
+// Per-span GEMM workspace: the prefill tail split's fp32 partials and tickets, grown on
+// demand outside graph captures (one workspace per span, so spans on different streams never
+// share tickets).
+struct GemmWs {
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  unsigned* cnt = nullptr;
+  int cnt_n = 0;
+};
+void gemm_ws_free(GemmWs* w);
+// ssq_out (EPI_RESID, M <= 64): per 16-column tile sums of squares of the stored outputs,
+// [N/16][64] floats -- the DecodeNorm input of the next normed GEMV.
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
-                 const RowNorm* norm = nullptr);
-// decode q/k/v with K split over `kslices` (M <= 16, NORM folded): part [kslices][M][N] fp32,
-// ssq [kslices][M] fp32; the fused decode attention reduces them
+                 const RowNorm* fold = nullptr, GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr,
+                 float* ssq_out = nullptr);
 // prefill q/k/v projection fused with q/k RMSNorm + RoPE and the K/V cache write (the
 // persistent GEMM's epilogue); returns false, launching nothing, where that body does not
 // apply (the caller then runs launch_gemm + launch_qk_norm_rope_kv)
-bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const RowNorm* norm,
+bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const RowNorm* fold,
                            const QkvEpilogue& e, hipStream_t s);
+// decode q/k/v with K split over `kslices` (M <= 16): part [kslices][M][N] fp32 (and with
+// DN_FOLD ssq [kslices][M] fp32); the fused decode attention reduces them
 void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
-                                float* part, float* ssq, float eps, hipStream_t s);
+                                float* part, float* ssq, const DecodeNorm& norm, hipStream_t s);
 // rs[row] = 1 / sqrt(mean(x[row][:K]^2) + eps)
 void launch_row_inv_rms(const u16* x, int64_t ldx, int M, int K, float eps, float* rs, hipStream_t s);
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
@@ -95,15 +121,8 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 // launch_qk_norm_rope_kv + launch_attn_decode on the decode path): qkv is the raw
 // [M][(H+2KV)*128] projection output.
 // With `part` non-null the q/k/v come from launch_gemm_decode_partial's fp32 K-slices
-// (part [ksl][M][ldqkv], ssq [ksl][M], K = hidden) instead of the bf16 rows `qkv`.
-// Decode attention (fused q/k/v epilogue, split-K partials) and o_proj + residual in one
-// grid (attention.hip attn_o_decode_kernel; mode 2: attn_o_persist_kernel, one workgroup per
-// CU doing attention item i then o tile i); false = shape not covered, nothing launched.
-// chain: 3 zeroed u32 (done counters + error flag), left zero after every launch.
-bool launch_attn_o_decode_fused(const u16* qn_w, const u16* kn_w, const u16* cos_t, const u16* sin_t, float eps,
-                                u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out, float* ws,
-                                const float* part, const float* ssq, int ksl, int K, int64_t ldqkv, const u16* Wo,
-                                int N, u16* C, const u16* R, unsigned* chain, hipStream_t s, int mode);
+// (part [ksl][M][ldqkv], K = hidden) instead of the bf16 rows `qkv`; ssq [ksl][M] (folded
+// norm) scales their sum by rsqrt(sum ssq / K + eps), null means the slices were normed.
 void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
                               const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
                               float scale, u16* out, float* ws, hipStream_t s, const float* part = nullptr,

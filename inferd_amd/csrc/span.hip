@@ -95,7 +95,15 @@ struct InferdSpan {
       *last = nullptr;
   float* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
-  unsigned* chain = nullptr;  // attn_o_decode_kernel counters (3 u32, zero between launches)
+  // RMSNorm: exact (default; the reference's rounding points) or folded (INFERD_NORM_FOLD=1 at
+  // span creation, A/B).  Exact on the decode GEMV path (<= 64 rows): the o and down GEMVs
+  // write per-tile row sums of squares of their outputs (ssq_post / ssq_in, [hidden/16][64]),
+  // and the gate/up and next layer's q/k/v GEMVs normalise their A fragments from them;
+  // otherwise (a span's first layer, prefill) rmsnorm_kernel writes the normed rows to xn.
+  bool norm_fold = false;
+  float* ssq_in = nullptr;
+  float* ssq_post = nullptr;
+  GemmWs gws;              // prefill tail-split workspace (per span: spans never share tickets)
   float* rs_ws = nullptr;  // folded-norm row scales of the prefill GEMMs [max_tokens]
   float* qkv_part = nullptr;  // decode split-K q/k/v partials [QKV_KSL_MAX][16][qkv_rows]
   float* qkv_ssq = nullptr;   // and their row sums of squares [QKV_KSL_MAX][16]
@@ -111,6 +119,7 @@ struct InferdSpan {
   ~InferdSpan() {
     for (hipEvent_t e : prof_events) (void)hipEventDestroy(e);
     for (void* p : allocs) (void)hipFree(p);
+    gemm_ws_free(&gws);
   }
   // returns the pair index or -1
   long prof_begin(int cls, hipStream_t st) {
@@ -153,8 +162,14 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
     return fail(INFERD_ERR_ARG, "hidden % 128, intermediate % 64 and vocab % 16 must be 0");
   if (c.n_layers < 0 || c.max_tokens <= 0 || c.max_seqs <= 0 || c.kv_pages <= 0 || c.max_positions <= 0)
     return fail(INFERD_ERR_ARG, "bad span sizes");
+  if (c.has_lm_head && c.max_seqs > 64)
+    return fail(INFERD_ERR_ARG, "a span with lm_head takes max_seqs <= 64 (the greedy argmax is per call of <= 64 rows)");
   InferdSpan* s = new InferdSpan();
   s->cfg = c;
+  {
+    const char* e = getenv("INFERD_NORM_FOLD");
+    s->norm_fold = e && *e == '1';
+  }
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
   s->layers.resize(c.n_layers);
   int rc = 0;
@@ -218,8 +233,8 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
-  SALLOC(s->chain, 64);
-  if (hipMemset(s->chain, 0, 64) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
+  SALLOC(s->ssq_in, (size_t)(h / 16) * 64 * 4);
+  SALLOC(s->ssq_post, (size_t)(h / 16) * 64 * 4);
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
   SALLOC(s->rs_ws, (size_t)c.max_tokens * 4);
   SALLOC(s->qkv_part, (size_t)QKV_KSL_MAX * 16 * s->qkv_rows() * 4);
@@ -246,9 +261,11 @@ struct Target {
   uint32_t marks = 0;         // a norm weight: projections it makes stale
 };
 
+int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t);
+
 int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
   const InferdSpanConfig& c = s->cfg;
-  const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
+  const int h = c.hidden;
   if (layer < 0) {
     if (!strcmp(name, "embed_tokens") && s->embed) { *t = {s->embed, 0, c.vocab, h, T_EMBED}; return 0; }
     if (!strcmp(name, "norm") && s->final_norm) { *t = {s->final_norm, 0, 1, h, T_NORM}; return 0; }
@@ -256,6 +273,18 @@ int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
     return fail(INFERD_ERR_ARG, std::string("unknown/unowned global weight ") + name);
   }
   if (layer >= c.n_layers) return fail(INFERD_ERR_ARG, "layer index out of span");
+  const int rc = resolve_layer(s, layer, name, t);
+  if (!rc && !s->norm_fold) {  // exact norms: nothing is folded, no order between weights
+    t->fold = nullptr;
+    t->stale_bit = 0;
+    t->marks = 0;
+  }
+  return rc;
+}
+
+int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t) {
+  const InferdSpanConfig& c = s->cfg;
+  const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
   LayerW& L = s->layers[layer];
   const int64_t qrows = (int64_t)H * HEAD_DIM, kvrows = (int64_t)KV * HEAD_DIM;
   if (!strcmp(name, "q_proj")) { *t = {L.qkv, 1, qrows, h, T_Q, L.in_ln, STALE_Q}; return 0; }
@@ -380,13 +409,6 @@ static bool fuse_prefill_rope() {
   return e && *e == '1';
 }
 
-// INFERD_FUSE_ATTN_O=1: decode attention and o_proj in one grid (attn_o_decode_kernel);
-// =2: the persistent one-workgroup-per-CU form (attn_o_persist_kernel); 0 / unset: two launches
-static int fuse_attn_o() {
-  const char* e = getenv("INFERD_FUSE_ATTN_O");
-  return e && (*e == '1' || *e == '2') ? *e - '0' : 0;
-}
-
 static bool fuse_decode_rope() {
   const char* e = getenv("INFERD_FUSE_DECODE_ROPE");
   return !(e && *e == '0');
@@ -431,40 +453,54 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
                                         ": a projection was packed before its RMSNorm weight was set "
                                         "(set input_layernorm / post_attention_layernorm first, then re-set "
                                         "q/k/v_proj / gate/up_proj)");
-  // input_layernorm and post_attention_layernorm are folded into the qkv and gate/up GEMMs
+  // RMSNorms (qwen3_server_module.py:19-25, :173-176): see InferdSpan::norm_fold.  gemv: every
+  // projection of this call is a decode GEMV (<= 64 rows), so the o / down GEMVs can hand the
+  // next norm its row sums of squares.
+  const bool fold = s->norm_fold;
+  const bool gemv = M <= 64;
   const RowNorm rn = {c.rms_eps, s->rs_ws};
+  const RowNorm* rfold = fold ? &rn : nullptr;
+  const int n_parts = h / 16;
   long pe = -1;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
     u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
     const bool fused = b->decode && fuse_decode_rope();
     const int ksl = (fused && M <= 16) ? qkv_split(h) : 1;
+    // ---- input_layernorm -> q/k/v projection
+    const u16* a_in = x;
+    DecodeNorm dn = {fold ? (int)DN_FOLD : (int)DN_NONE, c.rms_eps, nullptr, 0, nullptr};
+    if (!fold) {
+      if (gemv && l > 0) {
+        dn = {DN_EXACT, c.rms_eps, s->ssq_in, n_parts, W.in_ln};
+      } else {
+        pe = s->prof_begin(PROF_NORM, st);
+        launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
+        s->prof_end(pe, st);
+        a_in = s->xn;
+      }
+    }
     pe = s->prof_begin(PROF_QKV, st);
     // prefill: q/k norm + RoPE and the K/V cache write in the projection's epilogue when
     // the persistent GEMM runs it (else the separate qk_norm_rope_kv launch below)
     bool qkv_done = false;
     if (ksl > 1) {
-      launch_gemm_decode_partial(x, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, s->qkv_ssq, c.rms_eps, st);
+      launch_gemm_decode_partial(a_in, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, fold ? s->qkv_ssq : nullptr, dn, st);
     } else {
       if (!b->decode && !fuse_prefill_rope()) {
         const QkvEpilogue qe = {b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t, s->sin_t, s->q, kv_l,
                                 H, KV, c.rms_eps};
-        qkv_done = launch_gemm_qkv_fused(x, h, W.qkv, M, qkvN, h, &rn, qe, st);
+        qkv_done = launch_gemm_qkv_fused(a_in, h, W.qkv, M, qkvN, h, rfold, qe, st);
       }
-      if (!qkv_done) launch_gemm(x, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &rn);
+      if (!qkv_done)
+        launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, rfold, &s->gws, &dn);
     }
     s->prof_end(pe, st);
-    bool o_done = false;
     if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
-      if (ksl > 1 && fuse_attn_o())
-        o_done = launch_attn_o_decode_fused(W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV, scale,
-                                            s->attn, s->attn_ws, s->qkv_part, s->qkv_ssq, ksl, h, qkvN, W.o, h,
-                                            s->h, x, s->chain, st, fuse_attn_o());
-      if (o_done) {
-      } else if (ksl > 1)
+      if (ksl > 1)
         launch_attn_decode_fused(nullptr, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
-                                 scale, s->attn, s->attn_ws, st, s->qkv_part, s->qkv_ssq, ksl, h);
+                                 scale, s->attn, s->attn_ws, st, s->qkv_part, fold ? s->qkv_ssq : nullptr, ksl, h);
       else
         launch_attn_decode_fused(s->qkv, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
                                  scale, s->attn, s->attn_ws, st);
@@ -489,18 +525,32 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
         launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
       s->prof_end(pe, st);
     }
-    // h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
-    if (!o_done) {
-      pe = s->prof_begin(PROF_O, st);
-      launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st);
-      s->prof_end(pe, st);
+    // ---- h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
+    pe = s->prof_begin(PROF_O, st);
+    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st, nullptr,
+                &s->gws, nullptr, (gemv && !fold) ? s->ssq_post : nullptr);
+    s->prof_end(pe, st);
+    // ---- post_attention_layernorm -> gate/up (+SwiGLU)
+    const u16* m_in = s->h;
+    DecodeNorm dm = {fold ? (int)DN_FOLD : (int)DN_NONE, c.rms_eps, nullptr, 0, nullptr};
+    if (!fold) {
+      if (gemv) {
+        dm = {DN_EXACT, c.rms_eps, s->ssq_post, n_parts, W.post_ln};
+      } else {
+        pe = s->prof_begin(PROF_NORM, st);
+        launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
+        s->prof_end(pe, st);
+        m_in = s->xn;
+      }
     }
     pe = s->prof_begin(PROF_GATEUP, st);
-    launch_gemm(s->h, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, &rn);
+    launch_gemm(m_in, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, rfold, &s->gws, &dm);
     s->prof_end(pe, st);
+    // ---- x = h1 + down(act)
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
     pe = s->prof_begin(PROF_DOWN, st);
-    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, st);
+    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, st, nullptr, &s->gws, nullptr,
+                (gemv && !fold) ? s->ssq_in : nullptr);
     s->prof_end(pe, st);
     x = out;
     if (layer_out)
@@ -574,7 +624,8 @@ extern "C" void inferd_graph_destroy(InferdGraph* g) { delete g; }
 
 extern "C" int inferd_span_error_flags(InferdSpan* s, int32_t* flags) {
   if (!s || !flags) return fail(INFERD_ERR_ARG, "null argument");
-  HIP_TRY(hipMemcpy(flags, s->err, 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(flags, s->err, 4, hipMemcpyDeviceToHost));  // synchronises the device
+  if (*flags) HIP_TRY(hipMemset(s->err, 0, 4));
   return INFERD_OK;
 }
 

@@ -50,6 +50,33 @@ MODELS = {
     "qwen3-32b": ModelDims("qwen3-32b", 5120, 25600, 64, 8, 64, 151936),
 }
 
+# Counter-based synthetic weights (the engine's inferd_weightgen; oracle/weightgen.py
+# defines the same values): tensor ids and (scale, center) per kind.
+LAYER_TENSOR_IDS = {"q_proj": 0, "k_proj": 1, "v_proj": 2, "o_proj": 3, "q_norm": 4, "k_norm": 5,
+                    "input_layernorm": 6, "post_attention_layernorm": 7, "gate_proj": 8, "up_proj": 9,
+                    "down_proj": 10}
+GLOBAL_TENSOR_IDS = {"embed_tokens": 0xFFFF0000, "norm": 0xFFFF0001, "lm_head": 0xFFFF0002}
+LINEAR_SCALE, NORM_SCALE = 0.034641016151377546, 0.1
+# "peaked" profile (oracle/weightgen.py documents it): embed * EMBED_BOOST and lm_head row
+# p(t) = (PERM_MUL * t + PERM_ADD) mod V gets LM_MIX * embed[t] added -- large top-1 logit
+# margins for greedy-parity runs; every layer weight is unchanged.
+EMBED_BOOST, LM_MIX = 64.0, 1.0
+PERM_MUL, PERM_ADD = 7919, 17
+
+
+def gen_tensor(seed: int, tid: int, shape, norm: bool, device) -> torch.Tensor:
+    """One synthetic weight tensor (bf16, row-major) generated on the device."""
+    lib = _lib.load()
+    n = 1
+    for s in shape:
+        n *= s
+    device = torch.device(device)
+    t = torch.empty(n, dtype=torch.bfloat16, device=device)
+    with torch.cuda.device(device):
+        _lib.check(lib.inferd_weightgen(t.data_ptr(), n, seed, tid, NORM_SCALE if norm else LINEAR_SCALE,
+                                        1.0 if norm else 0.0, torch.cuda.current_stream(device).cuda_stream))
+    return t.reshape(tuple(shape))
+
 
 class PagePool:
     """Free list over the span's KV pages (all layers of a span share page ids)."""
@@ -152,7 +179,8 @@ class DecodeGraph:
     def launch(self, stream=None):
         if self.launched >= self.n_steps:
             raise RuntimeError("decode graph ran out of reserved steps")
-        _lib.check(self.span.lib.inferd_graph_launch(self.graph, _lib.stream_ptr(stream)))
+        s = stream if stream is not None else torch.cuda.current_stream(self.span.device)
+        _lib.check(self.span.lib.inferd_graph_launch(self.graph, s.cuda_stream))
         self.launched += 1
         for st in self.states:
             st.length += 1
@@ -175,6 +203,8 @@ class SpanRuntime:
         self.first_layer, self.n_layers = first_layer, n_layers
         self.has_embed, self.has_lm_head = has_embed, has_lm_head
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.max_tokens, self.max_seqs = max_tokens, max_seqs
         self.max_positions = max_positions or dims.max_positions
         cfg = _lib.SpanConfig(hidden=dims.hidden, intermediate=dims.intermediate, heads=dims.heads,
@@ -197,17 +227,43 @@ class SpanRuntime:
             self.handle = None
 
     # ----------------------------------------------------------------- weights
-    def init_synthetic(self, seed: int):
+    def _stream(self):
+        return torch.cuda.current_stream(self.device)
+
+    def init_synthetic(self, seed: int, profile: str = "random"):
+        """Counter-based weights (the offline stand-in for a checkpoint).  profile="peaked"
+        re-composes embed / lm_head as oracle/weightgen.py's peaked profile (large greedy
+        margins for token-exact parity runs)."""
+        if profile not in ("random", "peaked"):
+            raise ValueError(f"unknown synthetic profile {profile!r}")
         with torch.cuda.device(self.device):
-            _lib.check(self.lib.inferd_span_init_synthetic(self.handle, seed, _lib.stream_ptr()))
+            _lib.check(self.lib.inferd_span_init_synthetic(self.handle, seed, self._stream().cuda_stream))
+            if profile == "peaked" and (self.has_embed or self.has_lm_head):
+                d = self.dims
+                emb = gen_tensor(seed, GLOBAL_TENSOR_IDS["embed_tokens"], (d.vocab, d.hidden), False,
+                                 self.device).float()
+                if self.has_embed:
+                    self.set_weight(-1, "embed_tokens", (emb * EMBED_BOOST).to(torch.bfloat16))
+                if self.has_lm_head:
+                    lm = gen_tensor(seed, GLOBAL_TENSOR_IDS["lm_head"], (d.vocab, d.hidden), False,
+                                    self.device).float()
+                    perm = (torch.arange(d.vocab, device=self.device, dtype=torch.int64) * PERM_MUL + PERM_ADD) \
+                        % d.vocab
+                    lm[perm] = lm[perm] + LM_MIX * emb
+                    self.set_weight(-1, "lm_head", lm.to(torch.bfloat16))
+                del emb
+            self._stream().synchronize()
 
     def set_weight(self, layer: int, name: str, w: torch.Tensor):
-        """layer: span-local index or -1 for embed_tokens / norm / lm_head."""
-        w = w.to(device=self.device, dtype=torch.bfloat16).contiguous()
-        rows, cols = (1, w.shape[0]) if w.dim() == 1 else tuple(w.shape)
-        _lib.check(self.lib.inferd_span_set_weight(self.handle, layer, name.encode(), w.data_ptr(),
-                                                   rows, cols, _lib.stream_ptr()))
-        torch.cuda.current_stream(self.device).synchronize()
+        """layer: span-local index or -1 for embed_tokens / norm / lm_head.  Packs on this
+        span's device and stream, then waits so the source tensor may be freed."""
+        with torch.cuda.device(self.device):
+            w = w.to(device=self.device, dtype=torch.bfloat16).contiguous()
+            rows, cols = (1, w.shape[0]) if w.dim() == 1 else tuple(w.shape)
+            s = self._stream()
+            _lib.check(self.lib.inferd_span_set_weight(self.handle, layer, name.encode(), w.data_ptr(),
+                                                       rows, cols, s.cuda_stream))
+            s.synchronize()
 
     def load_layer_state_dict(self, layer: int, sd: dict):
         """Keys as in Qwen3DecoderLayer (qwen3_server_module.py:165-176): self_attn.q_proj.weight ...
@@ -216,6 +272,19 @@ class SpanRuntime:
         items.sort(key=lambda kv: 0 if kv[0].endswith("norm") else 1)
         for leaf, v in items:
             self.set_weight(layer, leaf, v)
+
+    def check_errors(self):
+        """Read (and clear) the span's sticky device error flags; raise on any.  Bit 0: a
+        token id outside [0, vocab) reached the embedding gather (the reference's
+        nn.Embedding raises IndexError); bit 1: a decode graph ran past its reserved pages."""
+        import ctypes as C
+        f = C.c_int32(0)
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.inferd_span_error_flags(self.handle, C.byref(f)))
+        if f.value & 1:
+            raise IndexError("index out of range in self (token id outside the vocabulary)")
+        if f.value:
+            raise RuntimeError(f"span device error flags 0x{f.value:x} (decode slot overflow)")
 
     # ----------------------------------------------------------------- sessions
     def release(self, session_id):
@@ -239,9 +308,10 @@ class SpanRuntime:
     def run(self, batch, ids=None, x=None, hidden=None, next_ids=None, logits=None, layers=None, stream=None):
         """Launch one span forward on a prebuilt Batch with caller-owned device tensors
         (no host sync, no allocation).  Used by the pipeline runtime and the bench."""
+        s = stream if stream is not None else self._stream()
         _lib.check(self.lib.inferd_span_forward(self.handle, batch, _lib.ptr(ids), _lib.ptr(x), _lib.ptr(hidden),
                                                 _lib.ptr(next_ids), _lib.ptr(logits), _lib.ptr(layers),
-                                                _lib.stream_ptr(stream)))
+                                                s.cuda_stream))
 
     def profile_start(self, max_pairs: int = 1 << 16):
         _lib.check(self.lib.inferd_span_profile_start(self.handle, max_pairs))
@@ -262,56 +332,127 @@ class SpanRuntime:
         return st
 
     # ----------------------------------------------------------------- forward
+    def _plan(self, requests):
+        """Cut the requests into engine calls of <= max_tokens rows and <= max_seqs
+        sequences, in order: [[(request index, first row within it, rows)]].  A request
+        longer than what is left of a call continues in the next call (chunked prefill:
+        the chunk attends to the pages its earlier chunks wrote), so two pieces of one
+        sequence never share a call."""
+        calls, cur, cur_tok = [], [], 0
+        for i, (_, n) in enumerate(requests):
+            done = 0
+            while done < n:
+                if len(cur) == self.max_seqs or cur_tok == self.max_tokens:
+                    calls.append(cur)
+                    cur, cur_tok = [], 0
+                take = min(n - done, self.max_tokens - cur_tok)
+                cur.append((i, done, take))
+                cur_tok += take
+                done += take
+        if cur:
+            calls.append(cur)
+        return calls
+
     @torch.no_grad()
     def forward(self, requests, ids: torch.Tensor | None = None, x: torch.Tensor | None = None, *,
                 want_hidden: bool = True, want_next_ids: bool = False, want_logits: bool = False,
                 want_layers: bool = False) -> dict:
         """requests: list of (session_id or None, n_new_tokens), tokens concatenated in order.
-        ids: int tensor [M] (first span); x: bf16 [M, hidden] (other spans)."""
+        ids: int tensor [M] (first span); x: bf16 [M, hidden] (other spans).  A session-less
+        request is a stateless recompute from position 0 whose pages are released afterwards.
+        Calls larger than the span's workspace (max_tokens rows / max_seqs sequences) run as
+        several engine calls, long sequences chunk by chunk through their own pages."""
         d = self.dims
-        temp = []
-        seqs = []
-        for sid, n in requests:
-            if sid is None:
-                st = SeqState()
-                temp.append(st)
-            else:
-                st = self.sessions.setdefault(sid, SeqState())
-            self._reserve(st, n)
-            seqs.append((st, n))
-        try:
-            batch, keep = self.build_batch(seqs)
-            M, B = batch.n_tokens, batch.n_seqs
-            dev = self.device
-            ids_d = None
+        dev = self.device
+        if not requests or any(n <= 0 for _, n in requests):
+            raise ValueError("forward needs at least one request with n_new_tokens >= 1")
+        sids = [sid for sid, _ in requests if sid is not None]
+        if len(set(sids)) != len(sids):
+            raise ValueError("a session may appear only once per forward call")
+        total = sum(n for _, n in requests)
+        with torch.cuda.device(dev):
+            ids_d = x_d = None
             if self.has_embed:
+                if ids is None:
+                    raise ValueError("first span needs token ids")
                 ids_d = ids.to(device=dev, dtype=torch.int32).reshape(-1).contiguous()
-                assert ids_d.numel() == M
-            x_d = None
-            if not self.has_embed:
-                x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(M, d.hidden).contiguous()
-            out = {}
-            hid = torch.empty((M, d.hidden), dtype=torch.bfloat16, device=dev) if want_hidden else None
-            nid = torch.empty((B,), dtype=torch.int32, device=dev) if (want_next_ids and self.has_lm_head) else None
-            lg = torch.empty((B, d.vocab), dtype=torch.bfloat16, device=dev) if (want_logits and self.has_lm_head) else None
-            lay = torch.empty((self.n_layers, M, d.hidden), dtype=torch.bfloat16, device=dev) if want_layers else None
-            with torch.cuda.device(dev):
-                _lib.check(self.lib.inferd_span_forward(self.handle, batch, _lib.ptr(ids_d), _lib.ptr(x_d),
-                                                        _lib.ptr(hid), _lib.ptr(nid), _lib.ptr(lg),
-                                                        _lib.ptr(lay), _lib.stream_ptr()))
-            for st, n in seqs:
-                st.length += n
-            if hid is not None:
-                out["hidden"] = hid
-            if nid is not None:
-                out["next_ids"] = nid
-            if lg is not None:
-                out["logits"] = lg
-            if lay is not None:
-                out["layers"] = lay
-            out["_keep"] = (keep, ids_d, x_d)
-            return out
-        finally:
-            for st in temp:
-                self.pool.free(st.pages)
-                st.pages = []
+                if ids_d.numel() != total:
+                    raise ValueError(f"{ids_d.numel()} ids for {total} request tokens")
+                lo, hi = torch.aminmax(ids_d)
+                if int(lo) < 0 or int(hi) >= d.vocab:     # nn.Embedding's IndexError (reference :48)
+                    raise IndexError("index out of range in self (token id outside the vocabulary)")
+            else:
+                if x is None:
+                    raise ValueError("span needs hidden states x")
+                x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(total, d.hidden).contiguous()
+            temp = []
+            states = []
+            for sid, _ in requests:
+                if sid is None:
+                    st = SeqState()
+                    temp.append(st)
+                else:
+                    st = self.sessions.setdefault(sid, SeqState())
+                states.append(st)
+            try:
+                for st, (_, n) in zip(states, requests):
+                    self._reserve(st, n)
+                B = len(requests)
+                lm = self.has_lm_head
+                hid = torch.empty((total, d.hidden), dtype=torch.bfloat16, device=dev) if want_hidden else None
+                nid = torch.empty((B,), dtype=torch.int32, device=dev) if (want_next_ids and lm) else None
+                lg = torch.empty((B, d.vocab), dtype=torch.bfloat16, device=dev) if (want_logits and lm) else None
+                lay = torch.empty((self.n_layers, total, d.hidden), dtype=torch.bfloat16, device=dev) \
+                    if want_layers else None
+                row0 = [0]
+                for _, n in requests:
+                    row0.append(row0[-1] + n)
+                calls = self._plan(requests)
+                keep = []
+                for call in calls:
+                    r0 = row0[call[0][0]] + call[0][1]
+                    m = sum(t for _, _, t in call)
+                    single = len(calls) == 1
+                    batch, bkeep = self.build_batch([(states[i], t) for i, _, t in call])
+                    keep.append(bkeep)
+                    finals = [j for j, (i, s0, t) in enumerate(call) if s0 + t == requests[i][1]]
+                    c_nid = nid if single else (torch.empty((len(call),), dtype=torch.int32, device=dev)
+                                                if nid is not None and finals else None)
+                    c_lg = lg if single else (torch.empty((len(call), d.vocab), dtype=torch.bfloat16, device=dev)
+                                              if lg is not None and finals else None)
+                    c_lay = lay if single else (torch.empty((self.n_layers, m, d.hidden), dtype=torch.bfloat16,
+                                                            device=dev) if lay is not None else None)
+                    self.run(batch, ids=None if ids_d is None else ids_d[r0:r0 + m],
+                             x=None if x_d is None else x_d[r0:r0 + m],
+                             hidden=None if hid is None else hid[r0:r0 + m], next_ids=c_nid, logits=c_lg,
+                             layers=c_lay)
+                    for i, _, t in call:
+                        states[i].length += t
+                    if not single:
+                        if finals:
+                            dst = torch.tensor([call[j][0] for j in finals], device=dev)
+                            src = torch.tensor(finals, device=dev)
+                            if c_nid is not None:
+                                nid[dst] = c_nid[src]
+                            if c_lg is not None:
+                                lg[dst] = c_lg[src]
+                        if c_lay is not None:
+                            lay[:, r0:r0 + m] = c_lay
+                        keep.append((c_nid, c_lg, c_lay))
+            finally:
+                for st in temp:
+                    self.pool.free(st.pages)
+                    st.pages = []
+        out = {}
+        if hid is not None:
+            out["hidden"] = hid
+        if nid is not None:
+            out["next_ids"] = nid
+        if lg is not None:
+            out["logits"] = lg
+        if lay is not None:
+            out["layers"] = lay
+        # batch descriptors and inputs stay referenced until the caller is done with the
+        # outputs (the launches are stream-ordered, nothing here synchronises)
+        out["_keep"] = (keep, ids_d, x_d)
+        return out

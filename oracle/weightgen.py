@@ -58,24 +58,50 @@ def tensor_key(seed: int, tid: int) -> int:
     return int(splitmix64(x)[0])
 
 
-def uniform_fp32(seed: int, tid: int, n: int, scale: float, center: float = 0.0,
-                 offset: int = 0) -> np.ndarray:
-    """fp32 values w(offset .. offset+n-1) as defined in the module docstring."""
-    key = np.uint64(tensor_key(seed, tid))
+def _uniform_chunk(key, scale, center, offset, n, out):
     idx = np.arange(offset, offset + n, dtype=np.uint64)
     with np.errstate(over="ignore"):
         z = splitmix64(idx + key)
     u24 = (z >> np.uint64(40)).astype(np.float32)
     t = u24 * np.float32(2.0 ** -23) - np.float32(1.0)          # exact
     w = (t * np.float32(scale)).astype(np.float32)              # one rounding
-    w = (w + np.float32(center)).astype(np.float32)             # one rounding
-    return w
+    out[:] = (w + np.float32(center)).astype(np.float32)        # one rounding
+
+
+_CHUNK = 1 << 22
+
+
+def _threads() -> int:
+    import os
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16, int(os.environ.get("OMP_NUM_THREADS", n))))
+
+
+def uniform_fp32(seed: int, tid: int, n: int, scale: float, center: float = 0.0,
+                 offset: int = 0) -> np.ndarray:
+    """fp32 values w(offset .. offset+n-1) as defined in the module docstring (large
+    tensors are generated in independent chunks on a thread pool: numpy releases the GIL)."""
+    key = np.uint64(tensor_key(seed, tid))
+    out = np.empty(n, dtype=np.float32)
+    starts = range(0, n, _CHUNK)
+    if n <= _CHUNK or _threads() == 1:
+        for s in starts:
+            _uniform_chunk(key, scale, center, offset + s, min(_CHUNK, n - s), out[s:s + _CHUNK])
+        return out
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(_threads()) as ex:
+        list(ex.map(lambda s: _uniform_chunk(key, scale, center, offset + s, min(_CHUNK, n - s),
+                                             out[s:s + _CHUNK]), starts))
+    return out
 
 
 def bf16_rne_bits(x: np.ndarray) -> np.ndarray:
     """fp32 -> bf16 bit pattern (uint16), round-to-nearest-even (finite inputs)."""
-    u = x.astype(np.float32).view(np.uint32).astype(np.uint64)
-    r = (u + np.uint64(0x7FFF) + ((u >> np.uint64(16)) & np.uint64(1))) >> np.uint64(16)
+    u = x.astype(np.float32).view(np.uint32)
+    r = (u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) >> np.uint32(16)
     return r.astype(np.uint16)
 
 
@@ -93,3 +119,24 @@ def gen_tensor_bf16_bits(seed: int, tid: int, shape, name: str) -> np.ndarray:
     scale, center = tensor_spec(name)
     n = int(np.prod(shape))
     return bf16_rne_bits(uniform_fp32(seed, tid, n, scale, center)).reshape(shape)
+
+
+# "peaked" profile (greedy-parity runs, SURVEY §7 "Hard parts"): random weights give top-1
+# logit margins of a few bf16 ulps, so a bf16 rounding difference anywhere in the span
+# flips ties.  The peaked profile keeps every layer weight and adds a token-transition
+# structure on top of the embedding / lm_head:
+#     embed'[t]      = embed[t] * EMBED_BOOST                       (exact: power of two)
+#     lm_head'[p(t)] = bf16(fp32(lm_head[p(t)]) + LM_MIX * fp32(embed[t]))
+#     p(t)           = (PERM_MUL * t + PERM_ADD) mod V                (a bijection of the vocab)
+# so the residual stream carries its token and lm_head row p(t) lines up with it: the
+# greedy chain walks t -> p(t) -> ... with a margin far above the bf16 error bound, while
+# the layers still add their full (random) contribution to every logit.  The HIP side
+# composes the same values (inferd_amd/runtime.py SpanRuntime.init_synthetic).
+EMBED_BOOST = 64.0
+LM_MIX = 1.0
+PERM_MUL, PERM_ADD = 7919, 17
+
+
+def peaked_perm(vocab: int) -> np.ndarray:
+    """p(t) for t = 0..vocab-1."""
+    return (np.arange(vocab, dtype=np.int64) * PERM_MUL + PERM_ADD) % vocab
