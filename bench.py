@@ -54,7 +54,6 @@ def parse():
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-layers", type=int, default=2, help="layers timed by the CPU baseline sample")
-    p.add_argument("--cpu-steps", type=int, default=3)
     p.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing pass")
     p.add_argument("--profile-steps", type=int, default=8, help="eager event-instrumented decode steps")
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
@@ -171,43 +170,99 @@ def step_bytes(d, n_layers: int, B: int, ctx_mean: float, lm_head: bool) -> floa
 
 
 # ------------------------------------------------------------------ CPU baseline
-def cpu_baseline(d_name: str, B: int, ctx: int, seed: int, n_layers_sample: int, n_steps: int) -> dict:
-    """Oracle (`port`) decode on the host cores: a bounded sample of `n_layers_sample`
-    Qwen3-8B layers x `n_steps` decode steps at B x ctx (KV cache pre-filled with random
-    bf16 K/V: the decode-step cost does not depend on the cached values), plus the
-    lm_head once; tokens/s extrapolated to the full 36-layer model."""
-    from oracle import qwen3_ref as R
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _cpu_threads() -> int:
     threads = len(os.sched_getaffinity(0))
-    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    return min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+
+
+def _median_time(fn, warmup: int = 2, reps: int = 5) -> float:
+    """BASELINE.md's CPU measurement plan: 2 warm-up runs, then the median of 5."""
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def cpu_baseline(d_name: str, B: int, ctx: int, seed: int, n_layers_sample: int) -> dict:
+    """Oracle (`port`) decode on the host cores: a bounded sample of `n_layers_sample`
+    Qwen3-8B layers, one decode step of B sequences at context ctx (KV cache pre-filled with
+    random bf16 K/V: the step's cost does not depend on the cached values; the cache is
+    reset to ctx tokens before every run), 2 warm-ups + median of 5, plus the final norm +
+    lm_head the same way; tokens/s extrapolated to the full 36-layer model."""
+    from oracle import qwen3_ref as R
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     d = R.CONFIGS[d_name]
     sp = R.RefSpan(d, seed, 0, n_layers_sample - 1, False, False, torch.bfloat16, "sdpa")
     g = torch.Generator().manual_seed(0)
-    caches = []
-    for _ in range(n_layers_sample):
-        c = R.LayerCache()
-        c.k = torch.randn((B, d.kv_heads, ctx, d.head_dim), generator=g).to(torch.bfloat16)
-        c.v = torch.randn((B, d.kv_heads, ctx, d.head_dim), generator=g).to(torch.bfloat16)
-        caches.append(c)
-    sp.sessions["bench"] = caches
+    kv = [((torch.randn((B, d.kv_heads, ctx, d.head_dim), generator=g)).to(torch.bfloat16),
+           (torch.randn((B, d.kv_heads, ctx, d.head_dim), generator=g)).to(torch.bfloat16))
+          for _ in range(n_layers_sample)]
     x = torch.randn((B, 1, d.hidden), generator=g).to(torch.bfloat16)
-    sp.forward_cached("bench", x)   # warm-up (1 step)
-    t0 = time.perf_counter()
-    for _ in range(n_steps):
+
+    def step():
+        caches = []
+        for k, v in kv:
+            c = R.LayerCache()
+            c.k, c.v = k, v
+            caches.append(c)
+        sp.sessions["bench"] = caches
         sp.forward_cached("bench", x)
-    t_layers = (time.perf_counter() - t0) / n_steps / n_layers_sample
+    t_layers = _median_time(step) / n_layers_sample
     gw = R.gen_global_weights(d, seed)
-    hn = R.rms_norm(x[:, -1], gw["norm"], d.eps)
-    torch.nn.functional.linear(hn, gw["lm_head"])
-    t0 = time.perf_counter()
-    torch.argmax(torch.nn.functional.linear(R.rms_norm(x[:, -1], gw["norm"], d.eps), gw["lm_head"]), -1)
-    t_head = time.perf_counter() - t0
+    t_head = _median_time(lambda: torch.argmax(torch.nn.functional.linear(
+        R.rms_norm(x[:, -1], gw["norm"], d.eps), gw["lm_head"]), -1))
     t_step = t_layers * d.layers + t_head
     return {"value": round(B / t_step, 3), "unit": "tokens/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/qwen3_ref.py bf16 on {threads} host threads: {n_layers_sample} Qwen3-8B layers x "
-                      f"{n_steps} decode steps at B={B}, ctx={ctx} (random KV) + lm_head once; "
-                      f"{t_layers * 1e3:.1f} ms/layer-step extrapolated to {d.layers} layers "
-                      f"({t_step:.2f} s/step)"}
+            "cpu": _cpu_model(),
+            "sample": f"oracle/qwen3_ref.py bf16 on {threads} host threads ({_cpu_model()}): {n_layers_sample} "
+                      f"Qwen3-8B layers, one decode step of B={B} at ctx={ctx} (random KV), 2 warm-ups + median of 5 "
+                      f"= {t_layers * 1e3:.1f} ms/layer; lm_head {t_head * 1e3:.1f} ms; extrapolated to {d.layers} "
+                      f"layers = {t_step:.2f} s/step"}
+
+
+def cpu_config1(seed: int, steps: int = 16) -> dict:
+    """BASELINE config 1 end to end on the host: Qwen3-0.6B as two 14-layer spans (the
+    oracle's restatement of the reference's FirstStage / LastStage), greedy decode of a
+    32-token prompt with the petals protocol's full recompute every step
+    (send_message.py:46-60), bf16; 2 warm-up steps, then `steps` timed steps."""
+    from oracle import qwen3_ref as R
+    threads = _cpu_threads()
+    torch.set_num_threads(threads)
+    d = R.CONFIGS["qwen3-0.6b"]
+    b0 = R.RefSpan(d, seed, 0, 13, True, False, torch.bfloat16, "sdpa")
+    b1 = R.RefSpan(d, seed, 14, 27, False, True, torch.bfloat16, "sdpa")
+    ids = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(11)).tolist()
+
+    def one(ids):
+        return int(torch.argmax(b1.forward(b0.forward(torch.tensor([ids])))[0, -1]))
+    for _ in range(2):
+        one(ids)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ids = ids + [one(ids)]
+    dt = time.perf_counter() - t0
+    return {"value": round(steps / dt, 3), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "cpu": _cpu_model(),
+            "sample": f"config 1: Qwen3-0.6B, 2 spans (14+14 layers), greedy, 32-token prompt, {steps} steps of "
+                      f"full recompute (T = 32..{31 + steps}), bf16, 2 warm-up steps"}
 
 
 # ------------------------------------------------------------------ main
@@ -218,7 +273,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     # INFERD_DIST_BACKEND=gloo (rehearsal on a box with fewer GPUs than ranks: ranks share
     # devices round-robin and the stage hand-offs go through host memory); default RCCL
     backend = os.environ.get("INFERD_DIST_BACKEND", "nccl")
@@ -232,6 +288,17 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+
+    ranks = [{"rank": rank, "local_rank": local_rank, "device": f"cuda:{dev_index}",
+              "name": torch.cuda.get_device_name(dev_index)}]
+    if dist:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, ranks[0])
+        ranks = gathered
+        if rank == 0:
+            print(f"bench.py: {world} ranks over {dist.get_backend()} ("
+                  f"{'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()}): "
+                  + ", ".join(f"rank {r['rank']} -> {r['device']}" for r in ranks), file=sys.stderr, flush=True)
 
     from inferd_amd import pipeline as P
     from inferd_amd.runtime import MODELS
@@ -355,10 +422,13 @@ def main():
             "prefill": {"tokens": n_mb * B * ctx, "seconds": round(t_prefill, 3),
                         "tokens_per_s": round(n_mb * B * ctx / t_prefill, 1)},
             "cpu_baseline": None,
+            "ranks": ranks if world > 1 else None,
+            "backend": None if not dist else dist.get_backend(),
         }
         if world == 1 and not args.no_cpu_baseline:
             st.release()
-            out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers, args.cpu_steps)
+            out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)
+            out["cpu_baseline_config1"] = cpu_config1(args.seed)
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

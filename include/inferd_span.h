@@ -106,12 +106,13 @@ int inferd_span_init_synthetic(InferdSpan* span, uint64_t seed, void* stream);
  * state-dict leaf names (qwen3_server_module.py:101-124, :169-176):
  * q_proj k_proj v_proj o_proj q_norm k_norm input_layernorm post_attention_layernorm
  * gate_proj up_proj down_proj | embed_tokens norm lm_head.  Projections are packed into
- * the device fragment layout (fused [q;k;v] and [gate;up]).  input_layernorm is folded
- * into q/k/v_proj and post_attention_layernorm into gate/up_proj at pack time
- * (W[n][k] * w[k]; the GEMM scales rows by rsqrt(mean(x^2) + eps)), so a layer's norm
- * weight must be set BEFORE the projections that consume it; re-setting a norm weight
- * marks those projections stale and forward returns INFERD_ERR_STATE until they are set
- * again. */
+ * the device fragment layout (fused [q;k;v] and [gate;up]).  The RMSNorms run at the
+ * reference's rounding points (bf16(w * bf16(x * rsqrt(mean(x^2) + eps)))), so weights may
+ * be set in any order.  Only a span created with INFERD_NORM_FOLD=1 (A/B builds of the
+ * folded norm: input_layernorm folded into q/k/v_proj and post_attention_layernorm into
+ * gate/up_proj at pack time, W[n][k] * w[k]) needs a layer's norm weight set BEFORE the
+ * projections that consume it: there re-setting a norm weight marks those projections
+ * stale and forward returns INFERD_ERR_STATE until they are set again. */
 int inferd_span_set_weight(InferdSpan* span, int32_t layer, const char* name,
                            const void* src, int64_t rows, int64_t cols, void* stream);
 
@@ -130,6 +131,12 @@ int inferd_span_forward(InferdSpan* span, const InferdBatch* batch, const int32_
                         const void* x_in, void* x_out, int32_t* next_ids, void* logits,
                         void* layer_out, void* stream);
 
+/* Final norm + lm_head over `rows` rows of bf16 hidden states x -> bf16 logits [rows][vocab]
+ * (LastStage.forward returns logits for all T positions, partitioned_models.py:95-96;
+ * inferd_span_forward computes the last row of each sequence only).  Last span only,
+ * rows <= max_tokens. */
+int inferd_span_lm_head(InferdSpan* span, const void* x, int32_t rows, void* logits, void* stream);
+
 /* Decode graphs.  Captures one span forward of `batch` (same arguments as
  * inferd_span_forward) into a HIP graph.  With advance = 1 the graph starts with a
  * device-side scheduler step: for every sequence b the new token goes to position
@@ -145,7 +152,10 @@ int inferd_span_graph_capture(InferdSpan* span, const InferdBatch* batch, int32_
                               void* stream, InferdGraph** out);
 int inferd_graph_launch(InferdGraph* graph, void* stream);
 void inferd_graph_destroy(InferdGraph* graph);
-/* Sticky device error flags (bit 0: token id out of range, bit 1: decode slot overflow). */
+/* Sticky device error flags, read and cleared (synchronises the device).  Bit 0: a token id
+ * outside [0, vocab) reached the embedding gather (it reads row 0 instead; the reference's
+ * nn.Embedding raises IndexError, so the Python host validates ids before the launch);
+ * bit 1: a decode graph ran past the pages reserved for it. */
 int inferd_span_error_flags(InferdSpan* span, int32_t* flags);
 
 /* Per-kernel-class timing: HIP events recorded on the launch stream around every kernel of

@@ -572,6 +572,21 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   return INFERD_OK;
 }
 
+// Final norm + lm_head over every row of x (LastStage.forward's logits over all T positions,
+// partitioned_models.py:95-96); inferd_span_forward computes them for the last rows only.
+extern "C" int inferd_span_lm_head(InferdSpan* s, const void* x, int32_t rows, void* logits, void* stream) {
+  if (!s || !x || !logits || rows <= 0) return fail(INFERD_ERR_ARG, "bad lm_head args");
+  const InferdSpanConfig& c = s->cfg;
+  if (!c.has_lm_head) return fail(INFERD_ERR_ARG, "span has no lm_head");
+  if (rows > c.max_tokens) return fail(INFERD_ERR_ARG, "rows > max_tokens");
+  hipStream_t st = (hipStream_t)stream;
+  launch_rmsnorm((const u16*)x, c.hidden, nullptr, 0, s->final_norm, s->xn, c.hidden, rows, c.hidden, c.rms_eps, st);
+  launch_gemm(s->xn, c.hidden, s->lm_head, rows, c.vocab, c.hidden, (u16*)logits, c.vocab, nullptr, 0, EPI_NONE,
+              nullptr, st, nullptr, &s->gws);
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
 // ------------------------------------------------------------------ decode graphs
 struct InferdGraph {
   hipGraph_t graph = nullptr;
@@ -714,8 +729,10 @@ extern "C" int inferd_gemm(const void* a, const void* w, void* c, const void* r,
   if (!a || !w || !c || m <= 0 || n % 16 || k % 32) return fail(INFERD_ERR_ARG, "gemm needs n%16==0, k%32==0");
   if (epi < 0 || epi > 2) return fail(INFERD_ERR_ARG, "bad epilogue");
   if (epi == INFERD_EPI_RESID && !r) return fail(INFERD_ERR_ARG, "resid epilogue needs R");
+  // the op API's own tail-split workspace (per host thread; spans keep theirs)
+  static thread_local GemmWs op_ws;
   launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr,
-              (hipStream_t)stream);
+              (hipStream_t)stream, nullptr, &op_ws);
   LAUNCH_CHECK();
   return INFERD_OK;
 }

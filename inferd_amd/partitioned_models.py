@@ -15,20 +15,26 @@ Differences, all on purpose:
   * the stage modules own a SpanRuntime (HIP kernels through the C-ABI) instead of HF
     decoder layers; compute is bf16 on the GPU and there is no CPU fallback;
   * the codec also carries bf16 (dtype "bfloat16", raw 16-bit words) -- the reference's
-    `.numpy()` raises on bf16 (SURVEY §8 a15);  fp32 payloads keep the reference format;
+    `.numpy()` raises on bf16;  fp32 payloads keep the reference format, and
+    INFERD_WIRE_DTYPE=float32 makes a GPU stage emit fp32 for a stock reference node
+    downstream (partitioned_models.py:20-26 cannot decode bf16);
   * the decoder mask argument is accepted for API compatibility but not materialised:
     causality is implicit in the attention kernels (partitioned_models.py:139-143 only
     ever builds a full causal mask with positions 0..T-1);
   * parts_path is a stage file written by inferd_amd.split_model (safetensors, loaded
     with a loader that executes nothing) or "synthetic:<seed>" for the counter-based
-    weights; the reference's pickled `torch.save(module)` (split_model.py:107) needs
-    `weights_only=False` and is not loaded.
+    weights; the reference's pickled `torch.save(module)` (split_model.py:107) is converted
+    once by `python -m inferd_amd.convert_parts` (an inert unpickler: nothing in the file
+    runs) instead of being loaded;
+  * an optional "session_id" in the input dict keeps K/V per sequence on every stage
+    (PartitionedQwen2 docstring); without it the protocol is the reference's, unchanged.
 """
 from __future__ import annotations
 
 import base64
 import json
 import os
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -73,13 +79,14 @@ def build_decoder_attention_mask(attn_mask_2d: torch.Tensor) -> torch.Tensor:
 # ------------------------------------------------------------------ stage modules
 class _Stage:
     """Common part of the three stage modules: a SpanRuntime and the reference's
-    forward(model_in, decoder_attn_mask, position_ids) contract (batch 1 rows per
-    sequence, full recompute from the given positions)."""
+    forward(model_in, decoder_attn_mask, position_ids) contract (full recompute from
+    position 0 of B sequences of T rows)."""
 
     first = last = False
 
     def __init__(self, span: SpanRuntime):
         self.span = span
+        self.last_next_ids = self.last_logits = None
 
     def to(self, *a, **k):
         return self
@@ -90,25 +97,37 @@ class _Stage:
     def __call__(self, *a, **k):
         return self.forward(*a, **k)
 
-    def _run(self, model_in, position_ids):
+    def forward(self, model_in, decoder_attn_mask=None, position_ids=None):
         B, T = model_in.shape[0], model_in.shape[1]
         if position_ids is not None:
             pos = position_ids.reshape(-1, T)[0].tolist()
             if pos != list(range(T)):
                 raise ValueError("stage modules recompute from position 0 (partitioned_models.py:139-143); "
-                                 "use Qwen3Server.send for cached positions")
-        reqs = [(None, T)] * B
-        kw = dict(want_hidden=not self.last, want_logits=self.last, want_next_ids=self.last)
+                                 "use Qwen3Server.send or a session_id for cached positions")
+        out = self.run([(None, T)] * B, model_in, all_logits=True)
+        return out.reshape(B, T, -1)
+
+    def run(self, requests, model_in, all_logits=False, want_hidden=None):
+        """requests: [(session key or None, new rows)] over the rows of model_in (ids (1,M) /
+        (M,) on the first span, hidden (.., M, h) otherwise).  Returns the hidden rows (M, h),
+        or on the last span the logits: (M, V) with all_logits, else the last row of each
+        request (n, V); greedy ids of those last rows land in self.last_next_ids."""
+        kw = {}
         if self.first:
-            out = self.span.forward(reqs, ids=model_in.reshape(-1), **kw)
+            kw["ids"] = model_in.reshape(-1)
         else:
-            out = self.span.forward(reqs, x=model_in.reshape(B * T, -1), **kw)
-        if self.last:
-            # greedy ids from the engine's own argmax (bf16 logits, lowest index on ties,
-            # = torch.argmax at partitioned_models.py:162)
-            self.last_next_ids = out["next_ids"]
-            return out["logits"].reshape(B, 1, -1)   # last position only (see LastStage)
-        return out["hidden"].reshape(B, T, -1)
+            kw["x"] = model_in.reshape(-1, self.span.dims.hidden)
+        if not self.last:
+            return self.span.forward(requests, want_hidden=True, **kw)["hidden"]
+        out = self.span.forward(requests, want_hidden=all_logits, want_logits=not all_logits, want_next_ids=True,
+                                **kw)
+        # greedy ids from the engine's own argmax (bf16 logits, lowest index on ties,
+        # = torch.argmax at partitioned_models.py:162)
+        self.last_next_ids = out["next_ids"]
+        if not all_logits:
+            self.last_logits = out["logits"]
+            return out["logits"]
+        return self.span.lm_head(out["hidden"])
 
 
 class FirstStage(_Stage):
@@ -121,43 +140,47 @@ class StageInner(_Stage):
 
 
 class LastStage(_Stage):
-    """partitioned_models.py:78-97: hidden (B,T,h) -> logits.  The reference computes
-    lm_head over all T rows and then uses only the last (:96, :162); this returns the
-    last row's logits as (B,1,V), which is everything `forward` consumes."""
+    """partitioned_models.py:78-97: hidden (B,T,h) -> logits (B,T,V) (final norm + lm_head on
+    every row, as the reference).  PartitionedQwen2.forward needs only the last row and calls
+    `run`, which computes that row alone."""
     last = True
 
 
 class FirstLastStage(_Stage):
-    """A single span holding the whole model (ids -> last-row logits)."""
+    """A single span holding the whole model (ids -> logits)."""
     first = last = True
-
-    def forward(self, model_in, decoder_attn_mask=None, position_ids=None):
-        return self._run(model_in, position_ids)
-
-
-for _cls in (FirstStage, StageInner, LastStage):
-    _cls.forward = lambda self, model_in, decoder_attn_mask=None, position_ids=None: self._run(model_in, position_ids)
 
 
 # ------------------------------------------------------------------ stage files
+def _span_kwargs():
+    """Workspace of a node's span: max_tokens rows per engine call (longer prompts run in
+    chunks through their own pages), a KV pool for a full-length prompt
+    (MAX_POSITION_EMBEDDINGS = 40960, qwen3_config.py:14) plus sessions."""
+    return dict(kv_pages=int(os.environ.get("INFERD_KV_PAGES", 1024)),
+                max_tokens=int(os.environ.get("INFERD_MAX_TOKENS", 4096)), max_seqs=64)
+
+
 def load_stage(parts_path: str, model_name: str, num_stages: int, stage: int, device) -> _Stage:
     """Build the stage module of `parts_path`:
-      * "synthetic:<seed>[:<model>:<start>:<end>]" -- counter-based weights (no checkpoint)
+      * "synthetic:<seed>[:<model>:<start>:<end>[:<profile>]]" -- counter-based weights (no
+        checkpoint); profile "peaked" = the large-margin embed / lm_head of oracle/weightgen.py
       * a .safetensors stage file written by inferd_amd.split_model (metadata: model dims,
         start/end layer, roles)."""
     if parts_path.startswith("synthetic:"):
         bits = parts_path.split(":")
         seed = int(bits[1])
-        dims = MODELS[bits[2] if len(bits) > 2 else _model_key(model_name)]
+        dims = MODELS[bits[2] if len(bits) > 2 and bits[2] else _model_key(model_name)]
         if len(bits) > 4:
             start, end = int(bits[3]), int(bits[4])
         else:
             per = dims.layers // num_stages
             start = stage * per
             end = dims.layers - 1 if stage == num_stages - 1 else start + per - 1
+        profile = bits[5] if len(bits) > 5 else "random"
         first, last = stage == 0, stage == num_stages - 1
-        span = SpanRuntime(dims, start, end - start + 1, has_embed=first, has_lm_head=last, device=device)
-        span.init_synthetic(seed)
+        span = SpanRuntime(dims, start, end - start + 1, has_embed=first, has_lm_head=last, device=device,
+                           **_span_kwargs())
+        span.init_synthetic(seed, profile)
         return _make_stage(span, first, last)
     from safetensors import safe_open
     with safe_open(parts_path, framework="pt", device="cpu") as f:
@@ -165,9 +188,9 @@ def load_stage(parts_path: str, model_name: str, num_stages: int, stage: int, de
         dims = ModelDims(**json.loads(meta["dims"]))
         start, end = int(meta["start_layer"]), int(meta["end_layer"])
         first, last = meta["first"] == "1", meta["last"] == "1"
-        span = SpanRuntime(dims, start, end - start + 1, has_embed=first, has_lm_head=last, device=device)
-        # norm weights first: the span folds them into the projections packed after them
-        for key in sorted(f.keys(), key=lambda k: 0 if k.endswith("norm.weight") else 1):
+        span = SpanRuntime(dims, start, end - start + 1, has_embed=first, has_lm_head=last, device=device,
+                           **_span_kwargs())
+        for key in f.keys():
             t = f.get_tensor(key)
             if key.startswith("layers."):
                 _, j, *rest = key.split(".")
@@ -189,6 +212,8 @@ def _model_key(model_name: str) -> str:
     for k in ("32b", "8b", "0.6b"):
         if k in n:
             return f"qwen3-{k}"
+    if n in MODELS:
+        return n
     return "qwen3-0.6b"
 
 
@@ -212,7 +237,22 @@ def _load_tokenizer(model_name):
 
 # ------------------------------------------------------------------ node-facing API
 class PartitionedQwen2:
-    """partitioned_models.py:102-168 -- same constructor, same forward(dict) -> dict."""
+    """partitioned_models.py:102-168 -- same constructor, same forward(dict) -> dict.
+
+    Stateless (the reference's protocol, unchanged): every call recomputes the whole
+    sequence from position 0 (send_message.py:46-60 resends all generated ids).
+
+    Session-cached (optional): an input dict that carries "session_id" keeps
+    that sequence's K/V on every stage, so a step costs O(new tokens) instead of O(T):
+      * stage 0 still receives the full `generated_ids` (the client loop is unchanged); it
+        runs only the ids past the ones it has cached for the session (a list that does not
+        extend the cached prefix restarts the session);
+      * hidden_meta then carries only the new rows, plus "session_id" and "past_len" (the
+        position of its first row) for the next stage, which appends them to its own pages;
+      * {"session_id": s, "close_session": True} releases the session along the chain.
+    Sessions beyond `max_sessions` (INFERD_MAX_SESSIONS, default 64) or a full KV pool evict
+    the least recently used one (the reference's session caches are never freed,
+    qwen3_server_module.py:220)."""
 
     def __init__(self, model_name: str, num_stages: int, stage: int, parts_path: str):
         self.stage = stage
@@ -220,10 +260,18 @@ class PartitionedQwen2:
         self.parts_path = parts_path
         if not torch.cuda.is_available():
             raise RuntimeError("PartitionedQwen2 (inferd_amd) runs on an MI355X GPU; no CPU path")
-        self.device = torch.device("cuda")
+        self.device = torch.device("cuda", torch.cuda.current_device())
         if stage == 0 or stage == num_stages - 1:
             self.tokenizer = _load_tokenizer(model_name)
         self.model = load_stage(parts_path, model_name, num_stages, stage, self.device)
+        self.span = self.model.span
+        self.wire_dtype = os.environ.get("INFERD_WIRE_DTYPE", _BF16)
+        self.max_sessions = int(os.environ.get("INFERD_MAX_SESSIONS", 64))
+        self._sessions = OrderedDict()   # session_id -> ids cached (stage 0) / rows cached
+
+    @property
+    def _last(self):
+        return self.stage == self.num_stages - 1
 
     def _prepare_inputs(self, input_data):
         """partitioned_models.py:119-137."""
@@ -236,23 +284,95 @@ class PartitionedQwen2:
                 return ids.reshape(-1).tolist(), ids
             if "generated_ids" in input_data:
                 lst = input_data["generated_ids"]
+                if isinstance(lst, int):          # a 1-token prompt arrives as an int (:124,:128)
+                    lst = [lst]
                 return lst, torch.tensor([lst], dtype=torch.long)
         if "hidden_meta" in input_data:
             hidden = base64_to_tensor(input_data["hidden_meta"])
             return input_data.get("generated_ids"), hidden
         raise RuntimeError(f"Bad input for stage {self.stage}: {input_data!r}")
 
+    def _encode(self, hidden):
+        return tensor_to_base64(hidden.float() if self.wire_dtype == "float32" else hidden)
+
+    def _output(self, out, gen_ids, rows, extra):
+        if not self._last:
+            res = {"hidden_meta": self._encode(out.reshape(1, rows, -1))}
+            if self.stage == 0:
+                res["generated_ids"] = gen_ids
+            res.update(extra)
+            return res
+        token_id = int(self.model.last_next_ids[0].item())
+        res = {"next_token_id": token_id, "next_token_str": self.tokenizer.decode(token_id),
+               "generated_ids": list(gen_ids if gen_ids is not None else []) + [token_id]}
+        res.update(extra)
+        return res
+
     def forward(self, inputs: dict) -> dict:
         """partitioned_models.py:145-168 (same output schema)."""
+        if isinstance(inputs, dict) and "session_id" in inputs:
+            return self._forward_session(inputs)
         gen_ids, model_in = self._prepare_inputs(inputs)
         T = model_in.size(1)
-        pos = torch.arange(T).unsqueeze(0)
         with torch.no_grad():
-            out = self.model(model_in, None, pos)
-        if self.stage < self.num_stages - 1:
-            if self.stage == 0:
-                return {"hidden_meta": tensor_to_base64(out), "generated_ids": gen_ids}
-            return {"hidden_meta": tensor_to_base64(out)}
-        token_id = int(self.model.last_next_ids[0].item())
-        return {"next_token_id": token_id, "next_token_str": self.tokenizer.decode(token_id),
-                "generated_ids": list(gen_ids) + [token_id]}
+            out = self.model.run([(None, T)], model_in)
+        self.span.check_errors()
+        return self._output(out, gen_ids, T, {})
+
+    # ---------------------------------------------------------------- sessions
+    def _touch(self, sid, value):
+        self._sessions[sid] = value
+        self._sessions.move_to_end(sid)
+        while len(self._sessions) > self.max_sessions:
+            old, _ = self._sessions.popitem(last=False)
+            self.span.release(("sess", old))
+
+    def close_session(self, sid):
+        self._sessions.pop(sid, None)
+        self.span.release(("sess", sid))
+
+    def _forward_session(self, inputs):
+        sid = inputs["session_id"]
+        if inputs.get("close_session"):
+            self.close_session(sid)
+            return {"session_id": sid, "close_session": True} if not self._last else \
+                {"session_id": sid, "closed": True}
+        gen_ids, model_in = self._prepare_inputs(inputs)
+        key = ("sess", sid)
+        cached = self.span.sessions.get(key)
+        past = 0 if cached is None else cached.length
+        if self.stage == 0:
+            seen = self._sessions.get(sid)
+            ids = model_in.reshape(-1).tolist()
+            if seen is None or past != len(seen) or ids[:past] != seen or len(ids) <= past:
+                self.close_session(sid)        # not a continuation: restart from position 0
+                past = 0
+            new = model_in[:, past:]
+        else:
+            first_pos = int(inputs.get("past_len", 0))
+            if first_pos != past:
+                if first_pos != 0:
+                    raise RuntimeError(f"session {sid!r}: hidden rows start at position {first_pos} but "
+                                       f"this stage has {past} cached")
+                self.close_session(sid)
+                past = 0
+            new = model_in
+        n = new.shape[1]
+        with torch.no_grad():
+            for attempt in range(self.max_sessions + 1):
+                try:
+                    out = self.model.run([(key, n)], new)
+                    break
+                except RuntimeError as e:
+                    if "KV pool exhausted" not in str(e) or not self._evict_other(sid):
+                        raise
+        self.span.check_errors()
+        self._touch(sid, (model_in.reshape(-1).tolist() if self.stage == 0 else past + n))
+        return self._output(out, gen_ids, n, {"session_id": sid, "past_len": past})
+
+    def _evict_other(self, sid):
+        for old in list(self._sessions):
+            if old != sid:
+                self.close_session(old)
+                return True
+        return False

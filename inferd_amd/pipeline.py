@@ -192,10 +192,13 @@ class PipelineStage:
 
     # ------------------------------------------------------------------ prefill
     @torch.no_grad()
-    def prefill(self, prompts):
+    def prefill(self, prompts, capture=None):
         """prompts: per microbatch an int tensor [B, T] (read on the first stage only).
         Runs every microbatch's prompt through the pipeline in chunks of prefill_chunk
-        sequences; leaves the first decode ids of every microbatch on stage 0."""
+        sequences; leaves the first decode ids of every microbatch on stage 0.  `capture`
+        (a dict, non-last stages): receives this stage's output for the first chunk of
+        microbatch 0 -- its sequences 0 .. prefill_chunk-1, [chunk * T, h] -- as a CPU copy
+        (the stage-boundary hidden state parity tests compare with the oracle)."""
         S, T = self.S, prompts[0].shape[1]
         items = [(m, c) for m in range(self.n_mb) for c in range(0, self.B, self.prefill_chunk)]
         h = self.dims.hidden
@@ -227,6 +230,8 @@ class PipelineStage:
                     ids_parts[(m, c)] = out
                 else:
                     bufs_out[i_cur] = out
+                    if capture is not None and i_cur == 0:
+                        capture["hidden"] = out.cpu()
         if self.last:
             for m in range(self.n_mb):
                 first_ids[m] = torch.cat([ids_parts[(m, c)] for c in range(0, self.B, self.prefill_chunk)])

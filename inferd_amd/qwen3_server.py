@@ -16,8 +16,11 @@ Arguments the GPU path derives itself:
 `cache_position` must continue the session's cached length; anything else raises
 (the reference would silently concatenate onto the cache).
 
-Unlike the reference, sessions can be released (`release(session_id)`), and
-`max_sessions` evicts the least recently used one when the pool would overflow.
+Sessions are keyed exactly as the reference keys its caches, `None` included (ProcessLayer
+maps an empty id to None, server.py:39, and every None call then shares that cache).
+Unlike the reference, sessions can be released (`release(session_id)`), and `max_sessions`
+evicts the least recently used one (a later call that continues an evicted session fails
+its cache_position check).
 """
 from __future__ import annotations
 
@@ -47,8 +50,9 @@ class Qwen3Server:
             self.load_layer_files(weights)
 
     def load_layer_files(self, pattern: str):
-        """Per-layer state dicts `layer_XX.pt` (qwen3_server_module.py:227-235), loaded with
-        weights_only=True; `pattern` contains `{idx:02d}`."""
+        """Per-layer state dicts `layer_XX.pt` (qwen3_server_module.py:227-235: the HF-hub
+        files of Qwen3Config.HF_REPO_ID), loaded with weights_only=True (nothing in the file
+        executes); `pattern` contains `{idx:02d}`, e.g. "/ckpt/layer_{idx:02d}.pt"."""
         for j, i in enumerate(range(self.start_layer, self.end_layer + 1)):
             sd = torch.load(pattern.format(idx=i), map_location="cpu", weights_only=True)
             self.span.load_layer_state_dict(j, sd)
@@ -57,9 +61,14 @@ class Qwen3Server:
     def session_caches(self):
         return self.span.sessions
 
+    def _keys(self, session_id, B):
+        # the reference keys DynamicCache by session_id -- None included: ProcessLayer maps an
+        # empty id to None (server.py:39) and defaultdict caches under it (:220, :253)
+        return [("srv", session_id, b) for b in range(B)]
+
     def release(self, session_id):
-        for key in [k for k in self.span.sessions
-                    if k == session_id or (isinstance(k, tuple) and len(k) == 2 and k[0] == session_id)]:
+        for key in [k for k in self.span.sessions if isinstance(k, tuple) and len(k) == 3 and k[0] == "srv"
+                    and k[1] == session_id]:
             self.span.release(key)
         self._lru.pop(session_id, None)
 
@@ -68,8 +77,8 @@ class Qwen3Server:
         """qwen3_server_module.py:237-255: hidden (B,T,h) -> hidden (B,T,h) through the span,
         appending T tokens to each of the B rows' caches of `session_id`."""
         B, T, h = hidden_states.shape
-        sids = [session_id] if B == 1 else [(session_id, b) for b in range(B)]
-        st = self.span.sessions.get(sids[0])
+        keys = self._keys(session_id, B)
+        st = self.span.sessions.get(keys[0])
         past = 0 if st is None else st.length
         if cache_position is not None:
             cp = torch.as_tensor(cache_position).reshape(-1).tolist()
@@ -81,5 +90,6 @@ class Qwen3Server:
             self.release(old)
         self._lru[session_id] = True
         self._lru.move_to_end(session_id)
-        out = self.span.forward([(sid, T) for sid in sids], x=hidden_states.reshape(B * T, h))
+        out = self.span.forward([(k, T) for k in keys], x=hidden_states.reshape(B * T, h))
+        self.span.check_errors()
         return out["hidden"].reshape(B, T, h)

@@ -331,6 +331,21 @@ class SpanRuntime:
         self._reserve(st, n_tokens)
         return st
 
+    @torch.no_grad()
+    def lm_head(self, hidden: torch.Tensor) -> torch.Tensor:
+        """Final norm + lm_head over every row of `hidden` (bf16 [rows, vocab]), in chunks of
+        max_tokens rows -- LastStage's all-position logits (partitioned_models.py:95-96)."""
+        d = self.dims
+        with torch.cuda.device(self.device):
+            x = hidden.to(device=self.device, dtype=torch.bfloat16).reshape(-1, d.hidden).contiguous()
+            out = torch.empty((x.shape[0], d.vocab), dtype=torch.bfloat16, device=self.device)
+            s = self._stream()
+            for r0 in range(0, x.shape[0], self.max_tokens):
+                n = min(self.max_tokens, x.shape[0] - r0)
+                _lib.check(self.lib.inferd_span_lm_head(self.handle, x[r0].data_ptr(), n, out[r0].data_ptr(),
+                                                        s.cuda_stream))
+        return out
+
     # ----------------------------------------------------------------- forward
     def _plan(self, requests):
         """Cut the requests into engine calls of <= max_tokens rows and <= max_seqs

@@ -24,3 +24,8 @@ def gpu_available():
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_sessionfinish(session, exitstatus):
+    from parity_log import write
+    write(ROOT)

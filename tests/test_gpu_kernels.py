@@ -137,15 +137,16 @@ def test_gemm_swiglu(lib, M, K):
     assert (bf16_ulp_diff(c.cpu(), ref.cpu()) > 2).float().mean() < 2e-3
 
 
-@pytest.mark.parametrize("variant", ["ring", "w4", "w4mg", "w4p", "256", "128"])
+@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 192), (777, 768, 1088), (2048, 1024, 4096), (1300, 256, 640),
-                                   (4096, 2048, 1024), (8092, 4096, 448)])
-def test_gemm_prefill_variants(lib, monkeypatch, variant, M, N, K):
-    """Every prefill GEMM body (INFERD_GEMM_TILE) on ragged M, short and long K, all epilogues.
-    (2048, 1024, 4096) and (4096, 2048, 1024) run the tail split (K cut 8 / 2 ways);
-    (8092, 4096, 448): 512 whole tiles, so the persistent w4p walks two tiles per workgroup
-    (ragged last row block, cross-tile prefetch, exact-count epilogue waits)."""
-    monkeypatch.setenv("INFERD_GEMM_TILE", variant)
+                                   (4096, 2048, 1024), (8092, 4096, 448), (300, 384, 1024)])
+def test_gemm_prefill_bodies(lib, monkeypatch, split, M, N, K):
+    """The prefill GEMM bodies on ragged M, short and long K, all epilogues: persistent
+    gemm_w4p; gemm_w4 with the tail split ((2048, 1024, 4096) and (4096, 2048, 1024) cut K
+    8 / 2 ways; INFERD_GEMM_SPLIT=0 runs them whole on w4p); (8092, 4096, 448): 512 whole
+    tiles, so w4p walks two tiles per workgroup (ragged last row block, cross-tile prefetch,
+    exact-count epilogue waits); (300, 384, 1024): the 128x128 gemm_tiled."""
+    monkeypatch.setenv("INFERD_GEMM_SPLIT", split)
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.03).to(torch.bfloat16)
@@ -276,10 +277,8 @@ def test_attention_decode(lib, H, KV):
 
 
 @pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2), (64, 8)])
-@pytest.mark.parametrize("variant", ["4", "8"])
-def test_attention_prefill(lib, monkeypatch, H, KV, variant):
-    """Both prefill kernels (8-wave staggered, 4-wave) on ragged prompts, with and without
-    cached prefixes, including a 700-token prompt (several 256-row blocks, > 4 pages)."""
-    monkeypatch.setenv("INFERD_ATTN_PREFILL", variant)
+def test_attention_prefill(lib, H, KV):
+    """The 4-wave prefill kernel on ragged prompts, with and without cached prefixes,
+    including a 700-token prompt (several 128-row blocks, > 4 pages)."""
     err, ref = _attn_case(lib, H, KV, [1, 17, 64, 130, 700], [0, 5, 0, 200, 61], seed=H + 1)
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()

@@ -1,0 +1,516 @@
+"""Parity of the HIP span engine against the oracle and the reference's golden vectors, at the
+BASELINE configs and through every boundary the reference exposes; every measured error,
+margin and greedy step lands in the parity record (tests/parity_log.py).
+
+Tolerances (asserted per tensor):
+  * bf16 hidden states / logits: max|got - ref| <= TOL_REL * max|ref| against the oracle with
+    the same attention semantics (SDPA), TOL_REL_EAGER against the gRPC golden (the
+    reference's eager attention rounds scores to bf16; the kernels keep them in fp32);
+  * greedy tokens: identical on every step; with the "peaked" synthetic profile (large top-1
+    margins, oracle/weightgen.py) free-running, and every step's oracle margin must exceed
+    twice the measured logit error, so the agreement is not luck; with plain random weights
+    (margins of a few bf16 ulps) the steps are teacher-forced and recorded, and agreement is
+    asserted where the margin exceeds twice the measured logit error.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import load, tensor
+from oracle import qwen3_ref as R
+from parity_log import errs, record
+
+pytestmark = pytest.mark.gpu
+
+SEED = 1234
+DEV = "cuda"
+TOL_REL = 2e-2
+TOL_REL_EAGER = 3e-2
+
+
+def _pq(model, n_stages, stage, start, end, profile="random"):
+    from inferd_amd.partitioned_models import PartitionedQwen2
+    return PartitionedQwen2(model, n_stages, stage, f"synthetic:{SEED}:{model}:{start}:{end}:{profile}")
+
+
+@pytest.fixture(scope="module")
+def q06_peaked():
+    """BASELINE config 1 as two PartitionedQwen2 nodes (layers 0-13, 14-27), peaked profile,
+    and the oracle's two spans on the same weights."""
+    d = R.CONFIGS["qwen3-0.6b"]
+    n0, n1 = _pq("qwen3-0.6b", 2, 0, 0, 13, "peaked"), _pq("qwen3-0.6b", 2, 1, 14, 27, "peaked")
+    b0 = R.RefSpan(d, SEED, 0, 13, True, False, torch.bfloat16, "sdpa", profile="peaked")
+    b1 = R.RefSpan(d, SEED, 14, 27, False, True, torch.bfloat16, "sdpa", profile="peaked")
+    return n0, n1, b0, b1
+
+
+def _hidden(meta):
+    from inferd_amd.partitioned_models import base64_to_tensor
+    return base64_to_tensor(meta)
+
+
+# ------------------------------------------------------------------ RMSNorm: exact vs folded
+@pytest.mark.parametrize("golden,cfg", [("q06_layer.npz", "qwen3-0.6b"), ("q8b_layer.npz", "qwen3-8b")])
+def test_norm_exact_vs_folded(monkeypatch, golden, cfg):
+    """The span's RMSNorms at the reference rounding points (default) against the folded A/B
+    path (INFERD_NORM_FOLD=1), on the reference's own Qwen3Server.send outputs (prefill +
+    cached decode calls) and the oracle (SDPA) on the same inputs."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    g = load(golden)
+    start = int(g["start"])
+    d = R.CONFIGS[cfg]
+    n_dec = sum(1 for k in g.files if k.startswith("bf16_in_dec"))
+    ins = [tensor(g["bf16_in_prefill"])] + [tensor(g[f"bf16_in_dec{i}"]) for i in range(n_dec)]
+    res = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("INFERD_NORM_FOLD", mode)
+        s = SpanRuntime(MODELS[cfg], start, 1, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8,
+                        max_tokens=64, max_seqs=4, max_positions=1024)
+        s.init_synthetic(SEED)
+        oracle = R.RefSpan(d, SEED, start, start, False, False, torch.bfloat16, "sdpa")
+        rows = []
+        for i, x in enumerate(ins):
+            B, T = x.shape[0], x.shape[1]
+            out = s.forward([(f"s{b}", T) for b in range(B)], x=x.reshape(B * T, -1))["hidden"].reshape(B, T, -1)
+            ref = torch.cat([oracle.forward_cached(f"s{b}", x[b:b + 1]) for b in range(B)])
+            e_or, e_gold = errs(out, ref), errs(out, tensor(g[f"bf16_out{i}"]))
+            rows.append({"call": i, "rows": T, "vs_oracle": e_or, "vs_golden_eager": e_gold})
+            assert e_or["max_norm"] < TOL_REL and e_gold["max_norm"] < TOL_REL_EAGER, (mode, i, e_or, e_gold)
+        res["folded" if mode == "1" else "exact"] = rows
+        del s
+    worst = {k: max(r["vs_oracle"]["max_norm"] for r in v) for k, v in res.items()}
+    rms = {k: max(r["vs_oracle"]["rms_rel"] for r in v) for k, v in res.items()}
+    print(f"{golden}: worst max_norm exact {worst['exact']:.2e} folded {worst['folded']:.2e}; "
+          f"rms_rel exact {rms['exact']:.2e} folded {rms['folded']:.2e}")
+    record(f"norm_exact_vs_folded[{cfg}]", **res)
+
+
+# ------------------------------------------------------------------ greedy parity, config 1
+def test_config1_free_running_greedy_peaked(q06_peaked):
+    """BASELINE config 1 (Qwen3-0.6B as two 14-layer spans, 32-token prompt) behind the
+    node-facing dict protocol, 16 FREE-RUNNING greedy steps of full recompute
+    (send_message.py:46-60): each side feeds back its own tokens; identical ids on every
+    step, every oracle margin above twice the measured logit error."""
+    n0, n1, b0, b1 = q06_peaked
+    d = R.CONFIGS["qwen3-0.6b"]
+    prompt = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(11)).tolist()
+    gpu_ids, ref_ids = list(prompt), list(prompt)
+    steps = []
+    for step in range(16):
+        o0 = n0.forward({"generated_ids": gpu_ids})
+        o1 = n1.forward(o0)
+        h_ref = b0.forward(torch.tensor([ref_ids]))
+        lg_ref = b1.forward(h_ref)[0, -1]
+        rid, margin = int(torch.argmax(lg_ref)), R.top2_margin(lg_ref)
+        e_h = errs(_hidden(o0["hidden_meta"])[0], h_ref[0])
+        e_lg = errs(n1.model.last_logits[0], lg_ref)
+        steps.append({"step": step, "gpu": o1["next_token_id"], "ref": rid, "margin": margin,
+                      "logit_err": e_lg, "boundary_hidden_err": e_h})
+        print(f"step {step}: gpu {o1['next_token_id']} ref {rid} margin {margin:.3f} "
+              f"logit max_abs {e_lg['max_abs']:.3f} boundary max_norm {e_h['max_norm']:.2e}")
+        assert o1["next_token_id"] == rid, step
+        assert margin > 2 * e_lg["max_abs"], (step, margin, e_lg)
+        assert e_h["max_norm"] < TOL_REL
+        gpu_ids = o1["generated_ids"]
+        ref_ids = ref_ids + [rid]
+    assert gpu_ids == ref_ids
+    record("config1_free_running_peaked", agree=16, steps=steps)
+
+
+def test_config1_teacher_forced_random_weights():
+    """The same chain on plain random weights (margins of a few bf16 ulps), 16 teacher-forced
+    steps: recorded per step; ids must agree wherever the oracle margin exceeds twice the
+    measured logit error."""
+    d = R.CONFIGS["qwen3-0.6b"]
+    n0, n1 = _pq("qwen3-0.6b", 2, 0, 0, 13), _pq("qwen3-0.6b", 2, 1, 14, 27)
+    b0 = R.RefSpan(d, SEED, 0, 13, True, False, torch.bfloat16, "sdpa")
+    b1 = R.RefSpan(d, SEED, 14, 27, False, True, torch.bfloat16, "sdpa")
+    ids = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(11)).tolist()
+    steps, agree, checked = [], 0, 0
+    for step in range(16):
+        o1 = n1.forward(n0.forward({"generated_ids": ids}))
+        lg = b1.forward(b0.forward(torch.tensor([ids])))[0, -1]
+        rid, m = int(torch.argmax(lg)), R.top2_margin(lg)
+        e_lg = errs(n1.model.last_logits[0], lg)
+        ok = o1["next_token_id"] == rid
+        agree += int(ok)
+        if m > 2 * e_lg["max_abs"]:
+            checked += 1
+            assert ok, (step, m, e_lg)
+        steps.append({"step": step, "gpu": o1["next_token_id"], "ref": rid, "margin": m, "logit_err": e_lg})
+        ids = ids + [rid]
+    print(f"random weights: {agree}/16 agree; {checked} steps above the measured error bound")
+    record("config1_teacher_forced_random", agree=agree, checked=checked, steps=steps)
+
+
+# ------------------------------------------------------------------ f1: sessions at /nn_forward
+def test_nn_forward_session_cache_matches_full_recompute(q06_peaked):
+    """The optional session_id at the node API: stage 0 runs only the ids past its cached
+    prefix, hidden_meta carries the new rows, stage 1 appends them to its pages; the greedy
+    ids equal the stateless full-recompute chain's over 16 steps, and closing the session
+    frees every page."""
+    n0, n1, _, _ = q06_peaked
+    d = R.CONFIGS["qwen3-0.6b"]
+    prompt = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(12)).tolist()
+    ids, full, full_h = list(prompt), [], []
+    for _ in range(16):
+        o0 = n0.forward({"generated_ids": ids})
+        full_h.append(_hidden(o0["hidden_meta"])[0, -1])
+        o1 = n1.forward(o0)
+        full.append(o1["next_token_id"])
+        ids = o1["generated_ids"]
+    free0, free1 = n0.span.pool.n_free, n1.span.pool.n_free
+    ids, cached, worst = list(prompt), [], 0.0
+    for step in range(16):
+        o0 = n0.forward({"generated_ids": ids, "session_id": "s1"})
+        h = _hidden(o0["hidden_meta"])
+        assert h.shape[1] == (32 if step == 0 else 1) and o0["past_len"] == (0 if step == 0 else 31 + step)
+        worst = max(worst, errs(h[0, -1], full_h[step])["max_norm"])
+        o1 = n1.forward(o0)
+        assert o1["session_id"] == "s1"
+        cached.append(o1["next_token_id"])
+        ids = o1["generated_ids"]
+    print(f"session chain: last-row hidden vs full recompute worst max_norm {worst:.2e}")
+    assert cached == full
+    assert worst < TOL_REL
+    # a request that does not extend the cached prefix restarts the session
+    o1 = n1.forward(n0.forward({"generated_ids": prompt, "session_id": "s1"}))
+    assert o1["next_token_id"] == full[0]
+    c = n1.forward(n0.forward({"session_id": "s1", "close_session": True}))
+    assert c == {"session_id": "s1", "closed": True}
+    assert n0.span.pool.n_free == free0 and n1.span.pool.n_free == free1
+    record("nn_forward_session_vs_full", steps=16, identical=True, last_row_hidden_worst_max_norm=worst)
+
+
+def test_nn_forward_long_prompt_chunked(q06_peaked):
+    """A 4500-token prompt (> the 4096-row engine call) through the node API, stateless and
+    with a session: chunked prefill through the sequence's own pages; the greedy id and the
+    stage-boundary rows around the chunk seam agree with the oracle's one-shot forward."""
+    n0, n1, b0, b1 = q06_peaked
+    d = R.CONFIGS["qwen3-0.6b"]
+    T = 4500
+    ids = torch.randint(0, d.vocab, (T,), generator=torch.Generator().manual_seed(13)).tolist()
+    o0 = n0.forward({"generated_ids": ids})
+    o1 = n1.forward(o0)
+    os0 = n0.forward({"generated_ids": ids, "session_id": "long"})
+    os1 = n1.forward(os0)
+    h_ref = b0.forward(torch.tensor([ids]))
+    lg = b1.forward(h_ref)[0, -1]
+    rid = int(torch.argmax(lg))
+    h = _hidden(o0["hidden_meta"])[0]
+    rows = list(range(4080, 4112)) + list(range(T - 32, T))
+    e = errs(h[rows], h_ref[0, rows])
+    print(f"T={T}: gpu {o1['next_token_id']} / session {os1['next_token_id']} ref {rid} margin "
+          f"{R.top2_margin(lg):.3f}; boundary rows max_norm {e['max_norm']:.2e}")
+    assert o1["next_token_id"] == rid and os1["next_token_id"] == rid
+    assert e["max_norm"] < TOL_REL
+    n1.forward(n0.forward({"session_id": "long", "close_session": True}))
+    record("nn_forward_long_prompt", tokens=T, boundary_rows_err=e, token_ok=True)
+
+
+def test_stage_modules_all_positions_and_bad_ids(q06_peaked):
+    """LastStage.forward returns logits for every position (B,T,V), as the reference
+    (partitioned_models.py:95-96); an out-of-range token id raises IndexError as
+    nn.Embedding does, and the node keeps working."""
+    n0, n1, b0, b1 = q06_peaked
+    ids = torch.tensor([[5, 77, 1234, 151935, 42, 9]])
+    h = n0.model(ids, None, torch.arange(6)[None])
+    lg = n1.model(h, None, torch.arange(6)[None])
+    assert lg.shape == (1, 6, 151936)
+    ref = b1.forward(b0.forward(ids))
+    e = errs(lg[0], ref[0])
+    assert e["max_norm"] < TOL_REL, e
+    with pytest.raises(IndexError):
+        n0.forward({"generated_ids": [1, 2, 151936]})
+    with pytest.raises(IndexError):
+        n0.forward({"generated_ids": [-1, 2]})
+    o = n1.forward(n0.forward({"generated_ids": [5, 77, 1234]}))
+    assert o["next_token_id"] == int(torch.argmax(b1.forward(b0.forward(torch.tensor([[5, 77, 1234]])))[0, -1]))
+    record("stage_modules_all_positions", logits_err=e)
+
+
+def test_span_forward_chunks_match_one_call():
+    """SpanRuntime.forward cuts calls larger than its workspace (max_tokens rows, max_seqs
+    sequences) into engine calls, long sequences chunk by chunk through their pages: the
+    hidden rows, per-layer captures and last-row logits agree with one large call."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["tiny"]
+    reqs = [(None, 150), ("a", 30), ("b", 70), (None, 9), ("c", 1)]
+    M = sum(n for _, n in reqs)
+    ids = torch.randint(0, d.vocab, (M,), generator=torch.Generator().manual_seed(3))
+    outs = []
+    for mt, ms in ((1024, 64), (64, 2)):
+        s = SpanRuntime(d, 0, d.layers, has_embed=True, has_lm_head=True, device=DEV, kv_pages=64,
+                        max_tokens=mt, max_seqs=ms, max_positions=2048)
+        s.init_synthetic(SEED)
+        o = s.forward(reqs, ids=ids, want_hidden=True, want_logits=True, want_next_ids=True, want_layers=True)
+        outs.append({k: v.cpu() for k, v in o.items() if k != "_keep"})
+    e_h, e_l, e_y = errs(outs[1]["hidden"], outs[0]["hidden"]), errs(outs[1]["layers"], outs[0]["layers"]), \
+        errs(outs[1]["logits"], outs[0]["logits"])
+    print(f"chunked vs one call: hidden {e_h['max_norm']:.2e} layers {e_l['max_norm']:.2e} logits {e_y['max_norm']:.2e}")
+    assert e_h["max_norm"] < TOL_REL and e_l["max_norm"] < TOL_REL and e_y["max_norm"] < TOL_REL
+    record("span_forward_chunked", hidden=e_h, layers=e_l, logits=e_y)
+
+
+# ------------------------------------------------------------------ BASELINE config 5 at T = 8192
+@pytest.mark.timeout(600)
+def test_config5_q32b_layer_prefill_8192():
+    """One Qwen3-32B layer prefilling the bench's full 8192-token prompt (persistent 4-wave
+    GEMMs, the o/down tail split over 640 tiles, the 4-wave prefill attention over 128 pages):
+    the last 256 rows, which attend over the whole prefix, against the oracle."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = R.CONFIGS["qwen3-32b"]
+    T, tail, layer = 8192, 256, 9
+    s = SpanRuntime(MODELS["qwen3-32b"], layer, 1, has_embed=False, has_lm_head=False, device=DEV,
+                    kv_pages=T // 64 + 2, max_tokens=T, max_seqs=1, max_positions=T + 64)
+    s.init_synthetic(SEED)
+    x = (torch.randn(1, T, d.hidden, generator=torch.Generator().manual_seed(21)) * 0.5).to(torch.bfloat16)
+    out = s.forward([("p", T)], x=x[0])["hidden"][T - tail:].cpu()
+    del s
+    ref = R.decoder_layer_tail(x, R.gen_layer_weights(d, SEED, layer), d, tail)[0]
+    e = errs(out, ref)
+    print(f"32B layer, T={T}, last {tail} rows: {e}")
+    assert e["max_norm"] < TOL_REL
+    record("config5_q32b_layer_T8192_tail256", **e)
+
+
+# ------------------------------------------------------------------ BASELINE configs 3/4 on real spans
+def _free_port():
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    p = so.getsockname()[1]
+    so.close()
+    return p
+
+
+B8, T8, STEPS8 = 16, 2048, 4
+
+
+def _prompts(n_mb):
+    g = torch.Generator().manual_seed(77)
+    return [torch.randint(0, 151936, (B8, T8), generator=g) for _ in range(n_mb)]
+
+
+def _pipe_worker(rank, world, port, sizes, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from inferd_amd.pipeline import PipelineStage
+    from inferd_amd.runtime import MODELS
+    d = MODELS["qwen3-8b"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    spans = [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
+    first, n = spans[rank]
+    st = PipelineStage(d, rank, world, first, n, device=dev, seed=SEED, n_microbatches=world, batch=B8,
+                       max_ctx=T8 + STEPS8 + 8, prefill_chunk=2)
+    cap = {} if rank == 0 else None
+    st.prefill(_prompts(world), capture=cap)
+    st.prepare_decode(STEPS8)
+    rec = []
+    st.decode(STEPS8, record=rec)
+    torch.cuda.synchronize()
+    if rank == 0:
+        torch.save({"rec": [(k, m, t.cpu()) for k, m, t in rec], "hidden": cap["hidden"]},
+                   os.path.join(out_dir, "pipe.pt"))
+    dist.barrier()
+    st.release()
+    dist.destroy_process_group()
+
+
+def _single_worker(port, n_mb, out_dir):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    from inferd_amd.pipeline import PipelineStage
+    from inferd_amd.runtime import MODELS
+    d = MODELS["qwen3-8b"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    prompts = _prompts(n_mb)
+    st = PipelineStage(d, 0, 1, 0, d.layers, device=dev, seed=SEED, n_microbatches=1, batch=B8,
+                       max_ctx=T8 + STEPS8 + 8, prefill_chunk=2)
+    recs = []
+    for m in range(n_mb):        # the pipeline's microbatches, one after another
+        st.prefill([prompts[m]])
+        st.prepare_decode(STEPS8)
+        rec = []
+        st.step_base = 0
+        st.decode(STEPS8, record=rec)
+        torch.cuda.synchronize()
+        recs.append([t.cpu() for _, _, t in rec])
+        st.release()
+    torch.save([(k, m, recs[m][k]) for k in range(STEPS8) for m in range(n_mb)], os.path.join(out_dir, "single.pt"))
+    dist.destroy_process_group()
+
+
+def _spawn(target, args_list):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=target, args=a) for a in args_list]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    for p in procs:
+        assert p.exitcode == 0, p.exitcode
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("sizes", [[9, 9, 9, 9], [5, 27, 4]], ids=["config3_even4", "config4_uneven3"])
+def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes):
+    """BASELINE configs 3 (Qwen3-8B, 4 even spans) and 4 (the uneven [5, 27, 4] split) on the
+    real HIP spans: world ranks sharing this box's GPU (hand-offs through gloo), 16 sequences
+    per microbatch prefilled with 2048 tokens, 4 decode steps as captured-graph replays.  The
+    greedy ids fed back to stage 0 equal a single 36-layer span's, and the first stage
+    boundary's hidden state (sequences 0 and 1) matches the oracle."""
+    world = len(sizes)
+    port = _free_port()
+    _spawn(_pipe_worker, [(r, world, port, sizes, str(tmp_path)) for r in range(world)])
+    _spawn(_single_worker, [(_free_port(), world, str(tmp_path))])
+    pipe = torch.load(os.path.join(tmp_path, "pipe.pt"), weights_only=True)
+    single = torch.load(os.path.join(tmp_path, "single.pt"), weights_only=True)
+    got = [(k, m, t.tolist()) for k, m, t in pipe["rec"]]
+    one = [(k, m, t.tolist()) for k, m, t in single]
+    assert len(got) == STEPS8 * world
+    assert got == one
+    d = R.CONFIGS["qwen3-8b"]
+    oracle = R.RefSpan(d, SEED, 0, sizes[0] - 1, True, False, torch.bfloat16, "sdpa")
+    ref = oracle.forward(_prompts(world)[0][:2])
+    h = pipe["hidden"].reshape(2, T8, -1)
+    e = [errs(h[b], ref[b]) for b in range(2)]
+    print(f"{sizes}: ids identical over {STEPS8} steps x {world} microbatches; stage-0 boundary "
+          f"max_norm {[x['max_norm'] for x in e]}")
+    assert all(x["max_norm"] < TOL_REL for x in e)
+    record(f"q8b_pipeline_{'-'.join(map(str, sizes))}", ids_identical=True, decode_steps=STEPS8,
+           microbatches=world, boundary_err=e)
+
+
+# ------------------------------------------------------------------ gRPC span server (b')
+def _client_inputs(d, x, past, dtype=torch.bfloat16):
+    """What Qwen3Client sends: the additive causal mask (client.py:221-224), the zero
+    (1,1,1,1) mask for a decode token (:249-250), cache_position, (cos, sin) (:226)."""
+    T = x.shape[1]
+    pos = torch.arange(past, past + T)
+    if T > 1:
+        tril = torch.tril(torch.ones(T, T, dtype=dtype))
+        mask = ((1.0 - tril) * torch.finfo(dtype).min)[None, None]
+    else:
+        mask = torch.zeros((1, 1, 1, 1), dtype=dtype)
+    cos, sin = R.rope_cos_sin(d, pos[None], dtype)
+    return mask, pos, cos, sin
+
+
+@pytest.mark.parametrize("golden,cfg", [("tiny_server.npz", "tiny"), ("q06_layer.npz", "qwen3-0.6b")])
+def test_qwen3_server_send_vs_reference_golden(golden, cfg):
+    """inferd_amd.qwen3_server.Qwen3Server.send driven exactly as the reference client drives
+    its server (mask, cache_position, (cos, sin)), prefill + 4 cached decode calls, against
+    the reference's own Qwen3Server.send outputs."""
+    from inferd_amd.qwen3_server import Qwen3Server
+    g = load(golden)
+    d = R.CONFIGS[cfg]
+    srv = Qwen3Server(int(g["start"]), int(g["end"]), model=cfg, weights=f"synthetic:{SEED}", kv_pages=16,
+                      max_tokens=64)
+    oracle = R.RefSpan(d, SEED, int(g["start"]), int(g["end"]), False, False, torch.bfloat16, "sdpa")
+    ins = [tensor(g["bf16_in_prefill"])] + [tensor(g[f"bf16_in_dec{i}"]) for i in range(4)]
+    past, rows = 0, []
+    for i, x in enumerate(ins):
+        mask, pos, cos, sin = _client_inputs(d, x, past)
+        out = srv.send("sess", x.to(DEV), mask.to(DEV), pos.to(DEV), (cos.to(DEV), sin.to(DEV))).cpu()
+        e_gold, e_or = errs(out, tensor(g[f"bf16_out{i}"])), errs(out, oracle.forward_cached("sess", x))
+        rows.append({"call": i, "vs_golden_eager": e_gold, "vs_oracle": e_or})
+        assert e_gold["max_norm"] < TOL_REL_EAGER and e_or["max_norm"] < TOL_REL, (i, e_gold, e_or)
+        past += x.shape[1]
+    record(f"qwen3_server_send[{cfg}]", calls=rows)
+
+
+def test_qwen3_server_sessions_files_and_grpc(tmp_path):
+    """Session semantics of the drop-in: session_id=None is one persistent cache as in the
+    reference (server.py:39, qwen3_server_module.py:220); LRU eviction frees pages and a
+    later continuation of the evicted session fails its cache_position check; per-layer
+    layer_XX.pt state dicts load weights-only into the same span as the synthetic weights;
+    the gRPC servicer answers torch.save and raw TensorBlobs with the same hidden states."""
+    import grpc
+    from inferd_amd.grpc_span import (LayerRequest, Qwen3LayerServicer, TensorBlob, blob_to_tensor, client_stub,
+                                      make_server, tensor_to_blob)
+    from inferd_amd.qwen3_server import Qwen3Server
+    g = load("tiny_server.npz")
+    d = R.CONFIGS["tiny"]
+    xp = tensor(g["bf16_in_prefill"])
+    xd = tensor(g["bf16_in_dec0"])
+    srv = Qwen3Server(0, 3, model="tiny", kv_pages=16, max_tokens=64, max_sessions=2)
+    ref_p = srv.send("a", xp.to(DEV), cache_position=torch.arange(8)).cpu()
+    ref_d = srv.send("a", xd.to(DEV), cache_position=torch.tensor([8])).cpu()
+    # None: persistent, shared by every None call
+    assert torch.equal(srv.send(None, xp.to(DEV), cache_position=torch.arange(8)).cpu(), ref_p)
+    assert torch.equal(srv.send(None, xd.to(DEV), cache_position=torch.tensor([8])).cpu(), ref_d)
+    # LRU: a, None resident; b evicts a
+    free_before = srv.span.pool.n_free
+    srv.send("b", xp.to(DEV), cache_position=torch.arange(8))
+    assert srv.span.pool.n_free == free_before  # a's page went back, b took one
+    with pytest.raises(ValueError):
+        srv.send("a", xd.to(DEV), cache_position=torch.tensor([9]))
+    # weights-only per-layer files (qwen3_server_module.py:227-235 key names)
+    attn = ("q_proj", "k_proj", "v_proj", "o_proj", "q_norm", "k_norm")
+    for i in range(4):
+        sd = {("self_attn." if k in attn else "mlp." if k.endswith("_proj") else "") + k + ".weight": v
+              for k, v in R.gen_layer_weights(d, SEED, i).items()}
+        torch.save(sd, os.path.join(tmp_path, f"layer_{i:02d}.pt"))
+    srv2 = Qwen3Server(0, 3, model="tiny", weights=os.path.join(tmp_path, "layer_{idx:02d}.pt"), kv_pages=16,
+                       max_tokens=64)
+    assert torch.equal(srv2.send("a", xp.to(DEV), cache_position=torch.arange(8)).cpu(), ref_p)
+    # gRPC, both blob formats, session continued across calls
+    servicer = Qwen3LayerServicer(0, 3, model="tiny", kv_pages=16, max_tokens=64)
+    server, port = make_server(servicer, 0, host="127.0.0.1")
+    server.start()
+    try:
+        stub = client_stub(grpc.insecure_channel(f"127.0.0.1:{port}"))
+        for raw, sid in ((False, "g1"), (True, "g2")):
+            outs = []
+            for x, past in ((xp, 0), (xd, 8)):
+                mask, pos, cos, sin = _client_inputs(d, x, past)
+                req = LayerRequest(hidden_states=TensorBlob(data=tensor_to_blob(x, raw)),
+                                   attention_mask=TensorBlob(data=tensor_to_blob(mask, raw)),
+                                   cache_position=TensorBlob(data=tensor_to_blob(pos, raw)),
+                                   cos_embedding=TensorBlob(data=tensor_to_blob(cos, raw)),
+                                   sin_embedding=TensorBlob(data=tensor_to_blob(sin, raw)), session_id=sid)
+                outs.append(blob_to_tensor(stub(req, timeout=60).hidden_states.data))
+            assert torch.equal(outs[0], ref_p) and torch.equal(outs[1], ref_d), raw
+        with pytest.raises(grpc.RpcError):   # a broken blob -> INVALID_ARGUMENT, as server.py:36-37
+            stub(LayerRequest(hidden_states=TensorBlob(data=b"not a tensor"), session_id="x"), timeout=60)
+    finally:
+        server.stop(0)
+    record("qwen3_server_sessions_files_grpc", none_session=True, lru=True, layer_files=True, grpc_blobs=["torch.save", "raw"])
+
+
+# ------------------------------------------------------------------ f4: stage files from checkpoints
+def test_partitioned_qwen2_from_hf_checkpoint_and_converted_parts(tmp_path):
+    """Stage files built offline from (a) a HF-format safetensors checkpoint directory
+    (split_model --checkpoint) and (b) the reference's pickled stage modules
+    (convert_parts, inert unpickler) load into PartitionedQwen2 and give the same hidden
+    states as the synthetic stage of the same weights."""
+    from hf_fixtures import write_hf_checkpoint, write_reference_parts
+    from inferd_amd.convert_parts import convert
+    from inferd_amd.partitioned_models import PartitionedQwen2
+    from inferd_amd.runtime import MODELS
+    from inferd_amd.split_model import hf_checkpoint_source, split
+    cfg = {"model_name": "tiny", "parts_dir": str(tmp_path / "parts"), "stages_count": 2,
+           "stages": [{"name": "node0", "stage": 0, "start_layer": 0, "end_layer": 1},
+                      {"name": "node1", "stage": 1, "start_layer": 2, "end_layer": 3}]}
+    ck = write_hf_checkpoint(tmp_path / "hf", R.CONFIGS["tiny"], SEED)
+    p_hf = split(cfg, MODELS["tiny"], *hf_checkpoint_source(str(ck)), out_dir=str(tmp_path / "from_hf"))
+    write_reference_parts(tmp_path / "parts", cfg, R.CONFIGS["tiny"], SEED)
+    p_ref = convert(cfg, MODELS["tiny"], str(tmp_path / "parts"), str(tmp_path / "converted"))
+    ids = list(range(3, 60, 3))
+    syn = PartitionedQwen2("tiny", 2, 0, f"synthetic:{SEED}:tiny:0:1").forward({"generated_ids": ids})
+    tok = PartitionedQwen2("tiny", 2, 1, f"synthetic:{SEED}:tiny:2:3").forward(syn)["next_token_id"]
+    for paths in (p_hf, p_ref):
+        o0 = PartitionedQwen2("tiny", 2, 0, paths[0]).forward({"generated_ids": ids})
+        assert o0["hidden_meta"] == syn["hidden_meta"]
+        assert PartitionedQwen2("tiny", 2, 1, paths[1]).forward(o0)["next_token_id"] == tok
+    record("stage_files_from_checkpoints", hf_safetensors=True, reference_pickles_inert=True)

@@ -194,11 +194,13 @@ def test_q06_full_model_greedy_cached():
     print(f"greedy agreement {agree}/{len(gpu_tokens)}")
 
 
-def test_norm_fold_order_enforced():
-    """The RMSNorm weights are folded into q/k/v and gate/up at pack time: re-setting a norm
-    weight after its projections leaves them stale and forward must refuse (no silent use of
-    the old fold); re-setting the projections restores the exact synthetic span."""
+def test_norm_fold_order_enforced(monkeypatch):
+    """Folded-norm A/B spans (INFERD_NORM_FOLD=1) fold the RMSNorm weights into q/k/v and
+    gate/up at pack time: re-setting a norm weight after its projections leaves them stale and
+    forward must refuse (no silent use of the old fold); re-setting the projections restores
+    the exact synthetic span.  Exact-norm spans (the default) take weights in any order."""
     from inferd_amd import _lib
+    monkeypatch.setenv("INFERD_NORM_FOLD", "1")
     s = span("tiny", 0, 1, True, False)
     ids = torch.arange(8, dtype=torch.int32)
     ref = s.forward([(None, 8)], ids=ids)["hidden"]
@@ -212,6 +214,14 @@ def test_norm_fold_order_enforced():
     again = s.forward([(None, 8)], ids=ids)["hidden"]
     assert torch.equal(again.cpu(), ref.cpu())
     assert _lib.load() is not None
+    monkeypatch.setenv("INFERD_NORM_FOLD", "0")
+    e = span("tiny", 0, 1, True, False)
+    ref = e.forward([(None, 8)], ids=ids)["hidden"]
+    e.set_weight(0, "input_layernorm", w_in)
+    changed = e.forward([(None, 8)], ids=ids)["hidden"]
+    assert not torch.equal(changed.cpu(), ref.cpu())
+    e.init_synthetic(SEED)
+    assert torch.equal(e.forward([(None, 8)], ids=ids)["hidden"].cpu(), ref.cpu())
 
 
 def test_decode_fused_rope_matches_separate(monkeypatch):
@@ -239,32 +249,6 @@ def test_decode_fused_rope_matches_separate(monkeypatch):
     e = rel_err(outs[0], outs[1])
     print(f"fused vs separate decode hidden rel err {e:.2e}")
     assert e < 2e-2
-
-
-def test_config1_q06_two_spans_greedy_dict_protocol():
-    """BASELINE config 1 on the GPU engine: Qwen3-0.6B as two 14-layer spans behind the
-    node-facing dict protocol (generated_ids -> bf16 hidden_meta -> next_token_id), greedy
-    full-recompute decode of a 32-token prompt (send_message.py:46-60 semantics), against
-    the oracle's two-span chain with the same attention semantics (SDPA)."""
-    from inferd_amd.partitioned_models import PartitionedQwen2
-    d = R.CONFIGS["qwen3-0.6b"]
-    n0 = PartitionedQwen2("qwen3-0.6b", 2, 0, f"synthetic:{SEED}:qwen3-0.6b:0:13")
-    n1 = PartitionedQwen2("qwen3-0.6b", 2, 1, f"synthetic:{SEED}:qwen3-0.6b:14:27")
-    b0 = R.RefSpan(d, SEED, 0, 13, True, False, torch.bfloat16, "sdpa")
-    b1 = R.RefSpan(d, SEED, 14, 27, False, True, torch.bfloat16, "sdpa")
-    ids = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(11)).tolist()
-    agree = checked = 0
-    for step in range(6):
-        o1 = n1.forward(n0.forward({"generated_ids": ids}))
-        lg = b1.forward(b0.forward(torch.tensor([ids])))[0, -1]
-        rid, m = int(torch.argmax(lg)), R.top2_margin(lg)
-        print(f"step {step}: gpu {o1['next_token_id']} ref {rid} margin {m:.4f}")
-        if m > MARGIN_FLOOR:
-            checked += 1
-            agree += int(o1["next_token_id"] == rid)
-            assert o1["next_token_id"] == rid, step
-        ids = ids + [rid]
-    print(f"config 1: {agree}/{checked} greedy steps above the margin floor agree")
 
 
 def test_config5_q32b_layer_prefill_vs_oracle():
@@ -393,38 +377,3 @@ def test_config3_q8b_layer_b16_ctx2048_decode_graph():
             worst = max(worst, e)
             assert e < TOL_REL, (k, b, e)
         print(f"decode step {k} (ctx {T + k + 1}): worst rel err {worst:.2e}")
-
-
-def test_attn_o_one_grid_bit_identical(monkeypatch):
-    """INFERD_FUSE_ATTN_O=1 / 2 (decode attention + o_proj in one grid, attention.hip
-    attn_o_decode_kernel / attn_o_persist_kernel) give bit-identical hidden states to the two
-    separate launches,
-    eager and through captured decode graphs (Qwen3-8B layer, 16 sequences, 300-token prompts)."""
-    from inferd_amd.runtime import DecodeGraph
-    d = R.CONFIGS["qwen3-8b"]
-    B, T, steps = 16, 300, 3
-    gen = torch.Generator().manual_seed(5)
-    x = (torch.randn(B * T, d.hidden, generator=gen) * 0.5).to(torch.bfloat16).to(DEV)
-    xs = [(torch.randn(B, d.hidden, generator=gen) * 0.5).to(torch.bfloat16).to(DEV) for _ in range(2 * steps)]
-    outs = []
-    for flag in ("0", "1", "2"):
-        monkeypatch.setenv("INFERD_FUSE_ATTN_O", flag)
-        s = span("qwen3-8b", 7, 1, False, False, kv_pages=B * 8 + 4, max_tokens=B * T, max_seqs=B,
-                 max_positions=T + 64)
-        sess = [f"f{b}" for b in range(B)]
-        s.forward([(sid, T) for sid in sess], x=x)
-        got = []
-        for k in range(steps):  # eager
-            got.append(s.forward([(sid, 1) for sid in sess], x=xs[k])["hidden"].clone())
-        xin = torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV)
-        hout = torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV)
-        g = DecodeGraph(s, sess, steps, x=xin, hidden_out=hout)
-        for k in range(steps):  # graph replays
-            xin.copy_(xs[steps + k])
-            g.launch()
-            got.append(hout.clone())
-        torch.cuda.synchronize()
-        outs.append(torch.stack(got).cpu())
-        del g, s
-    for o in outs[1:]:
-        assert torch.equal(outs[0], o), (outs[0].float() - o.float()).abs().max()

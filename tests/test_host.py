@@ -203,3 +203,97 @@ def test_build_batch_descriptor_layout():
         assert dev.tolist() == start + pos + slots + ctx + table
         assert batch.n_tokens == sum(n for _, n in seqs) and batch.max_ctx_len == max(ctx)
         assert batch.max_q_len == max(n for _, n in seqs) and batch.max_pages == max_pages
+
+
+def test_split_model_from_hf_checkpoint(tmp_path):
+    """split_model's HF-safetensors source (sharded checkpoint dir, split_model.py:81's
+    from_pretrained weights): every stage file holds the checkpoint's tensors under the
+    engine's keys, roles from `stage`."""
+    from safetensors import safe_open
+    from hf_fixtures import write_hf_checkpoint
+    from inferd_amd.runtime import MODELS
+    from inferd_amd.split_model import hf_checkpoint_source, split
+    from oracle import qwen3_ref as R
+    d = R.CONFIGS["tiny"]
+    ck = write_hf_checkpoint(str(tmp_path / "hf"), d, 99)
+    cfg = {"model_name": "tiny", "parts_dir": str(tmp_path / "out"), "stages_count": 2,
+           "stages": [{"name": "node0", "stage": 0, "start_layer": 0, "end_layer": 1},
+                      {"name": "node1", "stage": 1, "start_layer": 2, "end_layer": 3}]}
+    paths = split(cfg, MODELS["tiny"], *hf_checkpoint_source(ck))
+    g = R.gen_global_weights(d, 99)
+    with safe_open(paths[0], framework="pt") as f:
+        assert torch.equal(f.get_tensor("embed.weight"), g["embed_tokens"]) and "lm_head.weight" not in f.keys()
+        assert torch.equal(f.get_tensor("layers.1.mlp.up_proj.weight"), R.gen_layer_weights(d, 99, 1)["up_proj"])
+    with safe_open(paths[1], framework="pt") as f:
+        assert torch.equal(f.get_tensor("lm_head.weight"), g["lm_head"]) and f.metadata()["last"] == "1"
+        assert torch.equal(f.get_tensor("layers.0.self_attn.k_norm.weight"), R.gen_layer_weights(d, 99, 2)["k_norm"])
+
+
+def test_convert_reference_parts_executes_nothing(tmp_path):
+    """The reference's pickled stage modules (torch.save(module), split_model.py:107) convert
+    to engine stage files through the inert unpickler: tensors identical, every class the
+    pickle names stays a stub -- including one whose __setstate__ would record a call."""
+    import pickle
+    from safetensors import safe_open
+    import hf_fixtures
+    from inferd_amd import convert_parts as C
+    from inferd_amd.runtime import MODELS
+    from oracle import qwen3_ref as R
+    d = R.CONFIGS["tiny"]
+    cfg = {"model_name": "tiny", "parts_dir": str(tmp_path / "parts"), "stages_count": 3,
+           "stages": [{"name": "a", "stage": 0, "start_layer": 0, "end_layer": 0},
+                      {"name": "b", "stage": 1, "start_layer": 1, "end_layer": 2},
+                      {"name": "c", "stage": 2, "start_layer": 3, "end_layer": 3}]}
+    hf_fixtures.write_reference_parts(cfg["parts_dir"], cfg, d, 5)
+    calls = []
+    hf_fixtures.StageInner.__setstate__ = lambda self, st: calls.append(st)   # would run under torch.load
+    try:
+        paths = C.convert(cfg, MODELS["tiny"], cfg["parts_dir"], str(tmp_path / "out"))
+        tree = C.load_inert(str(tmp_path / "parts" / "b" / "model.pth"))
+    finally:
+        del hf_fixtures.StageInner.__setstate__
+    assert not calls and isinstance(tree, C.Stub) and tree.qualname.endswith("StageInner")
+    with safe_open(paths[1], framework="pt") as f:
+        assert sorted(f.keys()) == sorted(f"layers.{j}.{k}" for j in range(2) for k in C._LAYER_LEAVES)
+        assert torch.equal(f.get_tensor("layers.1.self_attn.o_proj.weight"), R.gen_layer_weights(d, 5, 2)["o_proj"])
+    with safe_open(paths[2], framework="pt") as f:
+        assert torch.equal(f.get_tensor("lm_head.weight"), R.gen_global_weights(d, 5)["lm_head"])
+    with safe_open(paths[0], framework="pt") as f:
+        assert torch.equal(f.get_tensor("embed.weight"), R.gen_global_weights(d, 5)["embed_tokens"])
+    with pytest.raises(pickle.UnpicklingError):    # no real class can be reconstructed
+        C._reconstructor(dict, object)
+
+
+def test_grpc_blob_codec_and_messages():
+    """TensorBlob payloads: the reference's torch.save bytes (read weights-only) and the raw
+    form round-trip every dtype the client sends; the message classes serialise with the
+    reference's field numbers (qwen3.proto:5-20)."""
+    from inferd_amd import grpc_span as G
+    for t in (torch.randn(1, 3, 8).to(torch.bfloat16), torch.randn(2, 5), torch.arange(7),
+              torch.zeros(1, 1, 4, 4, dtype=torch.bool), torch.randn(1, 1, 1, 1).to(torch.bfloat16)):
+        for raw in (False, True):
+            b = G.tensor_to_blob(t, raw)
+            assert G.blob_is_raw(b) == raw
+            back = G.blob_to_tensor(b)
+            assert back.dtype == t.dtype and torch.equal(back, t)
+    req = G.LayerRequest(hidden_states=G.TensorBlob(data=b"xy"), session_id="s")
+    wire = req.SerializeToString()
+    assert wire == b"\n\x04\n\x02xy2\x01s"     # field 1 (message: field 1 bytes), field 6 string
+    assert G.LayerRequest.FromString(wire).session_id == "s"
+
+
+def test_peaked_profile_oracle_definition():
+    """The peaked synthetic profile: embed scaled by a power of two (exact), lm_head row p(t)
+    = random row + LM_MIX * embed[t], p a bijection of the vocabulary."""
+    import numpy as np
+    from oracle import qwen3_ref as R
+    from oracle import weightgen as wg
+    d = R.CONFIGS["tiny"]
+    p = wg.peaked_perm(d.vocab)
+    assert sorted(p.tolist()) == list(range(d.vocab))
+    g, q = R.gen_global_weights(d, 3), R.gen_global_weights(d, 3, profile="peaked")
+    assert torch.equal(q["embed_tokens"].float(), g["embed_tokens"].float() * wg.EMBED_BOOST)
+    t = 17
+    assert torch.equal(q["lm_head"][int(p[t])], (g["lm_head"][int(p[t])].float() + wg.LM_MIX *
+                                                  g["embed_tokens"][t].float()).to(torch.bfloat16))
+    assert torch.equal(q["norm"], g["norm"]) and np.all(np.diff(np.sort(p)) == 1)
