@@ -22,7 +22,7 @@ the launch stream around every kernel of `--profile-steps` eager decode steps of
 workload, run right after the timed region (HIP cannot time event nodes inside a replayed
 graph); the dominant kernel class's algorithmic bytes per launch / its mean event time,
 against 8 TB/s HBM.  `traffic` = PMC-measured HBM bytes per launch of that class
-(tools/profile_decode.sh -> profiles/traffic_r01.json).  cpu_baseline: the oracle
+(tools/profile_round.sh -> the newest profiles/traffic_rNN.json).  cpu_baseline: the oracle
 (oracle/qwen3_ref.py, `port`) on the host cores, rank 0 at N = 1 only.
 """
 from __future__ import annotations
@@ -41,6 +41,19 @@ from inferd_amd.pipeline import balanced_split, even_split  # noqa: E402  (host 
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFLOPS = 2500.0
+
+
+def latest_traffic(kind: str, workload: str):
+    """The newest committed PMC traffic summary (profiles/traffic[_prefill]_rNN.json) measured
+    on `workload`: {kernel class: HBM bytes per launch}, or None."""
+    import glob
+    pat = os.path.join(ROOT, "profiles", f"traffic{'_prefill' if kind == 'prefill' else ''}_r[0-9]*.json")
+    for fn in sorted(glob.glob(pat), reverse=True):
+        with open(fn) as f:
+            tr = json.load(f)
+        if tr.get("workload") == workload:
+            return tr.get("per_launch_bytes", {})
+    return None
 
 
 def parse():
@@ -108,15 +121,10 @@ def run_prefill(args):
     kernels = {k: {"launches": n, "avg_ms": round(ms / max(n, 1), 3)} for k, (ms, n) in prof.items() if n}
     tf = fl / t / 1e12
     # PMC-measured L2-to-fabric bytes per launch of the dominant kernel class
-    # (tools/pmc_prefill.sh -> profiles/traffic_prefill_r01.json; MALL hits are counted too)
+    # (tools/pmc_prefill.sh -> the newest profiles/traffic_prefill_rNN.json; MALL hits count)
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_prefill_r01.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
-            tr = json.load(f)
-        if tr.get("workload") == f"{d.name}-prefill-{L}layers-T{T}" and B == 1:
-            traffic = tr["per_launch_bytes"].get(dom)
+    tr = latest_traffic("prefill", f"{d.name}-prefill-{L}layers-T{T}") if B == 1 else None
+    traffic = None if tr is None else tr.get(dom)
     print(json.dumps({
         "metric": "prefill tokens/sec, Qwen3-32B 8-layer span (one of 8 pipeline stages)",
         "value": round(B * T / t, 1), "unit": "tokens/s", "n_gpus": 1, "steps": args.steps,
@@ -375,13 +383,8 @@ def main():
                              "alg_bytes": int(kb[name]), "GB/s": round(gbs, 1),
                              "frac": round(gbs / HBM_PEAK_GBS, 4)}
         dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_r01.json")
-        if os.path.exists(tf):
-            with open(tf) as f:
-                tr = json.load(f)
-            if tr.get("workload") == f"{args.model}-decode-B{B}-ctx{ctx}" and dom in tr.get("per_launch_bytes", {}):
-                traffic = tr["per_launch_bytes"][dom]
+        tr = latest_traffic("decode", f"{args.model}-decode-B{B}-ctx{ctx}")
+        traffic = None if tr is None else tr.get(dom)
         roof = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["GB/s"], "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": kernels[dom]["frac"], "traffic": traffic,
                 "alg_bytes_per_launch": kernels[dom]["alg_bytes"]}

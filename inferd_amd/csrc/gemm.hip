@@ -73,7 +73,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
   __shared__ float sm_ss[NORM == DN_FOLD ? NW : 1][MT * 16];
-  __shared__ float sm_r[NORM == DN_EXACT ? NW * 64 : 1];
+  __shared__ __attribute__((aligned(16))) float sm_r[NORM == DN_EXACT ? NW * 256 : 4];
   // DN_EXACT: this workgroup's K range of the norm weight, staged once (<= 8192 columns)
   __shared__ __attribute__((aligned(16))) u16 sm_w[NORM == DN_EXACT ? DECODE_NORM_MAXK : 8];
   const int M = g.M;
@@ -121,24 +121,48 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
       ((b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
     }(std::make_integer_sequence<int, D - 1>{});
   }
+  // DN_EXACT operands, issued right behind the weight prologue (one round trip for both):
+  // the partial sums of squares of the M rows -- the threads cover (row quad, part) pairs,
+  // QM = ceil(M / 4) quads x PP part lanes, eight independent 16-B loads at a time -- and
+  // this thread's chunks of the norm weight
+  constexpr int WCH = (DECODE_NORM_MAXK / 8 + NW * 64 - 1) / (NW * 64);
+  f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+  u16x8 wst[NORM == DN_EXACT ? WCH : 1];
+  const int QM = (M + 3) >> 2, PP = (NW * 64) / QM;
+  if constexpr (NORM == DN_EXACT) {
+    // unconditional loads of clamped addresses (no branches between the loads and the
+    // weight prologue: a predicated load here made hipcc drain vmcnt early)
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int c = min((int)threadIdx.x + i * NW * 64, KT * 4 - 1);
+      wst[i] = *(const u16x8*)(g.norm_w + kt0 * 32 + c * 8);
+    }
+    const int quad = threadIdx.x % QM, p0 = min((int)threadIdx.x / QM, PP - 1);
+    for (int base = p0; base < g.n_parts; base += 8 * PP) {
+      f32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = *(const f32x4*)(g.ssq_in + min(base + i * PP, g.n_parts - 1) * 64 + 4 * quad);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (base + i * PP < g.n_parts) s4 += v[i];
+    }
+  }
   float rr[MT];  // DN_EXACT: r of row mt*16 + (lane & 15)
   if constexpr (NORM == DN_EXACT) {
-    // ssq_in[p][row], p < n_parts: thread t sums rows (t % 64) over parts t/64, t/64 + NW, ...
-    // then the NW partial sums of a row add in fixed order (deterministic)
-    const int row = threadIdx.x & 63;
-    float t = 0.f;
-    if (row < M)
-      for (int p = threadIdx.x >> 6; p < g.n_parts; p += NW) t += g.ssq_in[p * 64 + row];
-    sm_r[threadIdx.x] = t;
-    for (int c = threadIdx.x; c < KT * 4; c += NW * 64)
-      *(u16x8*)(sm_w + c * 8) = *(const u16x8*)(g.norm_w + kt0 * 32 + c * 8);
+    // the PP partial sums of a row add in fixed order (deterministic)
+    if (threadIdx.x < PP * QM) *(f32x4*)(sm_r + 4 * threadIdx.x) = s4;   // [p0][quad]
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int c = threadIdx.x + i * NW * 64;
+      if (c < KT * 4) *(u16x8*)(sm_w + c * 8) = wst[i];
+    }
     __syncthreads();
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int rw = mt * 16 + (lane & 15);
       float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) s += sm_r[w * 64 + rw];
+      if (rw < M)
+        for (int q = 0; q < PP; ++q) s += sm_r[4 * (q * QM + (rw >> 2)) + (rw & 3)];
       rr[mt] = 1.0f / sqrtf(s / (float)(g.KT * 32) + g.eps);
     }
   }

@@ -150,17 +150,17 @@ def test_config1_teacher_forced_random_weights():
 def test_nn_forward_session_cache_matches_full_recompute(q06_peaked):
     """The optional session_id at the node API: stage 0 runs only the ids past its cached
     prefix, hidden_meta carries the new rows, stage 1 appends them to its pages; the greedy
-    ids equal the stateless full-recompute chain's over 16 steps, and closing the session
-    frees every page."""
-    n0, n1, _, _ = q06_peaked
+    ids equal the stateless full-recompute chain's over 16 steps, each new row's boundary
+    hidden state matches the oracle's, and closing the session frees every page."""
+    n0, n1, b0, _ = q06_peaked
     d = R.CONFIGS["qwen3-0.6b"]
     prompt = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(12)).tolist()
-    ids, full, full_h = list(prompt), [], []
+    ids, full, ref_h = list(prompt), [], []
     for _ in range(16):
         o0 = n0.forward({"generated_ids": ids})
-        full_h.append(_hidden(o0["hidden_meta"])[0, -1])
         o1 = n1.forward(o0)
         full.append(o1["next_token_id"])
+        ref_h.append(b0.forward(torch.tensor([ids]))[0, -1])   # oracle boundary row of the new token
         ids = o1["generated_ids"]
     free0, free1 = n0.span.pool.n_free, n1.span.pool.n_free
     ids, cached, worst = list(prompt), [], 0.0
@@ -168,12 +168,12 @@ def test_nn_forward_session_cache_matches_full_recompute(q06_peaked):
         o0 = n0.forward({"generated_ids": ids, "session_id": "s1"})
         h = _hidden(o0["hidden_meta"])
         assert h.shape[1] == (32 if step == 0 else 1) and o0["past_len"] == (0 if step == 0 else 31 + step)
-        worst = max(worst, errs(h[0, -1], full_h[step])["max_norm"])
+        worst = max(worst, errs(h[0, -1], ref_h[step])["max_norm"])
         o1 = n1.forward(o0)
         assert o1["session_id"] == "s1"
         cached.append(o1["next_token_id"])
         ids = o1["generated_ids"]
-    print(f"session chain: last-row hidden vs full recompute worst max_norm {worst:.2e}")
+    print(f"session chain: new-row boundary hidden vs oracle worst max_norm {worst:.2e}")
     assert cached == full
     assert worst < TOL_REL
     # a request that does not extend the cached prefix restarts the session
@@ -182,7 +182,7 @@ def test_nn_forward_session_cache_matches_full_recompute(q06_peaked):
     c = n1.forward(n0.forward({"session_id": "s1", "close_session": True}))
     assert c == {"session_id": "s1", "closed": True}
     assert n0.span.pool.n_free == free0 and n1.span.pool.n_free == free1
-    record("nn_forward_session_vs_full", steps=16, identical=True, last_row_hidden_worst_max_norm=worst)
+    record("nn_forward_session_vs_full", steps=16, identical=True, new_row_hidden_vs_oracle_worst_max_norm=worst)
 
 
 def test_nn_forward_long_prompt_chunked(q06_peaked):

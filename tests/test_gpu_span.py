@@ -298,43 +298,41 @@ def test_prefill_fused_q_rope_matches_separate(monkeypatch):
     assert e < 2e-2
 
 
-@pytest.mark.gpu
 def test_prefill_qkv_epilogue_matches_separate(monkeypatch):
     """q/k RMSNorm + RoPE and the K/V cache write in the persistent q/k/v GEMM's epilogue
-    (default) against the separate qk_norm_rope_kv kernel (INFERD_FUSE_QKV_EPI=0): one
+    (default) and in the separate qk_norm_rope_kv kernel (INFERD_FUSE_QKV_EPI=0): one
     Qwen3-8B-dims layer, a 780-row ragged prefill (fused path), a 150-row cached extension
-    (too short for it: separate kernel) and a decode step reading the cache both wrote."""
+    (too short for it: separate kernel) and a decode step reading the cache both wrote --
+    both against the oracle.  The two differ only in the order of the q/k sum of squares (32
+    dims per lane then 4 lanes, vs 8 then 16), so a flip of one rounding reaches a few rows;
+    they must stay within a bf16-rounding distance of each other."""
     from inferd_amd.runtime import MODELS, SpanRuntime
     d = MODELS["qwen3-8b"]
+    g = torch.Generator().manual_seed(9)
+    x0 = (torch.randn(600 + 180, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+    x1 = (torch.randn(150, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+    x2 = (torch.randn(2, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+    oracle = R.RefSpan(R.CONFIGS["qwen3-8b"], SEED, 5, 5, False, False, torch.bfloat16, "sdpa")
+    ref = torch.cat([oracle.forward_cached("a", x0[None, :600])[0], oracle.forward_cached("b", x0[None, 600:])[0],
+                     oracle.forward_cached("a", x1[None])[0], oracle.forward_cached("a", x2[None, :1])[0],
+                     oracle.forward_cached("b", x2[None, 1:])[0]])
     outs = []
     for fused in ("1", "0"):
         monkeypatch.setenv("INFERD_FUSE_QKV_EPI", fused)
         s = SpanRuntime(d, 5, 1, has_embed=False, has_lm_head=False, device=DEV, max_positions=1024,
                         kv_pages=40, max_tokens=1024, max_seqs=4)
         s.init_synthetic(SEED)
-        g = torch.Generator().manual_seed(9)
-        x0 = (torch.randn(600 + 180, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
-        x1 = (torch.randn(150, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
-        x2 = (torch.randn(2, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
         h0 = s.forward([("a", 600), ("b", 180)], x=x0, want_hidden=True)["hidden"].cpu()
         h1 = s.forward([("a", 150)], x=x1, want_hidden=True)["hidden"].cpu()
         h2 = s.forward([("a", 1), ("b", 1)], x=x2, want_hidden=True)["hidden"].cpu()
         outs.append(torch.cat([h0, h1, h2]))
+        e = rel_err(outs[-1], ref)
+        print(f"INFERD_FUSE_QKV_EPI={fused}: vs oracle rel err {e:.2e}")
+        assert e < TOL_REL
     e = rel_err(outs[0], outs[1])
     diff = (outs[0].float() - outs[1].float()).abs()
     print(f"qkv-epilogue vs separate: rel err {e:.2e}, differing elements {(diff > 0).float().mean():.2e}")
-    n_rows = 0
-    for name, lo, hi in (("prefill a", 0, 600), ("prefill b", 600, 780), ("extend", 780, 930), ("decode", 930, 932)):
-        dd = diff[lo:hi]
-        rows = (dd.max(dim=1).values > 0).nonzero().flatten().tolist()
-        n_rows += len(rows)
-        print(f"  {name}: rel err {rel_err(outs[0][lo:hi], outs[1][lo:hi]):.2e} max {dd.max():.3g} "
-              f"rows differing {len(rows)} first {rows[:8]}")
-    # same arithmetic except the order of the q/k RMSNorm sum of squares (32 dims per lane,
-    # then 4 lanes, vs 8 dims per lane, then 16): a rounding flip reaches a few rows (one q
-    # row per prompt on the box); the extension and decode rows read the cache both wrote
-    assert n_rows <= 0.005 * 932, n_rows
-    assert e < 1e-2
+    assert e < 1e-2 and (diff > 0).float().mean() < 0.05
 
 
 def test_config3_q8b_layer_b16_ctx2048_decode_graph():

@@ -7,7 +7,7 @@ FETCH_SIZE and WRITE_SIZE do not fit one TCC pass):
       python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-profile
   rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- \
       python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-profile
-  python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic_r01.json
+  python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/traffic_rNN.json
 
 Corrections (MI355X_MICROARCH.md §HBM): both counters are in KiB; on gfx950 FETCH_SIZE reports
 half the bytes of a wide (16 B/lane) coalesced streaming read, so fetched bytes =
@@ -38,7 +38,7 @@ def rows(d):
     return out
 
 
-PREFILL_KEYS = ("gemm_tiled", "gemm_ring", "attn_prefill", "row_inv_rms")
+PREFILL_KEYS = ("gemm_tiled", "gemm_w4", "attn_prefill", "row_inv_rms", "qk_norm_rope_kv")
 
 
 def classify(name):
@@ -48,9 +48,9 @@ def classify(name):
         if not m:
             return "gemm_decode"
         epi = int(m.group(1).split(",")[5])  # <MT, S, NW, TW, D, EPI, NORM>
-        return {0: "qkv_gemm", 1: "resid_gemm", 2: "gateup_gemm", 3: "lm_head_argmax", 4: "qkv_gemm"}[epi]
+        return {0: "qkv_gemm", 1: "resid_gemm", 2: "gateup_gemm", 3: "lm_head_gemv", 4: "qkv_gemm"}[epi]
     for key, cls in (("attn_decode_kernel", "attention"), ("qk_norm_rope_kv", "qk_norm_rope_kv"),
-                     ("rmsnorm", "rmsnorm"), ("argmax_reduce", "lm_head_argmax")):
+                     ("rmsnorm", "rmsnorm"), ("argmax_reduce", "argmax_reduce")):
         if key in name:
             return cls
     return None
@@ -96,6 +96,10 @@ def main():
     fetch = summarize(per_dispatch(fetch_dir, "FETCH_SIZE"), 2 * 1024.0)
     write = summarize(per_dispatch(write_dir, "WRITE_SIZE"), 1024.0)
     per = {k: int(fetch.get(k, 0) + write.get(k, 0)) for k in sorted(set(fetch) | set(write))}
+    # the bench's lm_head_argmax class times the lm_head GEMV and the argmax reduce together
+    # (one launch of each per step): its per-launch traffic is their sum, not their mean
+    if "lm_head_gemv" in per:
+        per["lm_head_argmax"] = per["lm_head_gemv"] + per.get("argmax_reduce", 0)
     print(json.dumps({
         "workload": "qwen3-8b-decode-B16-ctx2048",
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); bytes = 2*FETCH_SIZE*1024 "
