@@ -122,22 +122,27 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
     }(std::make_integer_sequence<int, D - 1>{});
   }
   // DN_EXACT operands, issued right behind the weight prologue (one round trip for both):
-  // the partial sums of squares of the M rows -- the threads cover (row quad, part) pairs,
-  // QM = ceil(M / 4) quads x PP part lanes, eight independent 16-B loads at a time -- and
-  // this thread's chunks of the norm weight
-  constexpr int WCH = (DECODE_NORM_MAXK / 8 + NW * 64 - 1) / (NW * 64);
+  // the partial sums of squares of the M rows -- thread t takes row quad t / PP (QM =
+  // ceil(M / 4) quads, PP = the largest power of two <= threads / QM part lanes each) and
+  // parts t % PP, t % PP + PP, ..., eight independent 16-B loads at a time -- and this
+  // thread's chunks of the norm weight
+  constexpr int NT = NW * 64;
+  constexpr int WCH = (DECODE_NORM_MAXK / 8 + NT - 1) / NT;
   f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
   u16x8 wst[NORM == DN_EXACT ? WCH : 1];
-  const int QM = (M + 3) >> 2, PP = (NW * 64) / QM;
+  const int QM = (M + 3) >> 2;
+  int PP = NT;
+  while (PP * QM > NT) PP >>= 1;
+  const int GL = PP < 64 ? PP : 64;  // lanes of one shuffle-reduction group
   if constexpr (NORM == DN_EXACT) {
     // unconditional loads of clamped addresses (no branches between the loads and the
     // weight prologue: a predicated load here made hipcc drain vmcnt early)
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
-      const int c = min((int)threadIdx.x + i * NW * 64, KT * 4 - 1);
+      const int c = min((int)threadIdx.x + i * NT, KT * 4 - 1);
       wst[i] = *(const u16x8*)(g.norm_w + kt0 * 32 + c * 8);
     }
-    const int quad = threadIdx.x % QM, p0 = min((int)threadIdx.x / QM, PP - 1);
+    const int quad = min((int)threadIdx.x / PP, QM - 1), p0 = threadIdx.x % PP;
     for (int base = p0; base < g.n_parts; base += 8 * PP) {
       f32x4 v[8];
 #pragma unroll
@@ -149,11 +154,16 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   }
   float rr[MT];  // DN_EXACT: r of row mt*16 + (lane & 15)
   if constexpr (NORM == DN_EXACT) {
-    // the PP partial sums of a row add in fixed order (deterministic)
-    if (threadIdx.x < PP * QM) *(f32x4*)(sm_r + 4 * threadIdx.x) = s4;   // [p0][quad]
+    // butterfly over each group of GL part lanes (fixed pattern: deterministic), then the
+    // group leaders' sums in LDS, PP / GL groups per quad added in order below
+    for (int o = 1; o < GL; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s4[j] += __shfl_xor(s4[j], o);
+    }
+    if ((threadIdx.x % GL) == 0) *(f32x4*)(sm_r + 4 * (threadIdx.x / GL)) = s4;
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
-      const int c = threadIdx.x + i * NW * 64;
+      const int c = threadIdx.x + i * NT;
       if (c < KT * 4) *(u16x8*)(sm_w + c * 8) = wst[i];
     }
     __syncthreads();
@@ -161,8 +171,9 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
     for (int mt = 0; mt < MT; ++mt) {
       const int rw = mt * 16 + (lane & 15);
       float s = 0.f;
+      const int ng = PP / GL, g0 = (rw >> 2) * ng;
       if (rw < M)
-        for (int q = 0; q < PP; ++q) s += sm_r[4 * (q * QM + (rw >> 2)) + (rw & 3)];
+        for (int q = 0; q < ng; ++q) s += sm_r[4 * (g0 + q) + (rw & 3)];
       rr[mt] = 1.0f / sqrtf(s / (float)(g.KT * 32) + g.eps);
     }
   }

@@ -3,9 +3,10 @@ BASELINE configs and through every boundary the reference exposes; every measure
 margin and greedy step lands in the parity record (tests/parity_log.py).
 
 Tolerances (asserted per tensor):
-  * bf16 hidden states / logits: max|got - ref| <= TOL_REL * max|ref| against the oracle with
-    the same attention semantics (SDPA), TOL_REL_EAGER against the gRPC golden (the
-    reference's eager attention rounds scores to bf16; the kernels keep them in fp32);
+  * bf16 hidden states / logits of one layer: max|got - ref| <= TOL_REL * max|ref| against
+    the oracle with the same attention semantics (SDPA), TOL_REL_EAGER against the gRPC
+    golden (the reference's eager attention rounds scores to bf16; the kernels keep them in
+    fp32); after a whole span (>= 8 layers) TOL_SPAN / TOL_SPAN_RMS (span_ok);
   * greedy tokens: identical on every step; with the "peaked" synthetic profile (large top-1
     margins, oracle/weightgen.py) free-running, and every step's oracle margin must exceed
     twice the measured logit error, so the agreement is not luck; with plain random weights
@@ -29,6 +30,15 @@ SEED = 1234
 DEV = "cuda"
 TOL_REL = 2e-2
 TOL_REL_EAGER = 3e-2
+# hidden states after a whole multi-layer span (>= 8 layers): bf16 roundings of the two sides
+# compound layer over layer, so the per-tensor max bound is wider and an aggregate bound is
+# added: max|got - ref| <= TOL_SPAN * max|ref| and rms(got - ref) <= TOL_SPAN_RMS * rms(ref)
+TOL_SPAN = 4e-2
+TOL_SPAN_RMS = 1e-2
+
+
+def span_ok(e):
+    return e["max_norm"] < TOL_SPAN and e["rms_rel"] < TOL_SPAN_RMS
 
 
 def _pq(model, n_stages, stage, start, end, profile="random"):
@@ -113,7 +123,7 @@ def test_config1_free_running_greedy_peaked(q06_peaked):
               f"logit max_abs {e_lg['max_abs']:.3f} boundary max_norm {e_h['max_norm']:.2e}")
         assert o1["next_token_id"] == rid, step
         assert margin > 2 * e_lg["max_abs"], (step, margin, e_lg)
-        assert e_h["max_norm"] < TOL_REL
+        assert span_ok(e_h), e_h
         gpu_ids = o1["generated_ids"]
         ref_ids = ref_ids + [rid]
     assert gpu_ids == ref_ids
@@ -163,26 +173,28 @@ def test_nn_forward_session_cache_matches_full_recompute(q06_peaked):
         ref_h.append(b0.forward(torch.tensor([ids]))[0, -1])   # oracle boundary row of the new token
         ids = o1["generated_ids"]
     free0, free1 = n0.span.pool.n_free, n1.span.pool.n_free
-    ids, cached, worst = list(prompt), [], 0.0
+    ids, cached, worst, worst_rms = list(prompt), [], 0.0, 0.0
     for step in range(16):
         o0 = n0.forward({"generated_ids": ids, "session_id": "s1"})
         h = _hidden(o0["hidden_meta"])
         assert h.shape[1] == (32 if step == 0 else 1) and o0["past_len"] == (0 if step == 0 else 31 + step)
-        worst = max(worst, errs(h[0, -1], ref_h[step])["max_norm"])
+        e = errs(h[0, -1], ref_h[step])
+        worst, worst_rms = max(worst, e["max_norm"]), max(worst_rms, e["rms_rel"])
         o1 = n1.forward(o0)
         assert o1["session_id"] == "s1"
         cached.append(o1["next_token_id"])
         ids = o1["generated_ids"]
-    print(f"session chain: new-row boundary hidden vs oracle worst max_norm {worst:.2e}")
+    print(f"session chain: new-row boundary hidden vs oracle worst max_norm {worst:.2e} rms_rel {worst_rms:.2e}")
     assert cached == full
-    assert worst < TOL_REL
+    assert worst < TOL_SPAN and worst_rms < TOL_SPAN_RMS
     # a request that does not extend the cached prefix restarts the session
     o1 = n1.forward(n0.forward({"generated_ids": prompt, "session_id": "s1"}))
     assert o1["next_token_id"] == full[0]
     c = n1.forward(n0.forward({"session_id": "s1", "close_session": True}))
     assert c == {"session_id": "s1", "closed": True}
     assert n0.span.pool.n_free == free0 and n1.span.pool.n_free == free1
-    record("nn_forward_session_vs_full", steps=16, identical=True, new_row_hidden_vs_oracle_worst_max_norm=worst)
+    record("nn_forward_session_vs_full", steps=16, identical=True, new_row_hidden_vs_oracle_worst_max_norm=worst,
+           new_row_hidden_vs_oracle_worst_rms_rel=worst_rms)
 
 
 def test_nn_forward_long_prompt_chunked(q06_peaked):
@@ -206,7 +218,7 @@ def test_nn_forward_long_prompt_chunked(q06_peaked):
     print(f"T={T}: gpu {o1['next_token_id']} / session {os1['next_token_id']} ref {rid} margin "
           f"{R.top2_margin(lg):.3f}; boundary rows max_norm {e['max_norm']:.2e}")
     assert o1["next_token_id"] == rid and os1["next_token_id"] == rid
-    assert e["max_norm"] < TOL_REL
+    assert span_ok(e), e
     n1.forward(n0.forward({"session_id": "long", "close_session": True}))
     record("nn_forward_long_prompt", tokens=T, boundary_rows_err=e, token_ok=True)
 
@@ -222,7 +234,7 @@ def test_stage_modules_all_positions_and_bad_ids(q06_peaked):
     assert lg.shape == (1, 6, 151936)
     ref = b1.forward(b0.forward(ids))
     e = errs(lg[0], ref[0])
-    assert e["max_norm"] < TOL_REL, e
+    assert span_ok(e), e
     with pytest.raises(IndexError):
         n0.forward({"generated_ids": [1, 2, 151936]})
     with pytest.raises(IndexError):
@@ -385,8 +397,8 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes):
     h = pipe["hidden"].reshape(2, T8, -1)
     e = [errs(h[b], ref[b]) for b in range(2)]
     print(f"{sizes}: ids identical over {STEPS8} steps x {world} microbatches; stage-0 boundary "
-          f"max_norm {[x['max_norm'] for x in e]}")
-    assert all(x["max_norm"] < TOL_REL for x in e)
+          f"max_norm {[x['max_norm'] for x in e]} rms_rel {[x['rms_rel'] for x in e]}")
+    assert all(span_ok(x) for x in e)
     record(f"q8b_pipeline_{'-'.join(map(str, sizes))}", ids_identical=True, decode_steps=STEPS8,
            microbatches=world, boundary_err=e)
 
