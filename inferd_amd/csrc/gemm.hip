@@ -75,7 +75,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   __shared__ float sm_ss[NORM == DN_FOLD ? NW : 1][MT * 16];
   __shared__ __attribute__((aligned(16))) float sm_r[NORM == DN_EXACT ? NW * 256 : 4];
   // DN_EXACT: this workgroup's K range of the norm weight, staged once (<= 8192 columns)
-  __shared__ __attribute__((aligned(16))) u16 sm_w[NORM == DN_EXACT ? DECODE_NORM_MAXK : 8];
+  __shared__ __attribute__((aligned(16))) u16 sm_w[NORM == DN_EXACT ? DECODE_NORM_MAXK + NW * 512 : 8];
   const int M = g.M;
   const int nt = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -116,10 +116,12 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
       for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
   };
   if (b < nb) {
-    // prologue: stages 0..D-2 (the weight bytes are in flight while the row scales reduce)
+    // prologue: stages 0..D-2; with DN_EXACT all D stages (the row scales are waited for
+    // before the first step, so the step-0 issue of stage D-1 would come one round trip late;
+    // here it goes out with the rest and step 0 skips its issue)
     [&]<int... I>(std::integer_sequence<int, I...>) {
       ((b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
-    }(std::make_integer_sequence<int, D - 1>{});
+    }(std::make_integer_sequence<int, NORM == DN_EXACT ? D : D - 1>{});
   }
   // DN_EXACT operands, issued right behind the weight prologue (one round trip for both):
   // the partial sums of squares of the M rows -- thread t takes row quad t / PP (QM =
@@ -129,26 +131,27 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NT = NW * 64;
   constexpr int WCH = (DECODE_NORM_MAXK / 8 + NT - 1) / NT;
   f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-  u16x8 wst[NORM == DN_EXACT ? WCH : 1];
   const int QM = (M + 3) >> 2;
   int PP = NT;
   while (PP * QM > NT) PP >>= 1;
   const int GL = PP < 64 ? PP : 64;  // lanes of one shuffle-reduction group
   if constexpr (NORM == DN_EXACT) {
-    // unconditional loads of clamped addresses (no branches between the loads and the
-    // weight prologue: a predicated load here made hipcc drain vmcnt early)
+    // the norm weight goes straight to LDS (LDS-DMA, no registers: the whole ring is live here)
 #pragma unroll
     for (int i = 0; i < WCH; ++i) {
-      const int c = min((int)threadIdx.x + i * NT, KT * 4 - 1);
-      wst[i] = *(const u16x8*)(g.norm_w + kt0 * 32 + c * 8);
+      if (i * NT < KT * 4) {
+        const int c = min((int)threadIdx.x + i * NT, KT * 4 - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8),
+                                         (void*)(sm_w + (i * NT + wave * 64) * 8), 16, 0, 0);
+      }
     }
     const int quad = min((int)threadIdx.x / PP, QM - 1), p0 = threadIdx.x % PP;
-    for (int base = p0; base < g.n_parts; base += 8 * PP) {
-      f32x4 v[8];
+    for (int base = p0; base < g.n_parts; base += 4 * PP) {
+      f32x4 v[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = *(const f32x4*)(g.ssq_in + min(base + i * PP, g.n_parts - 1) * 64 + 4 * quad);
+      for (int i = 0; i < 4; ++i) v[i] = *(const f32x4*)(g.ssq_in + min(base + i * PP, g.n_parts - 1) * 64 + 4 * quad);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 4; ++i)
         if (base + i * PP < g.n_parts) s4 += v[i];
     }
   }
@@ -161,11 +164,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
       for (int j = 0; j < 4; ++j) s4[j] += __shfl_xor(s4[j], o);
     }
     if ((threadIdx.x % GL) == 0) *(f32x4*)(sm_r + 4 * (threadIdx.x / GL)) = s4;
-#pragma unroll
-    for (int i = 0; i < WCH; ++i) {
-      const int c = threadIdx.x + i * NT;
-      if (c < KT * 4) *(u16x8*)(sm_w + c * 8) = wst[i];
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS-DMA of the norm weight landed
     __syncthreads();
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -185,7 +184,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
           constexpr int d = decltype(stage)::value;
           if (fin) return;
           const int nxt = b + (D - 1) * NW;
-          if (nxt < nb) issue(std::integral_constant<int, (d + D - 1) % D>{}, nxt);
+          if (nxt < nb && (NORM != DN_EXACT || b != wave)) issue(std::integral_constant<int, (d + D - 1) % D>{}, nxt);
           // keep the issued loads ahead of the MFMAs (the scheduler would otherwise
           // interleave them to save registers, leaving few loads in flight)
           __builtin_amdgcn_sched_barrier(0);

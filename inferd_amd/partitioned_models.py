@@ -302,7 +302,7 @@ class PartitionedQwen2:
                 res["generated_ids"] = gen_ids
             res.update(extra)
             return res
-        token_id = int(self.model.last_next_ids[0].item())
+        token_id = int(self.last_next_ids[0].item())
         res = {"next_token_id": token_id, "next_token_str": self.tokenizer.decode(token_id),
                "generated_ids": list(gen_ids if gen_ids is not None else []) + [token_id]}
         res.update(extra)
@@ -314,10 +314,26 @@ class PartitionedQwen2:
             return self._forward_session(inputs)
         gen_ids, model_in = self._prepare_inputs(inputs)
         T = model_in.size(1)
-        with torch.no_grad():
-            out = self.model.run([(None, T)], model_in)
-        self.span.check_errors()
+        out = self._run([(None, T)], model_in)
         return self._output(out, gen_ids, T, {})
+
+    # compute / cache hooks (inferd_amd.node_group runs them across a multi-GPU group)
+    @torch.no_grad()
+    def _run(self, requests, model_in):
+        out = self.model.run(requests, model_in)
+        self.span.check_errors()
+        return out
+
+    def _release(self, key):
+        self.span.release(key)
+
+    def _cached_len(self, key):
+        st = self.span.sessions.get(key)
+        return 0 if st is None else st.length
+
+    @property
+    def last_next_ids(self):
+        return self.model.last_next_ids
 
     # ---------------------------------------------------------------- sessions
     def _touch(self, sid, value):
@@ -325,11 +341,11 @@ class PartitionedQwen2:
         self._sessions.move_to_end(sid)
         while len(self._sessions) > self.max_sessions:
             old, _ = self._sessions.popitem(last=False)
-            self.span.release(("sess", old))
+            self._release(("sess", old))
 
     def close_session(self, sid):
         self._sessions.pop(sid, None)
-        self.span.release(("sess", sid))
+        self._release(("sess", sid))
 
     def _forward_session(self, inputs):
         sid = inputs["session_id"]
@@ -339,8 +355,7 @@ class PartitionedQwen2:
                 {"session_id": sid, "closed": True}
         gen_ids, model_in = self._prepare_inputs(inputs)
         key = ("sess", sid)
-        cached = self.span.sessions.get(key)
-        past = 0 if cached is None else cached.length
+        past = self._cached_len(key)
         if self.stage == 0:
             seen = self._sessions.get(sid)
             ids = model_in.reshape(-1).tolist()
@@ -358,15 +373,14 @@ class PartitionedQwen2:
                 past = 0
             new = model_in
         n = new.shape[1]
-        with torch.no_grad():
-            for attempt in range(self.max_sessions + 1):
-                try:
-                    out = self.model.run([(key, n)], new)
-                    break
-                except RuntimeError as e:
-                    if "KV pool exhausted" not in str(e) or not self._evict_other(sid):
-                        raise
-        self.span.check_errors()
+        while True:   # make room first: a full pool evicts the least recently used session
+            try:
+                self.span.reserve(key, n)
+                break
+            except RuntimeError as e:
+                if "KV pool exhausted" not in str(e) or not self._evict_other(sid):
+                    raise
+        out = self._run([(key, n)], new)
         self._touch(sid, (model_in.reshape(-1).tolist() if self.stage == 0 else past + n))
         return self._output(out, gen_ids, n, {"session_id": sid, "past_len": past})
 

@@ -297,3 +297,15 @@ def test_peaked_profile_oracle_definition():
     assert torch.equal(q["lm_head"][int(p[t])], (g["lm_head"][int(p[t])].float() + wg.LM_MIX *
                                                   g["embed_tokens"][t].float()).to(torch.bfloat16))
     assert torch.equal(q["norm"], g["norm"]) and np.all(np.diff(np.sort(p)) == 1)
+
+
+def test_node_group_split_and_stage_range():
+    """A grouped stage's layers are split by decode bytes with the lm_head on the last rank."""
+    from inferd_amd.node_group import group_split, stage_range
+    from inferd_amd.runtime import MODELS
+    d, s, e, prof = stage_range("synthetic:1:qwen3-8b:0:17:peaked", "x", 2, 0)
+    assert (d.name, s, e, prof) == ("qwen3-8b", 0, 17, "peaked")
+    sp = group_split(MODELS["qwen3-8b"], 18, 4, lm_head=True)
+    sizes = [n for _, n in sp]
+    assert sum(sizes) == 18 and sizes[-1] < sizes[0]
+    assert [n for _, n in group_split(MODELS["qwen3-8b"], 18, 3, lm_head=False)] == [6, 6, 6]
