@@ -28,6 +28,16 @@
 
 __device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g)); }
 
+// sum over the 16 lanes of a DPP row (lanes 16k .. 16k+15), in every lane: rotations by 8, 4,
+// 2, 1 (row_ror DPP moves, no LDS); a fixed tree, so the result is deterministic
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false));
+  return v;
+}
+
 // ============================================================ decode (M <= 64) kernel
 // RMSNorm modes of the decode GEMV (NORM template argument, kernels.h DN_*):
 //  DN_NONE  A used as is;
@@ -67,13 +77,33 @@ struct DecodeArgs {
 };
 
 #define DECODE_NORM_MAXK 8192  // DN_EXACT: K of one workgroup (hidden <= 8192)
+// tools/decode_gemv_lab.hip builds this file with DN_PROBE set to time the parts of DN_EXACT
+// (1: no row-scale work, 2: no A-fragment normalisation, 3: no norm wave, 4: the usual D-1
+// stage prologue, 5: weights before activations in a stage); the library builds it with 0
+#ifndef DN_PROBE
+#define DN_PROBE 0
+#endif
+
+// DN_EXACT workgroups carry one extra "norm wave" (wave NW): it alone loads and reduces the
+// row sums of squares and stages the norm weight, so the NW streaming waves issue their whole
+// weight prologue at once and wait for the row scales on a raw barrier -- their vmcnt never
+// includes those loads (a wave that waited for its own row-scale loads had to drain its weight
+// stages behind them, since vmcnt retires in order; so does __syncthreads: +3-4 us per launch)
+template <int NORM>
+constexpr bool dn_norm_wave() {
+  return NORM == DN_EXACT && DN_PROBE != 3;
+}
+template <int NW, int NORM>
+constexpr int decode_threads() {
+  return (NW + (dn_norm_wave<NORM>() ? 1 : 0)) * 64;
+}
 
 template <int MT, int S, int NW, int TW, int D, int EPI, int NORM>
-__global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
+__global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
   __shared__ float sm_ss[NORM == DN_FOLD ? NW : 1][MT * 16];
-  __shared__ __attribute__((aligned(16))) float sm_r[NORM == DN_EXACT ? NW * 256 : 4];
+  __shared__ __attribute__((aligned(16))) float sm_r[NORM == DN_EXACT ? 64 : 4];
   // DN_EXACT: this workgroup's K range of the norm weight, staged once (<= 8192 columns)
   __shared__ __attribute__((aligned(16))) u16 sm_w[NORM == DN_EXACT ? DECODE_NORM_MAXK + NW * 512 : 8];
   const int M = g.M;
@@ -103,80 +133,102 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
   const int nb = KT / TW;  // batches (the dispatcher guarantees KT % TW == 0)
   int b = wave;
   bf16x8 wv[D][S][TW], av[D][TW][MT];
+  // DN_EXACT: a stage's activation fragments are issued BEFORE its weights, so the
+  // normalisation of A can run as soon as A (L2) lands, while the weight bytes (HBM) are
+  // still in flight (vmcnt retires in issue order)
+  constexpr bool A_FIRST = NORM == DN_EXACT && DN_PROBE != 5;
+  constexpr bool FULL_PROLOGUE = NORM == DN_EXACT && DN_PROBE != 4;
   auto issue = [&](auto stage, int bb) {
     constexpr int d = decltype(stage)::value;
+    if constexpr (A_FIRST) {
+#pragma unroll
+      for (int u = 0; u < TW; ++u)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
+    }
 #pragma unroll
     for (int u = 0; u < TW; ++u) {
       wv[d][0][u] = __builtin_nontemporal_load(w0 + (bb * TW + u) * 64);
       if constexpr (S == 2) wv[d][1][u] = __builtin_nontemporal_load(w1 + (bb * TW + u) * 64);
     }
+    if constexpr (!A_FIRST) {
 #pragma unroll
-    for (int u = 0; u < TW; ++u)
+      for (int u = 0; u < TW; ++u)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
+        for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
+    }
   };
-  if (b < nb) {
-    // prologue: stages 0..D-2; with DN_EXACT all D stages (the row scales are waited for
-    // before the first step, so the step-0 issue of stage D-1 would come one round trip late;
-    // here it goes out with the rest and step 0 skips its issue)
-    [&]<int... I>(std::integer_sequence<int, I...>) {
-      ((b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
-    }(std::make_integer_sequence<int, NORM == DN_EXACT ? D : D - 1>{});
-  }
-  // DN_EXACT operands, issued right behind the weight prologue (one round trip for both):
-  // the partial sums of squares of the M rows -- thread t takes row quad t / PP (QM =
-  // ceil(M / 4) quads, PP = the largest power of two <= threads / QM part lanes each) and
-  // parts t % PP, t % PP + PP, ..., eight independent 16-B loads at a time -- and this
-  // thread's chunks of the norm weight
-  constexpr int NT = NW * 64;
-  constexpr int WCH = (DECODE_NORM_MAXK / 8 + NT - 1) / NT;
-  f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-  const int QM = (M + 3) >> 2;
-  int PP = NT;
-  while (PP * QM > NT) PP >>= 1;
-  const int GL = PP < 64 ? PP : 64;  // lanes of one shuffle-reduction group
-  if constexpr (NORM == DN_EXACT) {
-    // the norm weight goes straight to LDS (LDS-DMA, no registers: the whole ring is live here)
+  float rr[MT];  // DN_EXACT: r of row mt*16 + (lane & 15)
 #pragma unroll
-    for (int i = 0; i < WCH; ++i) {
-      if (i * NT < KT * 4) {
-        const int c = min((int)threadIdx.x + i * NT, KT * 4 - 1);
-        __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8),
-                                         (void*)(sm_w + (i * NT + wave * 64) * 8), 16, 0, 0);
+  for (int mt = 0; mt < MT; ++mt) rr[mt] = 1.0f;
+  if constexpr (dn_norm_wave<NORM>()) {
+    if (wave == NW) {
+      // the norm wave: the norm weight of this workgroup's K range straight to LDS
+      // (LDS-DMA), then the M rows' partial sums of squares: lane l takes row quad l / PPW
+      // (QM = ceil(M / 4) quads, PPW = the largest power of two <= 64 / QM lanes each) and
+      // parts l % PPW, l % PPW + PPW, ... (sixteen 16-B loads in flight), a butterfly over the
+      // PPW lanes (fixed order: deterministic), r = 1 / sqrt(sum / K + eps) into LDS.  Its
+      // loads go out BEFORE the streaming waves' weight prologue (first barrier): issued
+      // behind the prologue they queued behind the HBM misses in the CU's memory pipeline
+      const int QM = (M + 3) >> 2;
+      int PPW = 64;
+      while (PPW * QM > 64) PPW >>= 1;
+      const int quad = min(lane / PPW, QM - 1), p0 = lane % PPW;
+      f32x4 v[16];
+      if constexpr (DN_PROBE != 1) {
+        for (int c = lane; c < KT * 4; c += 64)
+          __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8),
+                                           (void*)(sm_w + (c - lane) * 8), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)(g.ssq_in + min(p0 + i * PPW, g.n_parts - 1) * 64 + 4 * quad);
+      }
+      raw_barrier();  // #1: the row-scale loads are out; the streaming waves may issue theirs
+      if constexpr (DN_PROBE != 1) {
+        f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (p0 + i * PPW < g.n_parts) s4 += v[i];
+        for (int base = p0 + 16 * PPW; base < g.n_parts; base += PPW)   // M > 16 rows only
+          s4 += *(const f32x4*)(g.ssq_in + base * 64 + 4 * quad);
+        for (int o = 1; o < PPW; o <<= 1) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s4[j] += __shfl_xor(s4[j], o);
+        }
+        if (p0 == 0 && lane / PPW < QM) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sm_r[4 * quad + j] = 1.0f / sqrtf(s4[j] / (float)(g.KT * 32) + g.eps);
+        }
+        // the LDS-DMA and the sm_r stores complete before the barrier releases the others
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      raw_barrier();  // #2: row scales and norm weight in LDS
+    } else {
+      raw_barrier();  // #1
+      // prologue: all D stages (the step-0 issue of stage D-1 would wait behind barrier #2;
+      // here it goes out with the rest and step 0 skips its issue); batch indexes clamped (a
+      // wave without those batches loads valid bytes it never uses)
+      [&]<int... I>(std::integer_sequence<int, I...>) {
+        (issue(std::integral_constant<int, I>{}, min(b + I * NW, nb - 1)), ...);
+      }(std::make_integer_sequence<int, FULL_PROLOGUE ? D : D - 1>{});
+      // a barrier that does not drain vmcnt: __syncthreads() would first wait for every
+      // weight load just issued
+      raw_barrier();  // #2
+      if constexpr (DN_PROBE != 1) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) rr[mt] = sm_r[mt * 16 + (lane & 15)];
       }
     }
-    const int quad = min((int)threadIdx.x / PP, QM - 1), p0 = threadIdx.x % PP;
-    for (int base = p0; base < g.n_parts; base += 4 * PP) {
-      f32x4 v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = *(const f32x4*)(g.ssq_in + min(base + i * PP, g.n_parts - 1) * 64 + 4 * quad);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (base + i * PP < g.n_parts) s4 += v[i];
-    }
+  } else if (FULL_PROLOGUE) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      (issue(std::integral_constant<int, I>{}, min(b + I * NW, nb - 1)), ...);
+    }(std::make_integer_sequence<int, D>{});
+  } else if (b < nb) {
+    // prologue: stages 0..D-2
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      ((b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
+    }(std::make_integer_sequence<int, D - 1>{});
   }
-  float rr[MT];  // DN_EXACT: r of row mt*16 + (lane & 15)
-  if constexpr (NORM == DN_EXACT) {
-    // butterfly over each group of GL part lanes (fixed pattern: deterministic), then the
-    // group leaders' sums in LDS, PP / GL groups per quad added in order below
-    for (int o = 1; o < GL; o <<= 1) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s4[j] += __shfl_xor(s4[j], o);
-    }
-    if ((threadIdx.x % GL) == 0) *(f32x4*)(sm_r + 4 * (threadIdx.x / GL)) = s4;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS-DMA of the norm weight landed
-    __syncthreads();
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int rw = mt * 16 + (lane & 15);
-      float s = 0.f;
-      const int ng = PP / GL, g0 = (rw >> 2) * ng;
-      if (rw < M)
-        for (int q = 0; q < ng; ++q) s += sm_r[4 * (g0 + q) + (rw & 3)];
-      rr[mt] = 1.0f / sqrtf(s / (float)(g.KT * 32) + g.eps);
-    }
-  }
-  if (b < nb) {
+  if (b < nb && (!dn_norm_wave<NORM>() || wave < NW)) {
     bool fin = false;
     while (!fin) {
       [&]<int... I>(std::integer_sequence<int, I...>) {
@@ -184,11 +236,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
           constexpr int d = decltype(stage)::value;
           if (fin) return;
           const int nxt = b + (D - 1) * NW;
-          if (nxt < nb && (NORM != DN_EXACT || b != wave)) issue(std::integral_constant<int, (d + D - 1) % D>{}, nxt);
+          if (nxt < nb && (!FULL_PROLOGUE || b != wave)) issue(std::integral_constant<int, (d + D - 1) % D>{}, nxt);
           // keep the issued loads ahead of the MFMAs (the scheduler would otherwise
           // interleave them to save registers, leaving few loads in flight)
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (NORM == DN_EXACT) {
+          if constexpr (NORM == DN_EXACT && DN_PROBE != 2) {
 #pragma unroll
             for (int u = 0; u < TW; ++u) {
               const u16x8 nv = *(const u16x8*)(sm_w + (b * TW + u) * 32 + 8 * (lane >> 4));
@@ -226,10 +278,12 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
       }(std::make_integer_sequence<int, D>{});
     }
   }
+  if (!dn_norm_wave<NORM>() || wave < NW) {
 #pragma unroll
-  for (int s = 0; s < S; ++s)
+    for (int s = 0; s < S; ++s)
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) red[wave][(s * MT + mt) * 64 + lane] = acc[s][mt];
+      for (int mt = 0; mt < MT; ++mt) red[wave][(s * MT + mt) * 64 + lane] = acc[s][mt];
+  }
   if constexpr (NORM == DN_FOLD) {
     // lanes l, l^16, l^32, l^48 hold the four k-quarters of row (l & 15)
 #pragma unroll
@@ -306,9 +360,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_decode_kernel(DecodeArgs g) {
       const u16 ob = live ? f2bf(rbf(v[0][r]) + bf2f(g.R[(int64_t)row * g.ldr + col])) : (u16)0;
       if (live) g.C[(int64_t)row * g.ldc + col] = ob;
       if (g.ssq_out) {
-        float q = bf2f(ob) * bf2f(ob);
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) q += __shfl_xor(q, o, 16);
+        const float q = row16_sum(bf2f(ob) * bf2f(ob));
         if (live && (ln & 15) == 0) g.ssq_out[nt * 64 + row] = q;
       }
     } else if (row < M) {
@@ -337,12 +389,12 @@ template <int MT, int EPI, int NORM>
 static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   using C = DecodeCfg<MT, S>;
+  constexpr int T = decode_threads<C::NW, NORM>();
   if (a.KT % C::TW == 0)
-    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM>), dim3(a.n_tiles),
-                       dim3(C::NW * 64), 0, s, a);
+    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM>), dim3(a.n_tiles), dim3(T), 0, s,
+                       a);
   else  // odd K/32 (single-op API only; every Qwen3 projection has K % 128 == 0)
-    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM>), dim3(a.n_tiles), dim3(C::NW * 64), 0,
-                       s, a);
+    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM>), dim3(a.n_tiles), dim3(T), 0, s, a);
 }
 
 template <int EPI, int NORM>
@@ -379,7 +431,8 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
   a.norm_w = norm.w;
   const dim3 grid(N / 16, kslices);
   if (norm.mode == DN_EXACT)
-    hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT>), grid,
+                       dim3(decode_threads<4, DN_EXACT>()), 0, s, a);
   else if (norm.mode == DN_FOLD)
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_FOLD>), grid, dim3(256), 0, s, a);
   else
