@@ -98,20 +98,42 @@ constexpr int decode_threads() {
   return (NW + (dn_norm_wave<NORM>() ? 1 : 0)) * 64;
 }
 
+// dynamic LDS of a DN_EXACT workgroup over KT 32-column steps: the bf16 norm weight (plus its
+// fp32 image in one-stream kernels; gemm_decode_kernel's dn_lds)
+template <int NORM, int S>
+constexpr unsigned dn_lds_bytes(int KT) {
+  return NORM == DN_EXACT ? (unsigned)KT * (S == 1 ? 192u : 64u) : 0u;
+}
+
 template <int MT, int S, int NW, int TW, int D, int EPI, int NORM>
 __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
   __shared__ float sm_ss[NORM == DN_FOLD ? NW : 1][MT * 16];
   __shared__ __attribute__((aligned(16))) float sm_r[NORM == DN_EXACT ? 64 : 4];
-  // DN_EXACT: this workgroup's K range of the norm weight, staged once (<= 8192 columns)
-  __shared__ __attribute__((aligned(16))) u16 sm_w[NORM == DN_EXACT ? DECODE_NORM_MAXK + NW * 512 : 8];
+  // DN_EXACT (dynamic LDS, dn_lds_bytes): this workgroup's K range of the norm weight as loaded
+  // (bf16, sm_wb, KT * 32) and, for one-stream kernels, as fp32 (sm_w: saves the streaming
+  // waves one unpack per element; the two-stream kernels amortise the unpack over two MFMAs
+  // and have no registers to spare for the wider reads)
+  extern __shared__ __attribute__((aligned(16))) float dn_lds[];
+  constexpr bool W_F32 = S == 1;
+  float* const sm_w = dn_lds;
   const int M = g.M;
   const int nt = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // K range of this workgroup (all of K unless EPI_PARTIAL splits it over gridDim.y)
   const int kt0 = (EPI == EPI_PARTIAL) ? (int)blockIdx.y * (g.KT / (int)gridDim.y) : 0;
   const int KT = (EPI == EPI_PARTIAL) ? g.KT / (int)gridDim.y : g.KT;
+  u16* const sm_wb = (u16*)(dn_lds + (W_F32 ? KT * 32 : 0));
+  // Two ring forms.  The exact-norm kernels (PADDED) load through buffer descriptors: a batch
+  // index past the wave's last batch becomes an out-of-range offset (the load returns zeros),
+  // every step issues unconditionally and the loop runs whole passes of straight-line code, so
+  // hipcc's waitcnt pass counts exactly (a conditional issue makes it merge the issued and
+  // not-issued paths and wait with the smallest count: with the norm wave's barriers in the
+  // same kernel that drained the ring every pass, 14.55 -> 14.19 us for the Qwen3-8B q/k/v).
+  // The other kernels keep global loads with the issue guarded: out-of-range loads are not
+  // free (padding their short streams to whole passes cost 10-25 %: o 8.8 -> 10.1 us,
+  // lm_head 232 -> 287 us), and there the merged waits cost less than the padding.
   const bf16x8* w0 = (const bf16x8*)(g.Wp + ((int64_t)nt * g.KT + kt0) * 512) + lane;
   const bf16x8* w1 = (const bf16x8*)(g.Wp + ((int64_t)(nt + g.n_tiles) * g.KT + kt0) * 512) + lane;
   const u16* a[MT];
@@ -121,6 +143,20 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
     row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
     a[mt] = g.A + (int64_t)row * g.lda + 8 * (lane >> 4) + kt0 * 32;
   }
+  const __amdgpu_buffer_rsrc_t w0r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.Wp + ((int64_t)nt * g.KT + kt0) * 512), 0, KT * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.Wp + ((int64_t)(nt + g.n_tiles) * g.KT + kt0) * 512), 0, KT * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.A + kt0 * 32), 0, (int)(((int64_t)(M - 1) * g.lda + KT * 32) * 2), 0x00020000);
+  int a_off[MT];  // byte offset of this lane's A fragment (k step 0) from ar
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    int row = mt * 16 + (lane & 15);
+    row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
+    a_off[mt] = (int)(((int64_t)row * g.lda + 8 * (lane >> 4)) * 2);
+  }
+  constexpr int OOB = 0x40000000;  // beyond every descriptor's range
   f32x4 acc[S][MT];
 #pragma unroll
   for (int s = 0; s < S; ++s)
@@ -131,40 +167,68 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   for (int mt = 0; mt < MT; ++mt) ssq[mt] = 0.f;
 
   const int nb = KT / TW;  // batches (the dispatcher guarantees KT % TW == 0)
-  int b = wave;
+  const int swave = __builtin_amdgcn_readfirstlane(wave);
+  int b = swave;
+  // this wave's batches b, b + NW, ... < nb
+  const int nbw = swave < nb ? (nb - swave + NW - 1) / NW : 0;
   bf16x8 wv[D][S][TW], av[D][TW][MT];
   // DN_EXACT: a stage's activation fragments are issued BEFORE its weights, so the
   // normalisation of A can run as soon as A (L2) lands, while the weight bytes (HBM) are
   // still in flight (vmcnt retires in issue order)
   constexpr bool A_FIRST = NORM == DN_EXACT && DN_PROBE != 5;
   constexpr bool FULL_PROLOGUE = NORM == DN_EXACT && DN_PROBE != 4;
+  constexpr bool PADDED = NORM == DN_EXACT;
   auto issue = [&](auto stage, int bb) {
     constexpr int d = decltype(stage)::value;
-    if constexpr (A_FIRST) {
+    if constexpr (!PADDED) {
+      if constexpr (A_FIRST) {
+#pragma unroll
+        for (int u = 0; u < TW; ++u)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
+      }
+#pragma unroll
+      for (int u = 0; u < TW; ++u) {
+        wv[d][0][u] = __builtin_nontemporal_load(w0 + (bb * TW + u) * 64);
+        if constexpr (S == 2) wv[d][1][u] = __builtin_nontemporal_load(w1 + (bb * TW + u) * 64);
+      }
+      if constexpr (!A_FIRST) {
+#pragma unroll
+        for (int u = 0; u < TW; ++u)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
+      }
+      return;
+    }
+    const bool live = bb < nb;
+    const int wo = (live ? bb * TW * 1024 : OOB) + lane * 16;
+    const int ao = live ? bb * TW * 64 : OOB;
+    auto load_a = [&]() {
 #pragma unroll
       for (int u = 0; u < TW; ++u)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
-    }
+        for (int mt = 0; mt < MT; ++mt)
+          av[d][u][mt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ar, a_off[mt] + ao + u * 64, 0, 0));
+    };
+    if constexpr (A_FIRST) load_a();
 #pragma unroll
-    for (int u = 0; u < TW; ++u) {
-      wv[d][0][u] = __builtin_nontemporal_load(w0 + (bb * TW + u) * 64);
-      if constexpr (S == 2) wv[d][1][u] = __builtin_nontemporal_load(w1 + (bb * TW + u) * 64);
+    for (int u = 0; u < TW; ++u) {  // weights: nt (read once per step)
+      wv[d][0][u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w0r, wo + u * 1024, 0, 2));
+      if constexpr (S == 2)
+        wv[d][1][u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w1r, wo + u * 1024, 0, 2));
     }
-    if constexpr (!A_FIRST) {
-#pragma unroll
-      for (int u = 0; u < TW; ++u)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
-    }
+    if constexpr (!A_FIRST) load_a();
+    // stages stay in issue order (the prologue's too: the loop's counted waits assume it)
+    __builtin_amdgcn_sched_barrier(0);
   };
+  static_assert(!FULL_PROLOGUE || PADDED, "the full prologue issues unguarded");
   float rr[MT];  // DN_EXACT: r of row mt*16 + (lane & 15)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) rr[mt] = 1.0f;
   if constexpr (dn_norm_wave<NORM>()) {
     if (wave == NW) {
-      // the norm wave: the norm weight of this workgroup's K range straight to LDS
-      // (LDS-DMA), then the M rows' partial sums of squares: lane l takes row quad l / PPW
+      // the norm wave: the norm weight of this workgroup's K range (to LDS as fp32), then
+      // the M rows' partial sums of squares: lane l takes row quad l / PPW
       // (QM = ceil(M / 4) quads, PPW = the largest power of two <= 64 / QM lanes each) and
       // parts l % PPW, l % PPW + PPW, ... (sixteen 16-B loads in flight), a butterfly over the
       // PPW lanes (fixed order: deterministic), r = 1 / sqrt(sum / K + eps) into LDS.  Its
@@ -174,16 +238,31 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       int PPW = 64;
       while (PPW * QM > 64) PPW >>= 1;
       const int quad = min(lane / PPW, QM - 1), p0 = lane % PPW;
+      // every load of the norm wave is an LDS-DMA (no VGPRs held across the barrier: the
+      // kernel's register budget is the streaming waves')
       f32x4 v[16];
       if constexpr (DN_PROBE != 1) {
         for (int c = lane; c < KT * 4; c += 64)
           __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8),
-                                           (void*)(sm_w + (c - lane) * 8), 16, 0, 0);
+                                           (void*)(sm_wb + (c - lane) * 8), 16, 0, 0);
 #pragma unroll
         for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)(g.ssq_in + min(p0 + i * PPW, g.n_parts - 1) * 64 + 4 * quad);
       }
       raw_barrier();  // #1: the row-scale loads are out; the streaming waves may issue theirs
       if constexpr (DN_PROBE != 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (W_F32)
+        for (int c = lane; c < KT * 4; c += 64) {
+          const u16x8 nv = *(const u16x8*)(sm_wb + c * 8);
+          f32x4 lo, hi;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            lo[j] = bf2f(nv[j]);
+            hi[j] = bf2f(nv[4 + j]);
+          }
+          *(f32x4*)(sm_w + c * 8) = lo;
+          *(f32x4*)(sm_w + c * 8 + 4) = hi;
+        }
         f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int i = 0; i < 16; ++i)
@@ -198,17 +277,16 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
 #pragma unroll
           for (int j = 0; j < 4; ++j) sm_r[4 * quad + j] = 1.0f / sqrtf(s4[j] / (float)(g.KT * 32) + g.eps);
         }
-        // the LDS-DMA and the sm_r stores complete before the barrier releases the others
+        // the norm weight and sm_r stores complete before the barrier releases the others
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
       raw_barrier();  // #2: row scales and norm weight in LDS
     } else {
       raw_barrier();  // #1
       // prologue: all D stages (the step-0 issue of stage D-1 would wait behind barrier #2;
-      // here it goes out with the rest and step 0 skips its issue); batch indexes clamped (a
-      // wave without those batches loads valid bytes it never uses)
+      // here it goes out with the rest and step 0 skips its issue)
       [&]<int... I>(std::integer_sequence<int, I...>) {
-        (issue(std::integral_constant<int, I>{}, min(b + I * NW, nb - 1)), ...);
+        (issue(std::integral_constant<int, I>{}, b + I * NW), ...);
       }(std::make_integer_sequence<int, FULL_PROLOGUE ? D : D - 1>{});
       // a barrier that does not drain vmcnt: __syncthreads() would first wait for every
       // weight load just issued
@@ -218,64 +296,91 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
         for (int mt = 0; mt < MT; ++mt) rr[mt] = sm_r[mt * 16 + (lane & 15)];
       }
     }
-  } else if (FULL_PROLOGUE) {
+  } else if (nbw > 0) {
+    // prologue: stages 0..D-2 (all D with FULL_PROLOGUE)
     [&]<int... I>(std::integer_sequence<int, I...>) {
-      (issue(std::integral_constant<int, I>{}, min(b + I * NW, nb - 1)), ...);
-    }(std::make_integer_sequence<int, D>{});
-  } else if (b < nb) {
-    // prologue: stages 0..D-2
-    [&]<int... I>(std::integer_sequence<int, I...>) {
-      ((b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
-    }(std::make_integer_sequence<int, D - 1>{});
+      ((PADDED || b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
+    }(std::make_integer_sequence<int, FULL_PROLOGUE ? D : D - 1>{});
   }
-  if (b < nb && (!dn_norm_wave<NORM>() || wave < NW)) {
+  if (nbw > 0 && (!dn_norm_wave<NORM>() || wave < NW)) {
+    // one step: issue the batch D-1 steps ahead into the slot this step's predecessor freed,
+    // then consume slot d.  With FULL_PROLOGUE the first step's issue went out with the
+    // prologue, so that step is peeled (no issue) and the loop runs the slots rotated by one
     bool fin = false;
-    while (!fin) {
-      [&]<int... I>(std::integer_sequence<int, I...>) {
-        auto step = [&](auto stage) {
-          constexpr int d = decltype(stage)::value;
-          if (fin) return;
-          const int nxt = b + (D - 1) * NW;
-          if (nxt < nb && (!FULL_PROLOGUE || b != wave)) issue(std::integral_constant<int, (d + D - 1) % D>{}, nxt);
-          // keep the issued loads ahead of the MFMAs (the scheduler would otherwise
-          // interleave them to save registers, leaving few loads in flight)
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (NORM == DN_EXACT && DN_PROBE != 2) {
+    auto step = [&](auto stage, auto may_issue) {
+      constexpr int d = decltype(stage)::value;
+      if constexpr (!PADDED) {
+        if (fin) return;
+        const int nxt = b + (D - 1) * NW;
+        if (nxt < nb) issue(std::integral_constant<int, (d + D - 1) % D>{}, nxt);
+      } else if constexpr (decltype(may_issue)::value) {
+        issue(std::integral_constant<int, (d + D - 1) % D>{}, b + (D - 1) * NW);
+      }
+      // keep the issued loads ahead of the MFMAs (the scheduler would otherwise
+      // interleave them to save registers, leaving few loads in flight)
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NORM == DN_EXACT && DN_PROBE != 2) {
 #pragma unroll
-            for (int u = 0; u < TW; ++u) {
-              const u16x8 nv = *(const u16x8*)(sm_w + (b * TW + u) * 32 + 8 * (lane >> 4));
+        for (int u = 0; u < TW; ++u) {
+          const int wo = (min(b, nb - 1) * TW + u) * 32 + 8 * (lane >> 4);
+          float wf[8];
+          if constexpr (W_F32) {
+            const f32x4 w_lo = *(const f32x4*)(sm_w + wo), w_hi = *(const f32x4*)(sm_w + wo + 4);
 #pragma unroll
-              for (int mt = 0; mt < MT; ++mt) {
-                const u16x8 xv = __builtin_bit_cast(u16x8, av[d][u][mt]);
-                bf16x8 y;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) y[j] = (__bf16)(bf2f(nv[j]) * rbf(bf2f(xv[j]) * rr[mt]));
-                av[d][u][mt] = y;
-              }
+            for (int j = 0; j < 4; ++j) {
+              wf[j] = w_lo[j];
+              wf[4 + j] = w_hi[j];
             }
+          } else {
+            const u16x8 nv = *(const u16x8*)(sm_wb + wo);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wf[j] = bf2f(nv[j]);
           }
 #pragma unroll
-          for (int u = 0; u < TW; ++u)
+          for (int mt = 0; mt < MT; ++mt) {
+            const u16x8 xv = __builtin_bit_cast(u16x8, av[d][u][mt]);
+            bf16x8 y;
 #pragma unroll
-            for (int s = 0; s < S; ++s)
-#pragma unroll
-              for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[d][u][mt], wv[d][s][u], acc[s][mt]);
-          if constexpr (NORM == DN_FOLD) {
-#pragma unroll
-            for (int u = 0; u < TW; ++u)
-#pragma unroll
-              for (int mt = 0; mt < MT; ++mt) {
-                const u16x8 xv = __builtin_bit_cast(u16x8, av[d][u][mt]);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) ssq[mt] = fmaf(bf2f(xv[j]), bf2f(xv[j]), ssq[mt]);
-              }
+            for (int j = 0; j < 8; ++j) y[j] = (__bf16)(wf[j] * rbf(bf2f(xv[j]) * rr[mt]));
+            av[d][u][mt] = y;
           }
-          __builtin_amdgcn_sched_barrier(0);
-          b += NW;
-          if (b >= nb) fin = true;
-        };
-        (step(std::integral_constant<int, I>{}), ...);
-      }(std::make_integer_sequence<int, D>{});
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < TW; ++u)
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[d][u][mt], wv[d][s][u], acc[s][mt]);
+      if constexpr (NORM == DN_FOLD) {
+#pragma unroll
+        for (int u = 0; u < TW; ++u)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const u16x8 xv = __builtin_bit_cast(u16x8, av[d][u][mt]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ssq[mt] = fmaf(bf2f(xv[j]), bf2f(xv[j]), ssq[mt]);
+          }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      b += NW;
+      if (b >= nb) fin = true;
+    };
+    constexpr int R = FULL_PROLOGUE ? 1 : 0;  // slot rotation of the loop body
+    if constexpr (FULL_PROLOGUE) step(std::integral_constant<int, 0>{}, std::false_type{});
+    if constexpr (PADDED) {
+      // whole passes; steps past the wave's last batch consume the zeros their loads returned
+      for (int pass = (nbw - R + D - 1) / D; pass > 0; --pass) {
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          (step(std::integral_constant<int, (I + R) % D>{}, std::true_type{}), ...);
+        }(std::make_integer_sequence<int, D>{});
+      }
+    } else {
+      while (!fin) {
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          (step(std::integral_constant<int, I>{}, std::true_type{}), ...);
+        }(std::make_integer_sequence<int, D>{});
+      }
     }
   }
   if (!dn_norm_wave<NORM>() || wave < NW) {
@@ -391,10 +496,11 @@ static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   using C = DecodeCfg<MT, S>;
   constexpr int T = decode_threads<C::NW, NORM>();
   if (a.KT % C::TW == 0)
-    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM>), dim3(a.n_tiles), dim3(T), 0, s,
-                       a);
+    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM>), dim3(a.n_tiles), dim3(T),
+                       (dn_lds_bytes<NORM, S>(a.KT)), s, a);
   else  // odd K/32 (single-op API only; every Qwen3 projection has K % 128 == 0)
-    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM>), dim3(a.n_tiles), dim3(T), 0, s, a);
+    hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM>), dim3(a.n_tiles), dim3(T),
+                       (dn_lds_bytes<NORM, S>(a.KT)), s, a);
 }
 
 template <int EPI, int NORM>
@@ -432,7 +538,7 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
   const dim3 grid(N / 16, kslices);
   if (norm.mode == DN_EXACT)
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT>), grid,
-                       dim3(decode_threads<4, DN_EXACT>()), 0, s, a);
+                       dim3(decode_threads<4, DN_EXACT>()), (dn_lds_bytes<DN_EXACT, 1>(a.KT / kslices)), s, a);
   else if (norm.mode == DN_FOLD)
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_FOLD>), grid, dim3(256), 0, s, a);
   else
