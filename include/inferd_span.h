@@ -33,6 +33,7 @@ extern "C" {
 #define INFERD_ERR_ARG 1   /* bad argument / shape / unsupported configuration */
 #define INFERD_ERR_HIP 2   /* HIP runtime error (allocation, launch) */
 #define INFERD_ERR_STATE 3 /* handle not initialised / weights not ready (see set_weight) */
+#define INFERD_ERR_NOMEM 4 /* KV page pool exhausted (inferd_kv_reserve; nothing was taken) */
 
 #define INFERD_KV_PAGE_TOKENS 64
 
@@ -172,6 +173,38 @@ int inferd_span_error_flags(InferdSpan* span, int32_t* flags);
 #define INFERD_PROF_NCLASSES 8
 int inferd_span_profile_start(InferdSpan* span, int32_t max_pairs);
 int inferd_span_profile_stop(InferdSpan* span, double* total_ms, int32_t* counts, int32_t n_classes);
+
+/* ---- KV page table (host-side, no device calls).  The per-sequence page lists and cached
+ * lengths the span's paged KV pool is addressed by, and the InferdBatch a forward call reads.
+ * Replaces the reference's per-session cache bookkeeping -- session_caches[session_id], a
+ * DynamicCache appended to by every send (qwen3_server_module.py:220,253) -- and its position
+ * arithmetic: positions 0..T-1 of a stateless recompute (partitioned_models.py:139-143),
+ * cache_position = past .. past+T-1 of a cached step (client.py:244-266).  A sequence is any
+ * caller-chosen 64-bit key; pages come lowest id first, so a fixed call sequence yields fixed
+ * slots.  One table per span (kv_pages of its InferdSpanConfig). ------------------------ */
+typedef struct InferdKvTable InferdKvTable;
+int inferd_kv_create(int32_t n_pages, InferdKvTable** out);
+void inferd_kv_destroy(InferdKvTable* table);
+/* pages for n_new more tokens of `seq` (created empty if absent); all or nothing */
+int inferd_kv_reserve(InferdKvTable* table, uint64_t seq, int32_t n_new);
+/* n tokens of `seq` are now in the cache (within its reserved pages) */
+int inferd_kv_advance(InferdKvTable* table, uint64_t seq, int32_t n);
+/* drop `seq` and return its pages (absent: no-op) */
+int inferd_kv_release(InferdKvTable* table, uint64_t seq);
+/* cached length (-1: absent) and reserved page count of `seq` */
+int inferd_kv_query(const InferdKvTable* table, uint64_t seq, int32_t* length, int32_t* n_pages);
+int inferd_kv_pages(const InferdKvTable* table, uint64_t seq, int32_t* pages, int32_t cap);
+int inferd_kv_free_pages(const InferdKvTable* table, int32_t* n_free);
+/* The batch of n sequences, n_new[i] new tokens each (every seq reserved, each at most once):
+ * batch_words() is the int32 count of its descriptor (-1 on a bad request); build_batch()
+ * writes the words [seq_start | positions | slots | ctx_lens | block_table] to `host` and fills
+ * `out` with pointers into `device_base`, where the caller copies the words before the
+ * forward call.  Neither advances the sequences (inferd_kv_advance after the call). */
+int64_t inferd_kv_batch_words(const InferdKvTable* table, const uint64_t* seqs, const int32_t* n_new,
+                              int32_t n);
+int inferd_kv_build_batch(const InferdKvTable* table, const uint64_t* seqs, const int32_t* n_new,
+                          int32_t n, int32_t* host, int64_t words, const void* device_base,
+                          InferdBatch* out);
 
 /* Device base pointer of one layer's KV pool: bf16
  * [pages / 16][kv_heads][pages % 16][K|V][64*128] (super-pages of 16 pages; a pool spans

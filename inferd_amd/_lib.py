@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libinferd_span.so")
 
 INFERD_OK = 0
+INFERD_ERR_ARG, INFERD_ERR_NOMEM = 1, 4
 EPI_NONE, EPI_RESID, EPI_SILU = 0, 1, 2
 KV_PAGE = 64
 PROF_CLASSES = ("rmsnorm", "qkv_gemm", "qk_norm_rope_kv", "attention", "o_gemm", "gateup_gemm", "down_gemm",
@@ -60,6 +61,17 @@ SIGNATURES = {
     "inferd_qk_norm_rope_kv": (C.c_int, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32, c_f, c_p]),
     "inferd_attention": (C.c_int, [c_p, c_p, C.POINTER(Batch), c_i32, c_i32, c_p, c_p, c_i64, c_p]),
     "inferd_attention_workspace_bytes": (c_i64, [c_i32, c_i32, c_i32]),
+    "inferd_kv_create": (C.c_int, [c_i32, C.POINTER(c_p)]),
+    "inferd_kv_destroy": (None, [c_p]),
+    "inferd_kv_reserve": (C.c_int, [c_p, c_u64, c_i32]),
+    "inferd_kv_advance": (C.c_int, [c_p, c_u64, c_i32]),
+    "inferd_kv_release": (C.c_int, [c_p, c_u64]),
+    "inferd_kv_query": (C.c_int, [c_p, c_u64, C.POINTER(c_i32), C.POINTER(c_i32)]),
+    "inferd_kv_pages": (C.c_int, [c_p, c_u64, C.POINTER(c_i32), c_i32]),
+    "inferd_kv_free_pages": (C.c_int, [c_p, C.POINTER(c_i32)]),
+    "inferd_kv_batch_words": (c_i64, [c_p, C.POINTER(c_u64), C.POINTER(c_i32), c_i32]),
+    "inferd_kv_build_batch": (C.c_int, [c_p, C.POINTER(c_u64), C.POINTER(c_i32), c_i32, C.POINTER(c_i32), c_i64, c_p,
+                                        C.POINTER(Batch)]),
 }
 
 _lib = None
@@ -84,7 +96,10 @@ def load(path: str = LIB_PATH):
 def check(rc: int):
     if rc != INFERD_OK:
         msg = load().inferd_last_error()
-        raise RuntimeError(f"inferd error {rc}: {msg.decode() if msg else ''}")
+        msg = msg.decode() if msg else ''
+        if rc == INFERD_ERR_NOMEM:
+            raise RuntimeError(msg)
+        raise RuntimeError(f"inferd error {rc}: {msg}")
 
 
 def ptr(t) -> int | None:

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 typedef unsigned short u16;
 
 enum GemmEpilogue {
@@ -134,3 +136,6 @@ void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, 
                          float scale, u16* out, hipStream_t s, const u16* qkv = nullptr, int64_t ldqkv = 0,
                          const u16* qn_w = nullptr, const u16* cos_t = nullptr, const u16* sin_t = nullptr,
                          float eps = 0.f);
+
+// sets the thread-local message of inferd_last_error() and returns `code` (span.hip)
+int inferd_fail(int code, const std::string& msg);

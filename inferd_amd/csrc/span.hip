@@ -27,6 +27,7 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+int inferd_fail(int code, const std::string& msg) { return fail(code, msg); }
 
 #define HIP_TRY(expr)                                                                      \
   do {                                                                                     \

@@ -28,7 +28,7 @@ from __future__ import annotations
 
 import torch
 
-from .runtime import KV_PAGE, DecodeGraph, ModelDims, SpanRuntime, build_batch
+from .runtime import KV_PAGE, DecodeGraph, ModelDims, SpanRuntime
 
 
 def even_split(n_layers: int, n: int):
@@ -106,7 +106,7 @@ class SpanExecutor:
         for _ in range(n_steps):
             for m, sessions in enumerate(microbatches):
                 states = [self.span.reserve(sid, 1) for sid in sessions]
-                batch, keep = build_batch([(st, 1) for st in states], self.device)
+                batch, keep = self.span.build_batch([(st, 1) for st in states])
                 b = bufs[m]
                 self.span.run(batch, ids=b.get("ids"), x=b.get("x"), hidden=b.get("hidden_out"),
                               next_ids=b.get("next_ids"))

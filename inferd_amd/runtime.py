@@ -9,18 +9,19 @@ Semantics mirrored from the reference:
                                                         client.py:244-266
   * a session-less call is a stateless full recompute (positions 0..T-1) whose cache
     pages are released afterwards                    -- partitioned_models.py:139-151
-Device memory for activations is torch (plumbing); all compute runs in
-libinferd_span.so.
+The page table and the batch descriptors are native (inferd_kv_*, kvtable.hip); device
+memory for activations is torch (plumbing); all compute runs in libinferd_span.so.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+import ctypes as C
+import itertools
+from dataclasses import dataclass
 
-import numpy as np
 import torch
 
 from . import _lib
-from ._lib import KV_PAGE
+from ._lib import KV_PAGE  # noqa: F401  (re-exported: pipeline, tests)
 
 
 @dataclass(frozen=True)
@@ -78,64 +79,88 @@ def gen_tensor(seed: int, tid: int, shape, norm: bool, device) -> torch.Tensor:
     return t.reshape(tuple(shape))
 
 
-class PagePool:
-    """Free list over the span's KV pages (all layers of a span share page ids)."""
+class KvTable:
+    """The span's KV page table: the native one behind the C-ABI (inferd_kv_*, kvtable.hip).
+    Sequences are 64-bit keys; pages come lowest id first."""
 
     def __init__(self, n_pages: int):
+        self.lib = _lib.load()
         self.n_pages = n_pages
-        self._free = list(range(n_pages - 1, -1, -1))
+        h = _lib.c_p()
+        _lib.check(self.lib.inferd_kv_create(n_pages, h))
+        self.handle = h
 
-    def alloc(self, n: int) -> list:
-        if n > len(self._free):
-            raise RuntimeError(f"KV pool exhausted: need {n} pages, {len(self._free)} free of {self.n_pages}")
-        return [self._free.pop() for _ in range(n)]
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            self.lib.inferd_kv_destroy(h)
+            self.handle = None
 
-    def free(self, pages):
-        self._free.extend(reversed(pages))
+    def reserve(self, seq: int, n_new: int):
+        _lib.check(self.lib.inferd_kv_reserve(self.handle, seq, n_new))
+
+    def advance(self, seq: int, n: int):
+        _lib.check(self.lib.inferd_kv_advance(self.handle, seq, n))
+
+    def release(self, seq: int):
+        _lib.check(self.lib.inferd_kv_release(self.handle, seq))
+
+    def query(self, seq: int):
+        """(cached length or -1 if absent, reserved pages)"""
+        ln, npg = C.c_int32(0), C.c_int32(0)
+        _lib.check(self.lib.inferd_kv_query(self.handle, seq, C.byref(ln), C.byref(npg)))
+        return ln.value, npg.value
+
+    def pages(self, seq: int) -> list:
+        n = self.query(seq)[1]
+        buf = (C.c_int32 * max(n, 1))()
+        _lib.check(self.lib.inferd_kv_pages(self.handle, seq, buf, n))
+        return list(buf[:n])
 
     @property
     def n_free(self) -> int:
-        return len(self._free)
+        f = C.c_int32(0)
+        _lib.check(self.lib.inferd_kv_free_pages(self.handle, C.byref(f)))
+        return f.value
+
+    def build_batch(self, seqs, device):
+        """seqs: [(key, n_new)], pages already reserved.  Returns (Batch, the device int32
+        tensor backing its arrays); the words are built natively, then copied to `device`."""
+        n = len(seqs)
+        keys = (C.c_uint64 * n)(*[k for k, _ in seqs])
+        nn = (C.c_int32 * n)(*[m for _, m in seqs])
+        words = self.lib.inferd_kv_batch_words(self.handle, keys, nn, n)
+        if words < 0:
+            _lib.check(_lib.INFERD_ERR_ARG)
+        host = torch.empty(int(words), dtype=torch.int32, pin_memory=torch.device(device).type == "cuda")
+        dev = torch.empty(int(words), dtype=torch.int32, device=device)
+        b = _lib.Batch()
+        _lib.check(self.lib.inferd_kv_build_batch(self.handle, keys, nn, n,
+                                                  C.cast(host.data_ptr(), C.POINTER(C.c_int32)), words,
+                                                  dev.data_ptr(), b))
+        dev.copy_(host, non_blocking=True)
+        return b, (dev, host)
 
 
-@dataclass
-class SeqState:
-    pages: list = field(default_factory=list)
-    length: int = 0   # tokens already in the cache
+class SeqView:
+    """One sequence of a span's KvTable under a caller's session key: `length` (cached
+    tokens; assigning a larger value advances it) and `pages`, read from the native table."""
+    __slots__ = ("kv", "seq")
 
+    def __init__(self, kv: KvTable, seq: int):
+        self.kv, self.seq = kv, seq
 
-def build_batch(seqs, device):
-    """seqs: list of (SeqState, n_new) with pages already reserved.
-    Returns (Batch struct, device int32 tensor backing its arrays)."""
-    B = len(seqs)
-    M = sum(n for _, n in seqs)
-    max_pages = max(1, max(len(st.pages) for st, _ in seqs))
-    # one int32 host array [seq_start | positions | slots | ctx_lens | block_table], filled
-    # with vectorised numpy (a prefill of 8k tokens is 8k positions and slots)
-    host = np.zeros(B + 1 + 2 * M + B + B * max_pages, dtype=np.int32)
-    lens = np.array([n for _, n in seqs], dtype=np.int64)
-    host[1:B + 1] = np.cumsum(lens)
-    pos_v = host[B + 1:B + 1 + M]
-    slot_v = host[B + 1 + M:B + 1 + 2 * M]
-    ctx_v = host[B + 1 + 2 * M:B + 1 + 2 * M + B]
-    tab_v = host[B + 1 + 2 * M + B:].reshape(B, max_pages)
-    o = 0
-    for i, (st, n) in enumerate(seqs):
-        pages = np.asarray(st.pages, dtype=np.int64)
-        p = np.arange(st.length, st.length + n, dtype=np.int64)
-        pos_v[o:o + n] = p
-        slot_v[o:o + n] = pages[p // KV_PAGE] * KV_PAGE + p % KV_PAGE
-        ctx_v[i] = st.length + n
-        tab_v[i, :len(st.pages)] = pages
-        o += n
-    dev = torch.from_numpy(host).to(device)
-    o = [0, B + 1, B + 1 + M, B + 1 + 2 * M, B + 1 + 2 * M + B]
-    base = dev.data_ptr()
-    b = _lib.Batch(n_seqs=B, n_tokens=M, max_q_len=int(lens.max()), max_ctx_len=int(ctx_v.max()),
-                   max_pages=max_pages, decode=int(all(n == 1 for _, n in seqs)),
-                   seq_start=base + 4 * o[0], positions=base + 4 * o[1], slots=base + 4 * o[2],
-                   ctx_lens=base + 4 * o[3], block_table=base + 4 * o[4])
-    return b, dev
+    @property
+    def length(self) -> int:
+        return max(self.kv.query(self.seq)[0], 0)
+
+    @length.setter
+    def length(self, v: int):
+        self.kv.advance(self.seq, v - self.length)
+
+    @property
+    def pages(self) -> list:
+        return self.kv.pages(self.seq)
 
 
 class DecodeGraph:
@@ -151,10 +176,11 @@ class DecodeGraph:
         self.span, self.n_steps, self.launched = span, n_steps, 0
         self.states = [span.reserve(sid, n_steps) for sid in sessions]
         B = len(self.states)
-        max_pages = max(len(st.pages) for st in self.states)
+        pages = [st.pages for st in self.states]
+        max_pages = max(len(p) for p in pages)
         table = []
-        for st in self.states:
-            table.extend(st.pages + [0] * (max_pages - len(st.pages)))
+        for p in pages:
+            table.extend(p + [0] * (max_pages - len(p)))
         lengths = [st.length for st in self.states]
         host = torch.tensor(list(range(B + 1)) + [0] * B + [0] * B + lengths + table, dtype=torch.int32)
         self.buf = host.to(span.device)
@@ -183,7 +209,7 @@ class DecodeGraph:
         _lib.check(self.span.lib.inferd_graph_launch(self.graph, s.cuda_stream))
         self.launched += 1
         for st in self.states:
-            st.length += 1
+            self.span.kv.advance(st.seq, 1)
 
     def __del__(self):
         g = getattr(self, "graph", None)
@@ -217,8 +243,9 @@ class SpanRuntime:
         with torch.cuda.device(self.device):
             _lib.check(self.lib.inferd_span_create(cfg, h))
         self.handle = h
-        self.pool = PagePool(kv_pages)
-        self.sessions: dict = {}
+        self.kv = KvTable(kv_pages)
+        self.sessions: dict = {}   # session key -> SeqView
+        self._seq_ids = itertools.count(1)
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -290,19 +317,21 @@ class SpanRuntime:
     def release(self, session_id):
         st = self.sessions.pop(session_id, None)
         if st is not None:
-            self.pool.free(st.pages)
+            self.kv.release(st.seq)
 
     def release_all(self):
         for sid in list(self.sessions):
             self.release(sid)
 
-    def _reserve(self, st: SeqState, n_new: int):
-        need = (st.length + n_new + KV_PAGE - 1) // KV_PAGE - len(st.pages)
-        if need > 0:
-            st.pages.extend(self.pool.alloc(need))
+    def _seq(self, session_id) -> SeqView:
+        st = self.sessions.get(session_id)
+        if st is None:
+            st = self.sessions[session_id] = SeqView(self.kv, next(self._seq_ids))
+        return st
 
     def build_batch(self, seqs):
-        return build_batch(seqs, self.device)
+        """seqs: [(SeqView, n_new)] with pages reserved -> (Batch, keep-alive buffers)."""
+        return self.kv.build_batch([(st.seq, n) for st, n in seqs], self.device)
 
     # ----------------------------------------------------------------- fast path
     def run(self, batch, ids=None, x=None, hidden=None, next_ids=None, logits=None, layers=None, stream=None):
@@ -325,10 +354,10 @@ class SpanRuntime:
         _lib.check(self.lib.inferd_span_profile_stop(self.handle, ms, cnt, n))
         return {name: (ms[i], cnt[i]) for i, name in enumerate(_lib.PROF_CLASSES)}
 
-    def reserve(self, session_id, n_tokens: int) -> SeqState:
+    def reserve(self, session_id, n_tokens: int) -> SeqView:
         """Make sure `session_id` has pages for n_tokens more tokens (no forward)."""
-        st = self.sessions.setdefault(session_id, SeqState())
-        self._reserve(st, n_tokens)
+        st = self._seq(session_id)
+        self.kv.reserve(st.seq, n_tokens)
         return st
 
     @torch.no_grad()
@@ -403,15 +432,15 @@ class SpanRuntime:
             temp = []
             states = []
             for sid, _ in requests:
-                if sid is None:
-                    st = SeqState()
+                if sid is None:   # stateless: a table sequence of its own, released below
+                    st = SeqView(self.kv, next(self._seq_ids))
                     temp.append(st)
                 else:
-                    st = self.sessions.setdefault(sid, SeqState())
+                    st = self._seq(sid)
                 states.append(st)
             try:
                 for st, (_, n) in zip(states, requests):
-                    self._reserve(st, n)
+                    self.kv.reserve(st.seq, n)
                 B = len(requests)
                 lm = self.has_lm_head
                 hid = torch.empty((total, d.hidden), dtype=torch.bfloat16, device=dev) if want_hidden else None
@@ -442,7 +471,7 @@ class SpanRuntime:
                              hidden=None if hid is None else hid[r0:r0 + m], next_ids=c_nid, logits=c_lg,
                              layers=c_lay)
                     for i, _, t in call:
-                        states[i].length += t
+                        self.kv.advance(states[i].seq, t)
                     if not single:
                         if finals:
                             dst = torch.tensor([call[j][0] for j in finals], device=dev)
@@ -456,8 +485,7 @@ class SpanRuntime:
                         keep.append((c_nid, c_lg, c_lay))
             finally:
                 for st in temp:
-                    self.pool.free(st.pages)
-                    st.pages = []
+                    self.kv.release(st.seq)
         out = {}
         if hid is not None:
             out["hidden"] = hid

@@ -224,19 +224,23 @@ def test_rope_table_matches_hf(lib):
 
 def _attn_case(lib, H, KV, q_lens, past_lens, seed=0):
     """Random bf16 q/K/V; K/V written into shuffled pages; compare with fp32 SDPA."""
-    from inferd_amd.runtime import PagePool, SeqState, build_batch
+    from inferd_amd.runtime import KvTable, SeqView
     from kv_layout import K_IDX, V_IDX, block, pool_elems
     torch.manual_seed(seed)
     L = lib.load()
-    pool = PagePool(256)
-    pool._free = list(np.random.default_rng(seed).permutation(256))
+    table = KvTable(256)
+    # scatter the free list: one-page sequences released in a random order
+    for i in range(256):
+        table.reserve(10_000 + i, 1)
+    for i in np.random.default_rng(seed).permutation(256):
+        table.release(10_000 + int(i))
     kv = torch.zeros(pool_elems(256, KV), dtype=torch.bfloat16)
     seqs, Ks, Vs, Qs = [], [], [], []
-    for T, P in zip(q_lens, past_lens):
-        st = SeqState()
+    for j, (T, P) in enumerate(zip(q_lens, past_lens)):
+        st = SeqView(table, j)
         n = T + P
-        st.pages = pool.alloc((n + 63) // 64)
-        st.length = P
+        table.reserve(j, n)
+        table.advance(j, P)
         K = (torch.randn(KV, n, 128) * 1.0).to(torch.bfloat16)
         V = torch.randn(KV, n, 128).to(torch.bfloat16)
         for pi, p in enumerate(st.pages):
@@ -251,7 +255,7 @@ def _attn_case(lib, H, KV, q_lens, past_lens, seed=0):
         Ks.append(K)
         Vs.append(V)
         Qs.append((torch.randn(T, H, 128) * 1.5).to(torch.bfloat16))
-    batch, keep = build_batch(seqs, DEV)
+    batch, keep = table.build_batch([(st.seq, T) for st, T in seqs], DEV)
     q = torch.cat(Qs, 0).contiguous().to(DEV)
     out = torch.empty(q.shape[0], H * 128, dtype=torch.bfloat16, device=DEV)
     ws_bytes = L.inferd_attention_workspace_bytes(len(seqs), H, max(t + p for t, p in zip(q_lens, past_lens)))

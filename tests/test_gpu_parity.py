@@ -196,7 +196,7 @@ def test_nn_forward_session_cache_matches_full_recompute(q06_peaked):
         full.append(o1["next_token_id"])
         ref_h.append(b0.forward(torch.tensor([ids]))[0, -1])   # oracle boundary row of the new token
         ids = o1["generated_ids"]
-    free0, free1 = n0.span.pool.n_free, n1.span.pool.n_free
+    free0, free1 = n0.span.kv.n_free, n1.span.kv.n_free
     ids, cached, worst, worst_rms = list(prompt), [], 0.0, 0.0
     for step in range(16):
         o0 = n0.forward({"generated_ids": ids, "session_id": "s1"})
@@ -216,7 +216,7 @@ def test_nn_forward_session_cache_matches_full_recompute(q06_peaked):
     assert o1["next_token_id"] == full[0]
     c = n1.forward(n0.forward({"session_id": "s1", "close_session": True}))
     assert c == {"session_id": "s1", "closed": True}
-    assert n0.span.pool.n_free == free0 and n1.span.pool.n_free == free1
+    assert n0.span.kv.n_free == free0 and n1.span.kv.n_free == free1
     record("nn_forward_session_vs_full", steps=16, identical=True, new_row_hidden_vs_oracle_worst_max_norm=worst,
            new_row_hidden_vs_oracle_worst_rms_rel=worst_rms)
 
@@ -493,9 +493,9 @@ def test_qwen3_server_sessions_files_and_grpc(tmp_path):
     assert torch.equal(srv.send(None, xp.to(DEV), cache_position=torch.arange(8)).cpu(), ref_p)
     assert torch.equal(srv.send(None, xd.to(DEV), cache_position=torch.tensor([8])).cpu(), ref_d)
     # LRU: a, None resident; b evicts a
-    free_before = srv.span.pool.n_free
+    free_before = srv.span.kv.n_free
     srv.send("b", xp.to(DEV), cache_position=torch.arange(8))
-    assert srv.span.pool.n_free == free_before  # a's page went back, b took one
+    assert srv.span.kv.n_free == free_before  # a's page went back, b took one
     with pytest.raises(ValueError):
         srv.send("a", xd.to(DEV), cache_position=torch.tensor([9]))
     # weights-only per-layer files (qwen3_server_module.py:227-235 key names)

@@ -72,30 +72,42 @@ def test_module_surface_matches_reference():
     assert list(inspect.signature(P.PartitionedQwen2.forward).parameters)[1:] == ["inputs"]
 
 
-def test_page_pool_and_batch_descriptor():
-    from inferd_amd import _lib
-    from inferd_amd.runtime import PagePool, SeqState, build_batch
-    pool = PagePool(10)
-    a = SeqState(pages=pool.alloc(2), length=70)   # 70 cached tokens
-    b = SeqState(pages=pool.alloc(1), length=0)
-    assert pool.n_free == 7
-    batch, buf = build_batch([(a, 3), (b, 5)], "cpu")
+def test_kv_table_and_batch_descriptor():
+    """The native page table (inferd_kv_*, kvtable.hip; host-only calls, no GPU): reserve /
+    advance / release, lowest-page-first allocation, all-or-nothing exhaustion, and the batch
+    descriptor words of a cached continuation plus a fresh sequence."""
+    from inferd_amd.runtime import KvTable
+    kv = KvTable(10)
+    kv.reserve(1, 73)     # sequence a: 70 cached tokens + 3 new -> 2 pages
+    kv.advance(1, 70)
+    kv.reserve(2, 5)      # sequence b: 5 new tokens -> 1 page
+    assert kv.pages(1) == [0, 1] and kv.pages(2) == [2] and kv.n_free == 7
+    assert kv.query(1) == (70, 2) and kv.query(3) == (-1, 0)
+    batch, (buf, _) = kv.build_batch([(1, 3), (2, 5)], "cpu")
     assert (batch.n_seqs, batch.n_tokens, batch.max_q_len, batch.max_ctx_len, batch.decode) == (2, 8, 5, 73, 0)
-    base = buf.data_ptr()
 
     def arr(ptr, n):
         return list((ctypes.c_int32 * n).from_address(ptr))
     assert arr(batch.seq_start, 3) == [0, 3, 8]
     assert arr(batch.positions, 8) == [70, 71, 72, 0, 1, 2, 3, 4]
-    assert arr(batch.slots, 8)[:3] == [a.pages[1] * 64 + 6, a.pages[1] * 64 + 7, a.pages[1] * 64 + 8]
-    assert arr(batch.slots, 8)[3] == b.pages[0] * 64
+    assert arr(batch.slots, 8) == [1 * 64 + 6, 1 * 64 + 7, 1 * 64 + 8] + [2 * 64 + i for i in range(5)]
     assert arr(batch.ctx_lens, 2) == [73, 5]
-    assert arr(batch.block_table, 4) == [a.pages[0], a.pages[1], b.pages[0], 0]
-    assert batch.seq_start == base
-    pool.free(a.pages)
-    assert pool.n_free == 9
+    assert arr(batch.block_table, 4) == [0, 1, 2, 0]
+    assert batch.seq_start == buf.data_ptr()
+    with pytest.raises(RuntimeError, match="KV pool exhausted"):
+        kv.reserve(3, 8 * 64)
+    assert kv.n_free == 7 and kv.query(3)[1] == 0          # nothing taken
     with pytest.raises(RuntimeError):
-        pool.alloc(10)
+        kv.build_batch([(1, 3), (1, 3)], "cpu")             # a sequence twice
+    with pytest.raises(RuntimeError):
+        kv.build_batch([(2, 65)], "cpu")                    # pages not reserved
+    with pytest.raises(RuntimeError):
+        kv.advance(2, 65)                                   # past the reserved pages
+    kv.release(1)
+    assert kv.n_free == 9
+    kv.reserve(4, 64)                                       # a's first page comes back first
+    assert kv.pages(4) == [0]
+    kv.release(99)                                          # absent: no-op
 
 
 def test_split_model_writes_stage_files(tmp_path):
@@ -177,32 +189,45 @@ def test_bench_stage_split_qwen3_8b():
 
 
 def test_build_batch_descriptor_layout():
-    """runtime.build_batch (numpy-vectorised) against a per-token restatement of the
-    descriptor: seq_start | positions | slots (page * 64 + offset) | ctx_lens | block table."""
+    """The native batch builder (inferd_kv_build_batch) against a per-token restatement of
+    the descriptor: seq_start | positions | slots (page * 64 + offset) | ctx_lens | block
+    table, over random reserve / advance / release histories (scattered page lists)."""
     import random
-    from inferd_amd.runtime import KV_PAGE, SeqState, build_batch
+    from inferd_amd.runtime import KV_PAGE, KvTable
     rng = random.Random(0)
-    for _ in range(100):
+    kv = KvTable(4096)
+    live = {}
+    for it in range(100):
+        for _ in range(rng.randint(0, 3)):                  # churn: scatter the free list
+            if live and rng.random() < 0.5:
+                kv.release(live.pop(rng.choice(list(live))))
         seqs = []
         for _b in range(rng.randint(1, 6)):
-            st = SeqState()
-            st.length, n = rng.randint(0, 300), rng.randint(1, 200)
-            st.pages = rng.sample(range(1000), (st.length + n + KV_PAGE - 1) // KV_PAGE + rng.randint(0, 2))
-            seqs.append((st, n))
-        batch, dev = build_batch(seqs, "cpu")
-        max_pages = max(len(st.pages) for st, _ in seqs)
+            key = 1000 * it + _b
+            past, n = rng.randint(0, 300), rng.randint(1, 200)
+            kv.reserve(key, past + n + rng.randint(0, 100))
+            kv.advance(key, past)
+            live[key] = key
+            seqs.append((key, n))
+        batch, (dev, _) = kv.build_batch(seqs, "cpu")
+        pages = {k: kv.pages(k) for k, _ in seqs}
+        max_pages = max(len(pages[k]) for k, _ in seqs)
         start, pos, slots, ctx, table = [0], [], [], [], []
-        for st, n in seqs:
+        for k, n in seqs:
+            past = kv.query(k)[0]
             for i in range(n):
-                p = st.length + i
+                p = past + i
                 pos.append(p)
-                slots.append(st.pages[p // KV_PAGE] * KV_PAGE + p % KV_PAGE)
+                slots.append(pages[k][p // KV_PAGE] * KV_PAGE + p % KV_PAGE)
             start.append(start[-1] + n)
-            ctx.append(st.length + n)
-            table += st.pages + [0] * (max_pages - len(st.pages))
+            ctx.append(past + n)
+            table += pages[k] + [0] * (max_pages - len(pages[k]))
         assert dev.tolist() == start + pos + slots + ctx + table
         assert batch.n_tokens == sum(n for _, n in seqs) and batch.max_ctx_len == max(ctx)
         assert batch.max_q_len == max(n for _, n in seqs) and batch.max_pages == max_pages
+        for k, _ in seqs:
+            if rng.random() < 0.7:
+                kv.release(live.pop(k))
 
 
 def test_split_model_from_hf_checkpoint(tmp_path):

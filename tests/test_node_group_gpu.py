@@ -53,7 +53,7 @@ def _worker(rank, world, port, grouped_stage, out_path):
     res = {"split": grp.first_rank_layers, "stateless": _chain(n0, n1, prompt, 8),
            "session": _chain(n0, n1, prompt, 8, sid="g")}
     n1.forward(n0.forward({"session_id": "g", "close_session": True}))
-    res["free_after_close"] = grp.span.pool.n_free == grp.span.pool.n_pages
+    res["free_after_close"] = grp.span.kv.n_free == grp.span.kv.n_pages
     grp.shutdown()
     ref0 = PartitionedQwen2("qwen3-0.6b", 2, 0, SPECS[0])
     ref1 = PartitionedQwen2("qwen3-0.6b", 2, 1, SPECS[1])

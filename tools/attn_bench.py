@@ -17,7 +17,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from inferd_amd import _lib  # noqa: E402
-from inferd_amd.runtime import PagePool, SeqState, build_batch  # noqa: E402
+from inferd_amd.runtime import KvTable  # noqa: E402
 
 
 def main():
@@ -38,14 +38,11 @@ def main():
         H, KV, B, T, P = 32, 8, 16, 1, args.ctx - 1
     n = T + P
     pages_per = (n + 63) // 64
-    pool = PagePool(B * pages_per)
-    seqs = []
-    for _ in range(B):
-        st = SeqState()
-        st.pages = pool.alloc(pages_per)
-        st.length = P
-        seqs.append((st, T))
-    batch, keep = build_batch(seqs, dev)
+    table = KvTable(B * pages_per)
+    for b in range(B):
+        table.reserve(b, n)
+        table.advance(b, P)
+    batch, keep = table.build_batch([(b, T) for b in range(B)], dev)
     pool_pages = (B * pages_per + 15) // 16 * 16  # whole KV super-pages (common.h KV_SUPER)
     kv = (torch.rand(pool_pages * 2 * KV * 64 * 128, device=dev) * 2 - 1).to(torch.bfloat16)
     q = (torch.rand(B * T, H, 128, device=dev) * 4 - 2).to(torch.bfloat16)
