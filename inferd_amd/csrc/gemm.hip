@@ -66,12 +66,13 @@ struct DecodeArgs {
   float* part;
   int64_t ldp;
   float* ssq;
-  // DN_EXACT: producer partial sums of squares ssq_in[p * 64 + row], p < n_parts, and the
+  // DN_EXACT: producer partial sums of squares ssq_in[p * MP + row] (MP = M rounded up to a
+  // multiple of 4: one part's rows are contiguous), p < n_parts, and the
   // norm weight [K]
   const float* ssq_in;
   int n_parts;
   const u16* norm_w;
-  // EPI_RESID producer side: ssq_out[tile * 64 + row] = sum over the tile's 16 columns of
+  // EPI_RESID producer side: ssq_out[tile * MP + row] = sum over the tile's 16 columns of
   // the stored bf16 outputs squared (the next DN_EXACT consumer's ssq_in), or null
   float* ssq_out;
 };
@@ -79,7 +80,9 @@ struct DecodeArgs {
 #define DECODE_NORM_MAXK 8192  // DN_EXACT: K of one workgroup (hidden <= 8192)
 // tools/decode_gemv_lab.hip builds this file with DN_PROBE set to time the parts of DN_EXACT
 // (1: no row-scale work, 2: no A-fragment normalisation, 3: no norm wave, 4: the usual D-1
-// stage prologue, 5: weights before activations in a stage); the library builds it with 0
+// stage prologue, 5: weights before activations in a stage, 6: no sum-of-squares loads,
+// 7: no norm-weight loads, 8: the streaming waves do not wait for the row scales -- timing
+// only, its output is wrong); the library builds it with 0
 #ifndef DN_PROBE
 #define DN_PROBE 0
 #endif
@@ -238,15 +241,19 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       int PPW = 64;
       while (PPW * QM > 64) PPW >>= 1;
       const int quad = min(lane / PPW, QM - 1), p0 = lane % PPW;
-      // every load of the norm wave is an LDS-DMA (no VGPRs held across the barrier: the
-      // kernel's register budget is the streaming waves')
+      const int MP = QM * 4;  // part stride of ssq_in (rows rounded up to a quad)
+      // the norm weight goes to LDS by LDS-DMA, the sums of squares to registers (sixteen
+      // LDS-DMA loads made hipcc's waitcnt pass drain the streaming waves' ring)
       f32x4 v[16];
       if constexpr (DN_PROBE != 1) {
-        for (int c = lane; c < KT * 4; c += 64)
-          __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8),
-                                           (void*)(sm_wb + (c - lane) * 8), 16, 0, 0);
+        if constexpr (DN_PROBE != 7)
+          for (int c = lane; c < KT * 4; c += 64)
+            __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8),
+                                             (void*)(sm_wb + (c - lane) * 8), 16, 0, 0);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)(g.ssq_in + min(p0 + i * PPW, g.n_parts - 1) * 64 + 4 * quad);
+        for (int i = 0; i < 16; ++i)
+          v[i] = DN_PROBE == 6 ? f32x4{1.f, 1.f, 1.f, 1.f}
+                               : *(const f32x4*)(g.ssq_in + min(p0 + i * PPW, g.n_parts - 1) * MP + 4 * quad);
       }
       raw_barrier();  // #1: the row-scale loads are out; the streaming waves may issue theirs
       if constexpr (DN_PROBE != 1) {
@@ -268,7 +275,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
         for (int i = 0; i < 16; ++i)
           if (p0 + i * PPW < g.n_parts) s4 += v[i];
         for (int base = p0 + 16 * PPW; base < g.n_parts; base += PPW)   // M > 16 rows only
-          s4 += *(const f32x4*)(g.ssq_in + base * 64 + 4 * quad);
+          s4 += *(const f32x4*)(g.ssq_in + base * MP + 4 * quad);
         for (int o = 1; o < PPW; o <<= 1) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) s4[j] += __shfl_xor(s4[j], o);
@@ -280,7 +287,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
         // the norm weight and sm_r stores complete before the barrier releases the others
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
-      raw_barrier();  // #2: row scales and norm weight in LDS
+      if constexpr (DN_PROBE != 8) raw_barrier();  // #2: row scales and norm weight in LDS
     } else {
       raw_barrier();  // #1
       // prologue: all D stages (the step-0 issue of stage D-1 would wait behind barrier #2;
@@ -290,7 +297,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       }(std::make_integer_sequence<int, FULL_PROLOGUE ? D : D - 1>{});
       // a barrier that does not drain vmcnt: __syncthreads() would first wait for every
       // weight load just issued
-      raw_barrier();  // #2
+      if constexpr (DN_PROBE != 8) raw_barrier();  // #2
       if constexpr (DN_PROBE != 1) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) rr[mt] = sm_r[mt * 16 + (lane & 15)];
@@ -466,7 +473,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       if (live) g.C[(int64_t)row * g.ldc + col] = ob;
       if (g.ssq_out) {
         const float q = row16_sum(bf2f(ob) * bf2f(ob));
-        if (live && (ln & 15) == 0) g.ssq_out[nt * 64 + row] = q;
+        if (live && (ln & 15) == 0) g.ssq_out[nt * ((M + 3) & ~3) + row] = q;
       }
     } else if (row < M) {
       float o;

@@ -64,7 +64,8 @@ struct RowNorm {
 // RMSNorm modes of the decode (M <= 64) GEMV
 enum { DN_NONE = 0, DN_FOLD = 1, DN_EXACT = 2 };
 // DN_EXACT: Qwen3RMSNorm at the reference's rounding points applied to A inside the GEMV,
-// A' = bf16(w * bf16(A * r)), r = 1 / sqrt(sum_p ssq_in[p * 64 + row] / K + eps): the row sums
+// A' = bf16(w * bf16(A * r)), r = 1 / sqrt(sum_p ssq_in[p * MP + row] / K + eps) (MP = M rounded
+// up to a multiple of 4: compact parts, so a wave's loads cover whole cache lines): the row sums
 // of squares come from the kernel that produced A (launch_gemm's ssq_out on an EPI_RESID
 // GEMV, one partial per 16-column tile, n_parts = K / 16)
 struct DecodeNorm {

@@ -98,7 +98,7 @@ struct InferdSpan {
   size_t attn_ws_bytes = 0;
   // RMSNorm: exact (default; the reference's rounding points) or folded (INFERD_NORM_FOLD=1 at
   // span creation, A/B).  Exact on the decode GEMV path (<= 64 rows): the o and down GEMVs
-  // write per-tile row sums of squares of their outputs (ssq_post / ssq_in, [hidden/16][64]),
+  // write per-tile row sums of squares of their outputs (ssq_post / ssq_in, [hidden/16][MP], MP = rows rounded up to 4, <= 64),
   // and the gate/up and next layer's q/k/v GEMVs normalise their A fragments from them;
   // otherwise (a span's first layer, prefill) rmsnorm_kernel writes the normed rows to xn.
   bool norm_fold = false;
