@@ -660,17 +660,24 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wave_min_lim = min(wave_min_lim, __shfl_xor(wave_min_lim, o));
   const int n_pages = wg_last / KV_PAGE + 1;
-  const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
+  // K/V staging by buffer_load ... lds: one wave-uniform descriptor over the layer's pool, the
+  // page's byte offset (from a scalar load of the block table) and the piece offsets in SGPRs,
+  // lane * 16 the only VGPR -- the per-piece 64-bit address arithmetic of global_load_lds was
+  // ~60 VALU per page per wave.  A page's K block is followed by its V block (common.h
+  // kv_block), so its 32 pieces are one contiguous 32 KiB run.
+  typedef const __attribute__((address_space(4))) int* cptr;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  const cptr bt = (cptr)(b.block_table + (int64_t)bseq * b.max_pages);
+  const __amdgpu_buffer_rsrc_t kv_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)kv, 0, 0x7fffffff, 0x00020000);
+  const int swave = __builtin_amdgcn_readfirstlane(wave);
   auto stage = [&](int buf, int pi) {
-    const int phys = bt[pi];
-    const u16* kblk = kv + kv_block(phys, 0, g, KV);
-    const u16* vblk = kv + kv_block(phys, 1, g, KV);
+    const int kb = (int)(kv_block(bt[pi], 0, g, KV) * 2);
     char* base = lds + buf * 32768;
 #pragma unroll
     for (int pc = 0; pc < 8; ++pc) {
-      const int piece = wave * 8 + pc;  // 0..15 K tiles, 16..31 V tiles
-      const u16* src = (piece < 16 ? kblk + piece * 512 : vblk + (piece - 16) * 512) + lane * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(base + piece * 1024), 16, 0, 0);
+      const int piece = swave * 8 + pc;  // 0..15 K tiles, 16..31 V tiles
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(kv_rsrc, (lds_ptr)(base + piece * 1024), 16, lane * 16,
+                                               kb + piece * 1024, 0, 0);
     }
   };
   float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
