@@ -539,10 +539,12 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
                                                  int page_tok0, const int (&lim)[2], float c,
                                                  float (&m_i)[2], float (&l_i)[2], f32x4 (&o)[2][8], int lane) {
   f32x4 sc[2][4];
+  // k-slice outermost: eight accumulation chains in flight (tb outermost left two, with
+  // s_nops between dependent MFMAs)
 #pragma unroll
-  for (int tb = 0; tb < 4; ++tb)
+  for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
+    for (int tb = 0; tb < 4; ++tb) {
       const bf16x8 kf = *(const bf16x8*)(lds + (tb * 4 + ks) * 1024 + lane * 16);
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb)
