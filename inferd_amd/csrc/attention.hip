@@ -244,12 +244,15 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
   // Work items are 32-token half pages (K: 8 fragments, V: the 8 fragments of one kt), so
   // a chunk's 16-17 pages spread over the 8 waves in 4-5 items each instead of 2-3 pages:
   // the slowest wave sets the workgroup's time.  Halves past the last token are skipped.
-  const int* bt = b.block_table + (int64_t)bseq * b.max_pages;
+  // block-table entries by scalar loads (constant address space): a vector load of the page
+  // index in front of each item's addresses made every wait a vmcnt(0) that drained the ring
+  typedef const __attribute__((address_space(4))) int* cptr;
+  const cptr bt = (cptr)(b.block_table + (int64_t)bseq * b.max_pages);
   const int lim = ctx - 1;
   const int u_begin = 2 * cp0, u_end = min(2 * cp1, (lim >> 5) + 1);
   const int u_tok = lim >> 5;  // the token's own half page (last chunk)
   const bool writer = FUSED && chunk == nc - 1 && wave == (u_tok - u_begin) % NW;
-  int u = u_begin + wave;
+  int u = u_begin + __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: scalar block-table loads
   const bool has_item = u < u_end;
   auto kaddr = [&](int uu) {
     return (const bf16x8*)(kv + kv_block(bt[uu >> 1], 0, g, KV)) + (uu & 1) * 512 + lane;
@@ -279,7 +282,9 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
     for (int i = 0; i < 8; ++i) vf[st][i] = __builtin_nontemporal_load(vb + i * 64);
   };
   if (has_item) load_item(std::integral_constant<int, 0>{}, u);
-  if (u1 < u_end) load_item(std::integral_constant<int, 1>{}, u1);
+  // stage 1 unconditionally (a wave with one item loads it twice): an issue guarded by a
+  // branch makes hipcc's waitcnt pass merge the paths and drain the ring (vmcnt(0))
+  if (has_item) load_item(std::integral_constant<int, 1>{}, u1 < u_end ? u1 : u);
   if (writer && !tok_early) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
   bf16x8 qf[4];
   if constexpr (FUSED) {
@@ -295,11 +300,12 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
   f32x4 o[8];
 #pragma unroll
   for (int db = 0; db < 8; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // one item with its registers in ring stage ST; returns false after the wave's last item
-  auto item = [&](auto ST) -> bool {
+  // one item with its registers in ring stage ST; ISSUE: refill the stage with item u + 2 NW
+  // (the caller knows statically whether it exists -- see the loop below)
+  auto item = [&](auto ST, auto ISSUE) {
     constexpr int st = decltype(ST)::value;
+    constexpr bool more = decltype(ISSUE)::value;
     const int nxt = u + 2 * NW;  // refills this stage
-    const bool more = nxt < u_end;
     const int tok0 = u * 32;
     f32x4 sc[2];
 #pragma unroll
@@ -309,7 +315,7 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
       for (int ks = 0; ks < 4; ++ks) sc[t2] = mfma16(kf[st][t2 * 4 + ks], qf[ks], sc[t2]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (more) {
+    if constexpr (more) {
       if (writer && nxt == u_tok) vm_wait<0>();
       const bf16x8* kb = kaddr(nxt);
 #pragma unroll
@@ -351,19 +357,35 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
 #pragma unroll
     for (int db = 0; db < 8; ++db) o[db] = mfma16(vf[st][db], pf, o[db]);
     __builtin_amdgcn_sched_barrier(0);
-    if (more) {
+    if constexpr (more) {
       const bf16x8* vb = vaddr(nxt);
 #pragma unroll
       for (int i = 0; i < 8; ++i) vf[st][i] = __builtin_nontemporal_load(vb + i * 64);
     }
     __builtin_amdgcn_sched_barrier(0);
     u += NW;
-    return u < u_end;
   };
   if (has_item) {
-    for (;;) {
-      if (!item(std::integral_constant<int, 0>{})) break;
-      if (!item(std::integral_constant<int, 1>{})) break;
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using Y = std::true_type;
+    using N = std::false_type;
+    // steady state: both items of a pass refill their stage; then 1-3 items remain, run as
+    // straight-line tails (no guarded loads anywhere, so every wait is counted exactly)
+    while (u + 3 * NW < u_end) {
+      item(S0{}, Y{});
+      item(S1{}, Y{});
+    }
+    const int rem = (u_end - u + NW - 1) / NW;
+    if (rem == 3) {
+      item(S0{}, Y{});
+      item(S1{}, N{});
+      item(S0{}, N{});
+    } else if (rem == 2) {
+      item(S0{}, N{});
+      item(S1{}, N{});
+    } else {
+      item(S0{}, N{});
     }
   }
   // merge the NW waves through LDS
