@@ -72,6 +72,19 @@ int main() {
   run("o resid", [&](u16* w) { launch_gemm(A, h, w, M, h, h, C, h, R, h, EPI_RESID, nullptr, 0); });
   run("o resid + ssq_out", [&](u16* w) { launch_gemm(A, h, w, M, h, h, C, h, R, h, EPI_RESID, nullptr, 0, nullptr, nullptr, nullptr, ssq_out); });
   run("down resid", [&](u16* w) { launch_gemm(act, I, w, M, h, I, C, h, R, h, EPI_RESID, nullptr, 0); });
+  {
+    static unsigned long long* keys = nullptr;
+    const int V = 151936;
+    if (!keys) CHECK(hipMalloc((void**)&keys, (size_t)M * (V / 16) * 8));
+    // lm_head shape (V x h = 1.24 GB > the rotation buffers: one buffer pair, Infinity Cache
+    // defeated by its size)
+    static u16* lm = nullptr;
+    if (!lm) {
+      CHECK(hipMalloc((void**)&lm, (size_t)V * h * 2));
+      CHECK(hipMemset(lm, 0x3c, (size_t)V * h * 2));
+    }
+    run("lm_head argmax", [&](u16*) { launch_gemm(A, h, lm, M, V, h, nullptr, 0, nullptr, 0, EPI_ARGMAX, keys, 0); });
+  }
   run("down resid + ssq_out", [&](u16* w) { launch_gemm(act, I, w, M, h, I, C, h, R, h, EPI_RESID, nullptr, 0, nullptr, nullptr, nullptr, ssq_out); });
   return 0;
 }
