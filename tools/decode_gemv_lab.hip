@@ -84,6 +84,59 @@ int main() {
       CHECK(hipMemset(lm, 0x3c, (size_t)V * h * 2));
     }
     run("lm_head argmax", [&](u16*) { launch_gemm(A, h, lm, M, V, h, nullptr, 0, nullptr, 0, EPI_ARGMAX, keys, 0); });
+    // ring shapes for the many-round lm_head grid (the launcher's DecodeCfg is tuned on the
+    // one-round layer GEMVs)
+    DecodeArgs a = {};
+    a.M = M;
+    a.A = A;
+    a.lda = h;
+    a.Wp = lm;
+    a.KT = h / 32;
+    a.n_tiles = V / 16;
+    a.keys = keys;
+    auto cfg = [&](const char* name, auto kern, int threads) {
+      run(name, [&](u16*) { hipLaunchKernelGGL(kern, dim3(a.n_tiles), dim3(threads), 0, 0, a); });
+    };
+    cfg("lm_head NW8 TW4 D3", gemm_decode_kernel<1, 1, 8, 4, 3, EPI_ARGMAX, DN_NONE>, 512);
+    cfg("lm_head NW8 TW4 D2", gemm_decode_kernel<1, 1, 8, 4, 2, EPI_ARGMAX, DN_NONE>, 512);
+    cfg("lm_head NW8 TW2 D4", gemm_decode_kernel<1, 1, 8, 2, 4, EPI_ARGMAX, DN_NONE>, 512);
+    cfg("lm_head NW4 TW4 D3", gemm_decode_kernel<1, 1, 4, 4, 3, EPI_ARGMAX, DN_NONE>, 256);
+    cfg("lm_head NW4 TW4 D4", gemm_decode_kernel<1, 1, 4, 4, 4, EPI_ARGMAX, DN_NONE>, 256);
+    cfg("lm_head NW4 TW8 D2", gemm_decode_kernel<1, 1, 4, 8, 2, EPI_ARGMAX, DN_NONE>, 256);
+    cfg("lm_head NW16 TW2 D2", gemm_decode_kernel<1, 1, 16, 2, 2, EPI_ARGMAX, DN_NONE>, 1024);
+    cfg("lm_head NW16 TW4 D2", gemm_decode_kernel<1, 1, 16, 4, 2, EPI_ARGMAX, DN_NONE>, 1024);
+  }
+  {
+    // ring depth for the one-round o GEMV: D = 5 puts all four batches of a wave in flight
+    // in the prologue (no refill in the loop at all)
+    DecodeArgs a = {};
+    a.M = M;
+    a.A = A;
+    a.lda = h;
+    a.KT = h / 32;
+    a.n_tiles = h / 16;
+    a.C = C;
+    a.ldc = h;
+    a.R = R;
+    a.ldr = h;
+    a.ssq_out = ssq_out;
+    auto cfg = [&](const char* name, auto kern) {
+      run(name, [&](u16* w) {
+        a.Wp = w;
+        hipLaunchKernelGGL(kern, dim3(a.n_tiles), dim3(512), 0, 0, a);
+      });
+    };
+    cfg("o NW8 TW4 D3", gemm_decode_kernel<1, 1, 8, 4, 3, EPI_RESID, DN_NONE>);
+    cfg("o NW8 TW4 D4", gemm_decode_kernel<1, 1, 8, 4, 4, EPI_RESID, DN_NONE>);
+    cfg("o NW8 TW4 D5", gemm_decode_kernel<1, 1, 8, 4, 5, EPI_RESID, DN_NONE>);
+    cfg("o NW8 TW2 D5", gemm_decode_kernel<1, 1, 8, 2, 5, EPI_RESID, DN_NONE>);
+    cfg("o NW8 TW2 D9", gemm_decode_kernel<1, 1, 8, 2, 9, EPI_RESID, DN_NONE>);
+    a.A = act;
+    a.lda = I;
+    a.KT = I / 32;
+    cfg("down NW8 TW4 D3", gemm_decode_kernel<1, 1, 8, 4, 3, EPI_RESID, DN_NONE>);
+    cfg("down NW8 TW4 D4", gemm_decode_kernel<1, 1, 8, 4, 4, EPI_RESID, DN_NONE>);
+    cfg("down NW8 TW4 D5", gemm_decode_kernel<1, 1, 8, 4, 5, EPI_RESID, DN_NONE>);
   }
   run("down resid + ssq_out", [&](u16* w) { launch_gemm(act, I, w, M, h, I, C, h, R, h, EPI_RESID, nullptr, 0, nullptr, nullptr, nullptr, ssq_out); });
   return 0;
