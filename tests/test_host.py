@@ -334,3 +334,23 @@ def test_node_group_split_and_stage_range():
     sizes = [n for _, n in sp]
     assert sum(sizes) == 18 and sizes[-1] < sizes[0]
     assert [n for _, n in group_split(MODELS["qwen3-8b"], 18, 3, lm_head=False)] == [6, 6, 6]
+
+
+def test_c_host_kv_table(tmp_path):
+    """A plain-C host of the KV page table (tests/c_abi/kv_host.c): builds against
+    include/inferd_span.h with gcc, links libinferd_span.so, runs on the CPU."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib_dir = os.path.join(root, "inferd_amd")
+    if not os.path.exists(os.path.join(lib_dir, "libinferd_span.so")):
+        pytest.skip("libinferd_span.so not built")
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    exe = str(tmp_path / "kv_host")
+    subprocess.run([cc, "-std=c11", "-Wall", "-Werror", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "c_abi", "kv_host.c"), "-L", lib_dir, "-linferd_span",
+                    f"-Wl,-rpath,{lib_dir}", "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "C HOST OK" in r.stdout, r.stdout + r.stderr
