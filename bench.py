@@ -56,6 +56,46 @@ def latest_traffic(kind: str, workload: str):
     return None
 
 
+def measured_peaks(dev) -> dict:
+    """The two peaks re-measured on this box by the library's probe kernels
+    (inferd_amd/csrc/probe.hip), event-timed on the launch stream: a 1 GiB grid-stride read
+    (beyond the 256 MiB Infinity Cache) and dense v_mfma_f32_16x16x32_bf16 chains from
+    registers.  Median of 5 after 3 warm-ups.  Reported beside the spec peaks, which stay the
+    roofline denominators."""
+    import ctypes as C
+    from inferd_amd import _lib
+    L = _lib.load()
+    s = torch.cuda.current_stream(dev)
+    buf = torch.ones(1 << 28, dtype=torch.int32, device=dev)          # 1 GiB
+    sink = torch.zeros(1024, dtype=torch.int32, device=dev)
+    flops = C.c_double(0.0)
+
+    def timed(launch):
+        ts = []
+        for i in range(8):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            launch()
+            e1.record(s)
+            e1.synchronize()
+            if i >= 3:
+                ts.append(e0.elapsed_time(e1) * 1e-3)
+        return sorted(ts)[len(ts) // 2]
+
+    nbytes = buf.numel() * 4
+    t_rd = timed(lambda: _lib.check(L.inferd_probe_hbm_read(buf.data_ptr(), nbytes, sink.data_ptr(), 1024,
+                                                            s.cuda_stream)))
+    iters, n_wg = 8192, 2048
+    t_mf = timed(lambda: _lib.check(L.inferd_probe_mfma(iters, n_wg, sink.data_ptr(), s.cuda_stream,
+                                                        C.byref(flops))))
+    del buf
+    return {"hbm_read_GBps": round(nbytes / t_rd / 1e9, 1), "hbm_spec_GBps": HBM_PEAK_GBS,
+            "mfma_bf16_TFLOPs": round(flops.value / t_mf / 1e12, 1), "mfma_spec_TFLOPs": MFMA_BF16_PEAK_TFLOPS,
+            "how": "probe.hip: 1 GiB read (1024 workgroups x 8 waves, 1 MiB contiguous each, 16 B loads, 8 in "
+                   "flight per lane); 2048 x 4 waves of 8 independent v_mfma_f32_16x16x32_bf16 chains on random "
+                   "operands; HIP events, median of 5 after 3 warm-ups"}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -137,7 +177,8 @@ def run_prefill(args):
                      "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                      "traffic_kernel": dom,
                      "alg_flops_per_step": fl},
-        "kernels": kernels}), flush=True)
+        "kernels": kernels,
+        "peaks_measured": measured_peaks(dev)}), flush=True)
 
 
 def stage_split(d, n: int, B: int, ctx: int, how: str = "balanced"):
@@ -428,6 +469,7 @@ def main():
             "ranks": ranks if world > 1 else None,
             "backend": None if not dist else dist.get_backend(),
         }
+        out["peaks_measured"] = measured_peaks(dev)
         if world == 1 and not args.no_cpu_baseline:
             st.release()
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)

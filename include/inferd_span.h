@@ -245,6 +245,17 @@ int inferd_attention(const void* q, const void* kv_layer, const InferdBatch* bat
                      int64_t workspace_bytes, void* stream);
 int64_t inferd_attention_workspace_bytes(int32_t n_seqs, int32_t heads, int32_t max_ctx);
 
+/* ---- Measurement probes (not on the span path; no reference counterpart).  SURVEY.md §8(d)
+ * asks for the roofline peaks to be re-measured on the box beside the spec figures; bench.py
+ * times these two launches with events on `stream` and reports both. */
+/* streaming read of `bytes` at `buf`: n_wg workgroups of 512 lanes, each a contiguous run of
+ * floor(bytes / 1024 / n_wg) KiB (pick bytes a multiple of 1024 * n_wg); `sink` (>= 2 KiB,
+ * device) receives nothing for any realistic fill */
+int inferd_probe_hbm_read(const void* buf, int64_t bytes, void* sink, int32_t n_wg, void* stream);
+/* n_wg workgroups of 4 waves, each wave `iters` x 8 independent v_mfma_f32_16x16x32_bf16;
+ * *flops = the launch's dense flop count (2*16*16*32 per MFMA) */
+int inferd_probe_mfma(int32_t iters, int32_t n_wg, void* sink, void* stream, double* flops);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,8 @@ SIGNATURES = {
     "inferd_kv_batch_words": (c_i64, [c_p, C.POINTER(c_u64), C.POINTER(c_i32), c_i32]),
     "inferd_kv_build_batch": (C.c_int, [c_p, C.POINTER(c_u64), C.POINTER(c_i32), c_i32, C.POINTER(c_i32), c_i64, c_p,
                                         C.POINTER(Batch)]),
+    "inferd_probe_hbm_read": (C.c_int, [c_p, c_i64, c_p, c_i32, c_p]),
+    "inferd_probe_mfma": (C.c_int, [c_i32, c_i32, c_p, c_p, C.POINTER(C.c_double)]),
 }
 
 _lib = None

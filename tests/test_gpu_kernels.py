@@ -286,3 +286,12 @@ def test_attention_prefill(lib, H, KV):
     including a 700-token prompt (several 128-row blocks, > 4 pages)."""
     err, ref = _attn_case(lib, H, KV, [1, 17, 64, 130, 700], [0, 5, 0, 200, 61], seed=H + 1)
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
+
+
+def test_peak_probes_run():
+    """The roofline probes (probe.hip) launch and measure plausible rates: HBM read between
+    1 TB/s and the 8 TB/s spec, bf16 MFMA between 100 TF/s and the 2.5 PF/s dense spec."""
+    import bench
+    pk = bench.measured_peaks(torch.device(DEV, 0))
+    assert 1000.0 < pk["hbm_read_GBps"] <= 8000.0, pk
+    assert 100.0 < pk["mfma_bf16_TFLOPs"] <= 2500.0, pk
