@@ -138,6 +138,40 @@ int main() {
     cfg("down NW8 TW4 D4", gemm_decode_kernel<1, 1, 8, 4, 4, EPI_RESID, DN_NONE>);
     cfg("down NW8 TW4 D5", gemm_decode_kernel<1, 1, 8, 4, 5, EPI_RESID, DN_NONE>);
   }
+  {
+    // ring shapes for the split-K q/k/v GEMV with the exact norm (768 workgroups, 2 slices)
+    DecodeArgs a = {};
+    a.A = A;
+    a.lda = h;
+    a.KT = h / 32;
+    a.n_tiles = qkvN / 16;
+    a.M = M;
+    a.eps = 1e-6f;
+    a.part = part;
+    a.ldp = qkvN;
+    a.ssq_in = ssq;
+    a.n_parts = h / 16;
+    a.norm_w = nw;
+    auto cfg = [&](const char* name, auto kern, int nwv, int ksl) {
+      run(name, [&](u16* w) {
+        a.Wp = w;
+        hipLaunchKernelGGL(kern, dim3(a.n_tiles, ksl), dim3((nwv + 1) * 64), (dn_lds_bytes<DN_EXACT, 1>(a.KT / ksl)), 0, a);
+      });
+    };
+    cfg("qkv x2 NW4 TW4 D3", gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT>, 4, 2);
+    cfg("qkv x2 NW4 TW4 D2", gemm_decode_kernel<1, 1, 4, 4, 2, EPI_PARTIAL, DN_EXACT>, 4, 2);
+    cfg("qkv x2 NW4 TW4 D4", gemm_decode_kernel<1, 1, 4, 4, 4, EPI_PARTIAL, DN_EXACT>, 4, 2);
+    cfg("qkv x2 NW4 TW2 D4", gemm_decode_kernel<1, 1, 4, 2, 4, EPI_PARTIAL, DN_EXACT>, 4, 2);
+    cfg("qkv x2 NW4 TW2 D6", gemm_decode_kernel<1, 1, 4, 2, 6, EPI_PARTIAL, DN_EXACT>, 4, 2);
+    cfg("qkv x2 NW8 TW2 D2", gemm_decode_kernel<1, 1, 8, 2, 2, EPI_PARTIAL, DN_EXACT>, 8, 2);
+    cfg("qkv x2 NW8 TW2 D4", gemm_decode_kernel<1, 1, 8, 2, 4, EPI_PARTIAL, DN_EXACT>, 8, 2);
+    cfg("qkv x2 NW8 TW4 D2", gemm_decode_kernel<1, 1, 8, 4, 2, EPI_PARTIAL, DN_EXACT>, 8, 2);
+    cfg("qkv x2 NW2 TW4 D4", gemm_decode_kernel<1, 1, 2, 4, 4, EPI_PARTIAL, DN_EXACT>, 2, 2);
+    cfg("qkv x1 NW8 TW4 D3", gemm_decode_kernel<1, 1, 8, 4, 3, EPI_PARTIAL, DN_EXACT>, 8, 1);
+    cfg("qkv x1 NW8 TW4 D4", gemm_decode_kernel<1, 1, 8, 4, 4, EPI_PARTIAL, DN_EXACT>, 8, 1);
+    cfg("qkv x4 NW4 TW4 D2", gemm_decode_kernel<1, 1, 4, 4, 2, EPI_PARTIAL, DN_EXACT>, 4, 4);
+    cfg("qkv x4 NW2 TW4 D4", gemm_decode_kernel<1, 1, 2, 4, 4, EPI_PARTIAL, DN_EXACT>, 2, 4);
+  }
   run("down resid + ssq_out", [&](u16* w) { launch_gemm(act, I, w, M, h, I, C, h, R, h, EPI_RESID, nullptr, 0, nullptr, nullptr, nullptr, ssq_out); });
   return 0;
 }
