@@ -75,6 +75,9 @@ struct DecodeArgs {
   // EPI_RESID producer side: ssq_out[tile * MP + row] = sum over the tile's 16 columns of
   // the stored bf16 outputs squared (the next DN_EXACT consumer's ssq_in), or null
   float* ssq_out;
+  // GEMM_PACK_A / GEMM_PACK_C (launch_gemm `pack`): A read / EPI_SILU output written
+  // fragment-packed (packed_index); decode path only
+  int pack;
 };
 
 #define DECODE_NORM_MAXK 8192  // DN_EXACT: K of one workgroup (hidden <= 8192)
@@ -108,7 +111,18 @@ constexpr unsigned dn_lds_bytes(int KT) {
   return NORM == DN_EXACT ? (unsigned)KT * (S == 1 ? 192u : 64u) : 0u;
 }
 
-template <int MT, int S, int NW, int TW, int D, int EPI, int NORM>
+// Fragment-packed activations (APK: A is read so, CPK: the EPI_SILU output C is written so): the
+// row-tile mt, k-tile kt fragment of a [rows][K] bf16 matrix is 1 KiB at element
+// ((mt * K/32 + kt) * 64 + lane) * 8, lane l holding row 16 mt + l % 16, columns
+// 32 kt + 8 (l / 16) .. + 7 -- the MFMA A operand, so a wave reads it with one contiguous
+// 1 KiB load instead of sixteen 64-B row pieces (the decode MLP's act buffer: gate/up writes
+// it, down reads it; tools/mk_lab.hip: the row-major read costs the down GEMV ~1.5 us).
+__device__ __forceinline__ int64_t packed_index(int row, int col, int64_t row_len) {
+  return ((int64_t)(row >> 4) * (row_len >> 5) + (col >> 5)) * 512 + (row & 15) * 8 + ((col & 31) >> 3) * 128 +
+         (col & 7);
+}
+
+template <int MT, int S, int NW, int TW, int D, int EPI, int NORM, bool APK = false, bool CPK = false>
 __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
@@ -144,7 +158,8 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   for (int mt = 0; mt < MT; ++mt) {
     int row = mt * 16 + (lane & 15);
     row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
-    a[mt] = g.A + (int64_t)row * g.lda + 8 * (lane >> 4) + kt0 * 32;
+    a[mt] = APK ? g.A + ((int64_t)(mt * g.KT + kt0) * 64 + lane) * 8
+                : g.A + (int64_t)row * g.lda + 8 * (lane >> 4) + kt0 * 32;
   }
   const __amdgpu_buffer_rsrc_t w0r = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.Wp + ((int64_t)nt * g.KT + kt0) * 512), 0, KT * 1024, 0x00020000);
@@ -181,6 +196,9 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   constexpr bool A_FIRST = NORM == DN_EXACT && DN_PROBE != 5;
   constexpr bool FULL_PROLOGUE = NORM == DN_EXACT && DN_PROBE != 4;
   constexpr bool PADDED = NORM == DN_EXACT;
+  static_assert(!APK || (!PADDED && NORM != DN_FOLD), "packed A: plain (DN_NONE) kernels only");
+  static_assert(!CPK || EPI == EPI_SILU, "packed C: the SwiGLU output only");
+  constexpr int AKS = APK ? 512 : 32;  // elements between consecutive k-tiles of one lane's A
   auto issue = [&](auto stage, int bb) {
     constexpr int d = decltype(stage)::value;
     if constexpr (!PADDED) {
@@ -188,7 +206,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
 #pragma unroll
         for (int u = 0; u < TW; ++u)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
+          for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * AKS);
       }
 #pragma unroll
       for (int u = 0; u < TW; ++u) {
@@ -199,7 +217,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
 #pragma unroll
         for (int u = 0; u < TW; ++u)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * 32);
+          for (int mt = 0; mt < MT; ++mt) av[d][u][mt] = *(const bf16x8*)(a[mt] + (bb * TW + u) * AKS);
       }
       return;
     }
@@ -484,7 +502,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       } else {
         o = 0.f;  // EPI_PARTIAL returns above
       }
-      g.C[(int64_t)row * g.ldc + col] = f2bf(o);
+      g.C[CPK ? packed_index(row, col, g.ldc) : (int64_t)row * g.ldc + col] = f2bf(o);
     }
   }
 }
@@ -502,6 +520,20 @@ static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   using C = DecodeCfg<MT, S>;
   constexpr int T = decode_threads<C::NW, NORM>();
+  if constexpr (EPI == EPI_RESID && NORM == DN_NONE) {
+    if ((a.pack & GEMM_PACK_A) && a.KT % C::TW == 0) {
+      hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, true, false>), dim3(a.n_tiles),
+                         dim3(T), 0, s, a);
+      return;
+    }
+  }
+  if constexpr (EPI == EPI_SILU) {
+    if ((a.pack & GEMM_PACK_C) && a.KT % C::TW == 0) {
+      hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, false, true>), dim3(a.n_tiles),
+                         dim3(T), (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+      return;
+    }
+  }
   if (a.KT % C::TW == 0)
     hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM>), dim3(a.n_tiles), dim3(T),
                        (dn_lds_bytes<NORM, S>(a.KT)), s, a);
@@ -1498,7 +1530,7 @@ bool gemm_uses_tiled(int M, int N, int K, int epi) {
 
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
-                 const RowNorm* fold, GemmWs* ws, const DecodeNorm* dn, float* ssq_out) {
+                 const RowNorm* fold, GemmWs* ws, const DecodeNorm* dn, float* ssq_out, int pack) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
   const bool tiled = gemm_uses_tiled(M, N, K, epi);
@@ -1572,6 +1604,7 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     a.keys = keys;
     a.eps = fold ? fold->eps : (dn ? dn->eps : 0.f);
     a.ssq_out = (epi == EPI_RESID) ? ssq_out : nullptr;
+    a.pack = pack;
     if (mode == DN_EXACT) {
       a.ssq_in = dn->ssq_in;
       a.n_parts = dn->n_parts;

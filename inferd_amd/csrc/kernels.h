@@ -90,7 +90,10 @@ void gemm_ws_free(GemmWs* w);
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
                  const RowNorm* fold = nullptr, GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr,
-                 float* ssq_out = nullptr);
+                 float* ssq_out = nullptr, int pack = 0);
+// launch_gemm `pack` bits (decode path, M <= 64 only; gemm.hip packed_index): A is read
+// fragment-packed / the EPI_SILU output is written fragment-packed
+enum { GEMM_PACK_A = 1, GEMM_PACK_C = 2 };
 // prefill q/k/v projection fused with q/k RMSNorm + RoPE and the K/V cache write (the
 // persistent GEMM's epilogue); returns false, launching nothing, where that body does not
 // apply (the caller then runs launch_gemm + launch_qk_norm_rope_kv)

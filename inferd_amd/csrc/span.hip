@@ -228,7 +228,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->qkv, Mx * s->qkv_rows() * 2);
   SALLOC(s->q, Mx * H * HEAD_DIM * 2);
   SALLOC(s->attn, Mx * H * HEAD_DIM * 2);
-  SALLOC(s->act, Mx * I * 2);
+  SALLOC(s->act, ((Mx + 15) & ~(size_t)15) * I * 2);  // decode: whole 16-row packed tiles
   SALLOC(s->h, Mx * h * 2);
   SALLOC(s->last, (size_t)c.max_seqs * h * 2);
   s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
@@ -415,6 +415,13 @@ static bool fuse_decode_rope() {
   return !(e && *e == '0');
 }
 
+// Decode MLP: the SwiGLU activations go from gate/up to down fragment-packed (gemm.hip
+// packed_index); INFERD_PACK_ACT=0 keeps them row-major (A/B and the bit-exactness test).
+static bool pack_act() {
+  const char* e = getenv("INFERD_PACK_ACT");
+  return !(e && *e == '0');
+}
+
 // Decode q/k/v GEMM K-slices (reduced inside the fused attention); INFERD_QKV_SPLIT=1 keeps
 // the single-pass bf16 GEMM.  Needs M <= 16 and K/32 divisible by 4 * slices.
 static int qkv_split(int K) {
@@ -545,13 +552,17 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       }
     }
     pe = s->prof_begin(PROF_GATEUP, st);
-    launch_gemm(m_in, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, rfold, &s->gws, &dm);
+    // decode (the GEMV path): act goes between gate/up and down fragment-packed
+    const int pk =
+        (gemv && pack_act() && !gemm_uses_tiled(M, I, h, EPI_SILU) && !gemm_uses_tiled(M, h, I, EPI_RESID)) ? 1 : 0;
+    launch_gemm(m_in, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, rfold, &s->gws, &dm,
+                nullptr, pk ? GEMM_PACK_C : 0);
     s->prof_end(pe, st);
     // ---- x = h1 + down(act)
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
     pe = s->prof_begin(PROF_DOWN, st);
     launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, st, nullptr, &s->gws, nullptr,
-                (gemv && !fold) ? s->ssq_in : nullptr);
+                (gemv && !fold) ? s->ssq_in : nullptr, pk ? GEMM_PACK_A : 0);
     s->prof_end(pe, st);
     x = out;
     if (layer_out)

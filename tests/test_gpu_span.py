@@ -251,6 +251,32 @@ def test_decode_fused_rope_matches_separate(monkeypatch):
     assert e < 2e-2
 
 
+@pytest.mark.parametrize("B", [4, 16, 40, 64])
+def test_decode_packed_act_bit_exact(monkeypatch, B):
+    """The decode MLP's fragment-packed SwiGLU activations (gate/up writes them packed, down
+    reads them packed) against the row-major layout (INFERD_PACK_ACT=0): same arithmetic in
+    the same order, so the decode hidden states are bit-identical, for one (B <= 16) to four
+    (B = 64) 16-row tiles and a partial last tile (B = 40)."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["qwen3-0.6b"]
+    outs = []
+    for pack in ("1", "0"):
+        monkeypatch.setenv("INFERD_PACK_ACT", pack)
+        s = SpanRuntime(d, 0, 2, has_embed=True, has_lm_head=False, device=DEV, max_positions=256,
+                        kv_pages=2 * B + 4, max_tokens=64 * 8, max_seqs=B)
+        s.init_synthetic(SEED)
+        g = torch.Generator().manual_seed(B)
+        ids = torch.randint(0, d.vocab, (B * 8,), generator=g)
+        s.forward([(f"s{i}", 8) for i in range(B)], ids=ids, want_hidden=False)
+        hs = []
+        for step in range(3):
+            nxt = torch.tensor([(5 * step + 11 * i) % d.vocab for i in range(B)])
+            hs.append(s.forward([(f"s{i}", 1) for i in range(B)], ids=nxt, want_hidden=True)["hidden"].cpu())
+        outs.append(torch.stack(hs))
+        del s
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_config5_q32b_layer_prefill_vs_oracle():
     """BASELINE config 5 dims on the prefill path: one Qwen3-32B-dims layer (64 q / 8 kv
     heads, h 5120, I 25600) prefilling a 520-token prompt -- the ring-staged 256x256 GEMMs
