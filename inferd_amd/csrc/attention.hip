@@ -86,6 +86,9 @@ struct DecodeFuse {
   const float* ssq;   // [ksl][M]
   int ksl;
   int K;
+  // non-zero: the output is written fragment-packed (common.h packed_index) with this row
+  // length (H * 128) for the o projection's decode GEMV; zero: row-major
+  int64_t pack_ld;
 };
 
 // 8 consecutive q/k/v values of row `tok` starting at column `col` (fp32, bf16-rounded)
@@ -415,7 +418,9 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
       L += sm_l[w][n] * f;
     }
     if (nc == 1) {
-      op[n * HEAD_DIM + d] = f2bf(acc / L);
+      const u16 ov = f2bf(acc / L);
+      if (fz.pack_ld) out[packed_index(tok, (g * n_rep + n) * HEAD_DIM + d, fz.pack_ld)] = ov;
+      else op[n * HEAD_DIM + d] = ov;
     } else {
       float* pc = base + (int64_t)chunk * stride + n * PART_STRIDE;
       __hip_atomic_store(pc + d, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -455,7 +460,9 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
       L += __hip_atomic_load(pc + HEAD_DIM + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
       acc += __hip_atomic_load(pc + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
     }
-    op[n * HEAD_DIM + d] = f2bf(acc / L);
+    const u16 ov = f2bf(acc / L);
+    if (fz.pack_ld) out[packed_index(tok, (g * n_rep + n) * HEAD_DIM + d, fz.pack_ld)] = ov;
+    else op[n * HEAD_DIM + d] = ov;
   }
 }
 
@@ -531,8 +538,9 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
                               const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
                               float scale, u16* out, float* ws, hipStream_t s, const float* part,
-                              const float* ssq, int ksl, int K) {
-  const DecodeFuse fz = {qkv, ldqkv, qn_w, kn_w, cos_t, sin_t, eps, part, ssq, ksl, K};
+                              const float* ssq, int ksl, int K, bool pack_out) {
+  const DecodeFuse fz = {qkv, ldqkv, qn_w, kn_w, cos_t, sin_t, eps, part, ssq, ksl, K,
+                         pack_out ? (int64_t)H * HEAD_DIM : 0};
   attn_decode_go<true>(nullptr, kv_layer, b, H, KV, scale, out, ws, s, fz);
 }
 

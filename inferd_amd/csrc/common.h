@@ -86,3 +86,13 @@ __device__ __forceinline__ uint32_t float_key(float f) {
   uint32_t u = __float_as_uint(f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+
+// Fragment-packed activations: the row-tile mt, k-tile kt fragment of a [rows][K] bf16 matrix
+// is 1 KiB at element ((mt * K/32 + kt) * 64 + lane) * 8, lane l holding row 16 mt + l % 16,
+// columns 32 kt + 8 (l / 16) .. + 7 -- the MFMA A operand, so a decode GEMV wave reads it with
+// one contiguous 1 KiB load instead of sixteen 64-B row pieces (tools/mk_lab.hip: the
+// row-major read costs the down GEMV ~1.5 us).  Element (row, col) of a row_len-wide matrix:
+__device__ __forceinline__ int64_t packed_index(int row, int col, int64_t row_len) {
+  return ((int64_t)(row >> 4) * (row_len >> 5) + (col >> 5)) * 512 + (row & 15) * 8 + ((col & 31) >> 3) * 128 +
+         (col & 7);
+}

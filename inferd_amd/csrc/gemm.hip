@@ -111,17 +111,8 @@ constexpr unsigned dn_lds_bytes(int KT) {
   return NORM == DN_EXACT ? (unsigned)KT * (S == 1 ? 192u : 64u) : 0u;
 }
 
-// Fragment-packed activations (APK: A is read so, CPK: the EPI_SILU output C is written so): the
-// row-tile mt, k-tile kt fragment of a [rows][K] bf16 matrix is 1 KiB at element
-// ((mt * K/32 + kt) * 64 + lane) * 8, lane l holding row 16 mt + l % 16, columns
-// 32 kt + 8 (l / 16) .. + 7 -- the MFMA A operand, so a wave reads it with one contiguous
-// 1 KiB load instead of sixteen 64-B row pieces (the decode MLP's act buffer: gate/up writes
-// it, down reads it; tools/mk_lab.hip: the row-major read costs the down GEMV ~1.5 us).
-__device__ __forceinline__ int64_t packed_index(int row, int col, int64_t row_len) {
-  return ((int64_t)(row >> 4) * (row_len >> 5) + (col >> 5)) * 512 + (row & 15) * 8 + ((col & 31) >> 3) * 128 +
-         (col & 7);
-}
-
+// APK: A is read fragment-packed, CPK: the EPI_SILU output C is written so (common.h
+// packed_index; the decode MLP's act buffer and the decode attention output).
 template <int MT, int S, int NW, int TW, int D, int EPI, int NORM, bool APK = false, bool CPK = false>
 __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result

@@ -129,10 +129,11 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 // With `part` non-null the q/k/v come from launch_gemm_decode_partial's fp32 K-slices
 // (part [ksl][M][ldqkv], K = hidden) instead of the bf16 rows `qkv`; ssq [ksl][M] (folded
 // norm) scales their sum by rsqrt(sum ssq / K + eps), null means the slices were normed.
+// pack_out: `out` is written fragment-packed (common.h packed_index, whole 16-row tiles).
 void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
                               const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
                               float scale, u16* out, float* ws, hipStream_t s, const float* part = nullptr,
-                              const float* ssq = nullptr, int ksl = 0, int K = 0);
+                              const float* ssq = nullptr, int ksl = 0, int K = 0, bool pack_out = false);
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx);
 // With qkv non-null the kernel applies the q-norm + RoPE itself from the raw q/k/v rows
 // (qkv [M][ldqkv], q ignored); launch_qk_norm_rope_kv then only needs skip_q = true.

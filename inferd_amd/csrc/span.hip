@@ -227,7 +227,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->xn, Mx * h * 2);
   SALLOC(s->qkv, Mx * s->qkv_rows() * 2);
   SALLOC(s->q, Mx * H * HEAD_DIM * 2);
-  SALLOC(s->attn, Mx * H * HEAD_DIM * 2);
+  SALLOC(s->attn, ((Mx + 15) & ~(size_t)15) * H * HEAD_DIM * 2);  // decode: whole packed tiles
   SALLOC(s->act, ((Mx + 15) & ~(size_t)15) * I * 2);  // decode: whole 16-row packed tiles
   SALLOC(s->h, Mx * h * 2);
   SALLOC(s->last, (size_t)c.max_seqs * h * 2);
@@ -504,14 +504,17 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
         launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, rfold, &s->gws, &dn);
     }
     s->prof_end(pe, st);
+    // decode: the attention output goes to the o projection's GEMV fragment-packed
+    const bool pk_o = fused && gemv && pack_act() && !gemm_uses_tiled(M, h, H * HEAD_DIM, EPI_RESID);
     if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
       if (ksl > 1)
         launch_attn_decode_fused(nullptr, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
-                                 scale, s->attn, s->attn_ws, st, s->qkv_part, fold ? s->qkv_ssq : nullptr, ksl, h);
+                                 scale, s->attn, s->attn_ws, st, s->qkv_part, fold ? s->qkv_ssq : nullptr, ksl, h,
+                                 pk_o);
       else
         launch_attn_decode_fused(s->qkv, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
-                                 scale, s->attn, s->attn_ws, st);
+                                 scale, s->attn, s->attn_ws, st, nullptr, nullptr, 0, 0, pk_o);
       s->prof_end(pe, st);
     } else {
       // prefill: the attention kernel applies the q-norm + RoPE itself; this launch then
@@ -536,7 +539,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // ---- h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
     pe = s->prof_begin(PROF_O, st);
     launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st, nullptr,
-                &s->gws, nullptr, (gemv && !fold) ? s->ssq_post : nullptr);
+                &s->gws, nullptr, (gemv && !fold) ? s->ssq_post : nullptr, pk_o ? GEMM_PACK_A : 0);
     s->prof_end(pe, st);
     // ---- post_attention_layernorm -> gate/up (+SwiGLU)
     const u16* m_in = s->h;
