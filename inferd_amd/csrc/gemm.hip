@@ -111,9 +111,9 @@ constexpr unsigned dn_lds_bytes(int KT) {
   return NORM == DN_EXACT ? (unsigned)KT * (S == 1 ? 192u : 64u) : 0u;
 }
 
-// APK: A is read fragment-packed, CPK: the EPI_SILU output C is written so (common.h
-// packed_index; the decode MLP's act buffer and the decode attention output).
-template <int MT, int S, int NW, int TW, int D, int EPI, int NORM, bool APK = false, bool CPK = false>
+// APK: A is read fragment-packed (common.h packed_index: the decode path's act buffer, attention
+// output and residual stream); the epilogue's R / C addressing follows g.pack at run time.
+template <int MT, int S, int NW, int TW, int D, int EPI, int NORM, bool APK = false>
 __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
@@ -157,13 +157,15 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.Wp + ((int64_t)(nt + g.n_tiles) * g.KT + kt0) * 512), 0, KT * 1024, 0x00020000);
   const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.A + kt0 * 32), 0, (int)(((int64_t)(M - 1) * g.lda + KT * 32) * 2), 0x00020000);
+      (void*)(g.A + kt0 * (APK ? 512 : 32)), 0,
+      APK ? (int)(((int64_t)(MT - 1) * g.KT + KT) * 1024) : (int)(((int64_t)(M - 1) * g.lda + KT * 32) * 2),
+      0x00020000);
   int a_off[MT];  // byte offset of this lane's A fragment (k step 0) from ar
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     int row = mt * 16 + (lane & 15);
     row = row < M ? row : M - 1;  // rows >= M compute garbage that is never stored
-    a_off[mt] = (int)(((int64_t)row * g.lda + 8 * (lane >> 4)) * 2);
+    a_off[mt] = APK ? (int)((int64_t)mt * g.KT * 1024 + lane * 16) : (int)(((int64_t)row * g.lda + 8 * (lane >> 4)) * 2);
   }
   constexpr int OOB = 0x40000000;  // beyond every descriptor's range
   f32x4 acc[S][MT];
@@ -187,9 +189,9 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   constexpr bool A_FIRST = NORM == DN_EXACT && DN_PROBE != 5;
   constexpr bool FULL_PROLOGUE = NORM == DN_EXACT && DN_PROBE != 4;
   constexpr bool PADDED = NORM == DN_EXACT;
-  static_assert(!APK || (!PADDED && NORM != DN_FOLD), "packed A: plain (DN_NONE) kernels only");
-  static_assert(!CPK || EPI == EPI_SILU, "packed C: the SwiGLU output only");
+  static_assert(!APK || NORM != DN_FOLD, "packed A: not with the folded-norm A/B path");
   constexpr int AKS = APK ? 512 : 32;  // elements between consecutive k-tiles of one lane's A
+  constexpr int AKB = 2 * AKS;         // the same in bytes (buffer-load offsets)
   auto issue = [&](auto stage, int bb) {
     constexpr int d = decltype(stage)::value;
     if constexpr (!PADDED) {
@@ -214,13 +216,13 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
     }
     const bool live = bb < nb;
     const int wo = (live ? bb * TW * 1024 : OOB) + lane * 16;
-    const int ao = live ? bb * TW * 64 : OOB;
+    const int ao = live ? bb * TW * AKB : OOB;
     auto load_a = [&]() {
 #pragma unroll
       for (int u = 0; u < TW; ++u)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-          av[d][u][mt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ar, a_off[mt] + ao + u * 64, 0, 0));
+          av[d][u][mt] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ar, a_off[mt] + ao + u * AKB, 0, 0));
     };
     if constexpr (A_FIRST) load_a();
 #pragma unroll
@@ -478,8 +480,9 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
     } else if constexpr (EPI == EPI_RESID) {
       // all lanes take part in the 16-lane ssq reduction: rows >= M contribute zero
       const bool live = row < M;
-      const u16 ob = live ? f2bf(rbf(v[0][r]) + bf2f(g.R[(int64_t)row * g.ldr + col])) : (u16)0;
-      if (live) g.C[(int64_t)row * g.ldc + col] = ob;
+      const int64_t ri = (g.pack & GEMM_PACK_R) ? packed_index(row, col, g.ldr) : (int64_t)row * g.ldr + col;
+      const u16 ob = live ? f2bf(rbf(v[0][r]) + bf2f(g.R[ri])) : (u16)0;
+      if (live) g.C[(g.pack & GEMM_PACK_C) ? packed_index(row, col, g.ldc) : (int64_t)row * g.ldc + col] = ob;
       if (g.ssq_out) {
         const float q = row16_sum(bf2f(ob) * bf2f(ob));
         if (live && (ln & 15) == 0) g.ssq_out[nt * ((M + 3) & ~3) + row] = q;
@@ -493,7 +496,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       } else {
         o = 0.f;  // EPI_PARTIAL returns above
       }
-      g.C[CPK ? packed_index(row, col, g.ldc) : (int64_t)row * g.ldc + col] = f2bf(o);
+      g.C[(g.pack & GEMM_PACK_C) ? packed_index(row, col, g.ldc) : (int64_t)row * g.ldc + col] = f2bf(o);
     }
   }
 }
@@ -511,17 +514,14 @@ static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   using C = DecodeCfg<MT, S>;
   constexpr int T = decode_threads<C::NW, NORM>();
-  if constexpr (EPI == EPI_RESID && NORM == DN_NONE) {
-    if ((a.pack & GEMM_PACK_A) && a.KT % C::TW == 0) {
-      hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, true, false>), dim3(a.n_tiles),
-                         dim3(T), 0, s, a);
-      return;
-    }
-  }
-  if constexpr (EPI == EPI_SILU) {
-    if ((a.pack & GEMM_PACK_C) && a.KT % C::TW == 0) {
-      hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, false, true>), dim3(a.n_tiles),
-                         dim3(T), (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+  if constexpr (NORM != DN_FOLD && EPI != EPI_ARGMAX) {
+    if (a.pack & GEMM_PACK_A) {
+      if (a.KT % C::TW == 0)
+        hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, true>), dim3(a.n_tiles),
+                           dim3(T), (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+      else
+        hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM, true>), dim3(a.n_tiles), dim3(T),
+                           (dn_lds_bytes<NORM, S>(a.KT)), s, a);
       return;
     }
   }
@@ -550,7 +550,7 @@ static void decode_mt(const DecodeArgs& a, hipStream_t s) {
 // workgroups of Qwen3-8B sit 3 per CU, every CU streaming the same bytes.  `norm` selects
 // the RMSNorm mode: DN_EXACT (ssq_in / n_parts / norm_w), DN_FOLD (writes ssq) or none.
 void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
-                                float* part, float* ssq, const DecodeNorm& norm, hipStream_t s) {
+                                float* part, float* ssq, const DecodeNorm& norm, hipStream_t s, int pack) {
   DecodeArgs a = {};
   a.A = A;
   a.lda = lda;
@@ -565,8 +565,12 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
   a.ssq_in = norm.ssq_in;
   a.n_parts = norm.n_parts;
   a.norm_w = norm.w;
+  a.pack = pack;
   const dim3 grid(N / 16, kslices);
-  if (norm.mode == DN_EXACT)
+  if (norm.mode == DN_EXACT && (pack & GEMM_PACK_A))
+    hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT, true>), grid,
+                       dim3(decode_threads<4, DN_EXACT>()), (dn_lds_bytes<DN_EXACT, 1>(a.KT / kslices)), s, a);
+  else if (norm.mode == DN_EXACT)
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT>), grid,
                        dim3(decode_threads<4, DN_EXACT>()), (dn_lds_bytes<DN_EXACT, 1>(a.KT / kslices)), s, a);
   else if (norm.mode == DN_FOLD)

@@ -91,9 +91,10 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
                  const RowNorm* fold = nullptr, GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr,
                  float* ssq_out = nullptr, int pack = 0);
-// launch_gemm `pack` bits (decode path, M <= 64 only; gemm.hip packed_index): A is read
-// fragment-packed / the EPI_SILU output is written fragment-packed
-enum { GEMM_PACK_A = 1, GEMM_PACK_C = 2 };
+// launch_gemm `pack` bits (decode path, M <= 64 only; common.h packed_index): A is read
+// fragment-packed / the EPI_SILU or EPI_RESID output C is written so / the EPI_RESID residual
+// R is read so
+enum { GEMM_PACK_A = 1, GEMM_PACK_C = 2, GEMM_PACK_R = 4 };
 // prefill q/k/v projection fused with q/k RMSNorm + RoPE and the K/V cache write (the
 // persistent GEMM's epilogue); returns false, launching nothing, where that body does not
 // apply (the caller then runs launch_gemm + launch_qk_norm_rope_kv)
@@ -102,7 +103,7 @@ bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int 
 // decode q/k/v with K split over `kslices` (M <= 16): part [kslices][M][N] fp32 (and with
 // DN_FOLD ssq [kslices][M] fp32); the fused decode attention reduces them
 void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
-                                float* part, float* ssq, const DecodeNorm& norm, hipStream_t s);
+                                float* part, float* ssq, const DecodeNorm& norm, hipStream_t s, int pack = 0);
 // rs[row] = 1 / sqrt(mean(x[row][:K]^2) + eps)
 void launch_row_inv_rms(const u16* x, int64_t ldx, int M, int K, float eps, float* rs, hipStream_t s);
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,

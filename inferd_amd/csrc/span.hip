@@ -224,12 +224,12 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   }
   // workspace
   const size_t Mx = c.max_tokens;
-  SALLOC(s->xn, Mx * h * 2);
+  SALLOC(s->xn, ((Mx + 15) & ~(size_t)15) * h * 2);  // decode: whole packed tiles
   SALLOC(s->qkv, Mx * s->qkv_rows() * 2);
   SALLOC(s->q, Mx * H * HEAD_DIM * 2);
   SALLOC(s->attn, ((Mx + 15) & ~(size_t)15) * H * HEAD_DIM * 2);  // decode: whole packed tiles
   SALLOC(s->act, ((Mx + 15) & ~(size_t)15) * I * 2);  // decode: whole 16-row packed tiles
-  SALLOC(s->h, Mx * h * 2);
+  SALLOC(s->h, ((Mx + 15) & ~(size_t)15) * h * 2);  // decode: whole packed tiles
   SALLOC(s->last, (size_t)c.max_seqs * h * 2);
   s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
   SALLOC(s->attn_ws, s->attn_ws_bytes);
@@ -469,6 +469,11 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   const RowNorm rn = {c.rms_eps, s->rs_ws};
   const RowNorm* rfold = fold ? &rn : nullptr;
   const int n_parts = h / 16;
+  // decode: the residual stream between layers (and h1 inside a layer) fragment-packed
+  // (common.h packed_index) for the GEMVs that read it; the input and the last layer's
+  // output stay row-major, and so does every layer's output when layer_out asks for them
+  const bool pkx = gemv && !fold && pack_act() && !layer_out && h % 128 == 0 && I % 128 == 0;
+  bool x_packed = false;  // x (this layer's input) is fragment-packed
   long pe = -1;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
@@ -493,7 +498,8 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // the persistent GEMM runs it (else the separate qk_norm_rope_kv launch below)
     bool qkv_done = false;
     if (ksl > 1) {
-      launch_gemm_decode_partial(a_in, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, fold ? s->qkv_ssq : nullptr, dn, st);
+      launch_gemm_decode_partial(a_in, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, fold ? s->qkv_ssq : nullptr, dn, st,
+                                 (x_packed && a_in == x) ? GEMM_PACK_A : 0);
     } else {
       if (!b->decode && !fuse_prefill_rope()) {
         const QkvEpilogue qe = {b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t, s->sin_t, s->q, kv_l,
@@ -501,7 +507,8 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
         qkv_done = launch_gemm_qkv_fused(a_in, h, W.qkv, M, qkvN, h, rfold, qe, st);
       }
       if (!qkv_done)
-        launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, rfold, &s->gws, &dn);
+        launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, rfold, &s->gws, &dn,
+                    nullptr, (x_packed && a_in == x) ? GEMM_PACK_A : 0);
     }
     s->prof_end(pe, st);
     // decode: the attention output goes to the o projection's GEMV fragment-packed
@@ -537,19 +544,27 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       s->prof_end(pe, st);
     }
     // ---- h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
+    // h1 is packed iff pkx.  An in-place epilogue needs one layout on both sides, so h1 goes
+    // to s->xn (free after the q/k/v projection) where s->h holds a row-major x (the first
+    // span's embedding output) or is to receive this layer's row-major output (the last layer
+    // without x_out).
+    u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
+    const bool out_packed = pkx && l < c.n_layers - 1;
+    u16* h1 = (pkx && ((x == s->h && !x_packed) || (out == s->h && !out_packed))) ? s->xn : s->h;
     pe = s->prof_begin(PROF_O, st);
-    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, s->h, h, x, h, EPI_RESID, nullptr, st, nullptr,
-                &s->gws, nullptr, (gemv && !fold) ? s->ssq_post : nullptr, pk_o ? GEMM_PACK_A : 0);
+    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, nullptr,
+                &s->gws, nullptr, (gemv && !fold) ? s->ssq_post : nullptr,
+                (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (pkx ? GEMM_PACK_C : 0));
     s->prof_end(pe, st);
     // ---- post_attention_layernorm -> gate/up (+SwiGLU)
-    const u16* m_in = s->h;
+    const u16* m_in = h1;
     DecodeNorm dm = {fold ? (int)DN_FOLD : (int)DN_NONE, c.rms_eps, nullptr, 0, nullptr};
     if (!fold) {
       if (gemv) {
         dm = {DN_EXACT, c.rms_eps, s->ssq_post, n_parts, W.post_ln};
       } else {
         pe = s->prof_begin(PROF_NORM, st);
-        launch_rmsnorm(s->h, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
+        launch_rmsnorm(h1, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
         s->prof_end(pe, st);
         m_in = s->xn;
       }
@@ -559,15 +574,16 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     const int pk =
         (gemv && pack_act() && !gemm_uses_tiled(M, I, h, EPI_SILU) && !gemm_uses_tiled(M, h, I, EPI_RESID)) ? 1 : 0;
     launch_gemm(m_in, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, rfold, &s->gws, &dm,
-                nullptr, pk ? GEMM_PACK_C : 0);
+                nullptr, (pk ? GEMM_PACK_C : 0) | ((pkx && m_in == h1) ? GEMM_PACK_A : 0));
     s->prof_end(pe, st);
     // ---- x = h1 + down(act)
-    u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
     pe = s->prof_begin(PROF_DOWN, st);
-    launch_gemm(s->act, I, W.down, M, h, I, out, h, s->h, h, EPI_RESID, nullptr, st, nullptr, &s->gws, nullptr,
-                (gemv && !fold) ? s->ssq_in : nullptr, pk ? GEMM_PACK_A : 0);
+    launch_gemm(s->act, I, W.down, M, h, I, out, h, h1, h, EPI_RESID, nullptr, st, nullptr, &s->gws, nullptr,
+                (gemv && !fold) ? s->ssq_in : nullptr,
+                (pk ? GEMM_PACK_A : 0) | (pkx ? GEMM_PACK_R : 0) | (out_packed ? GEMM_PACK_C : 0));
     s->prof_end(pe, st);
     x = out;
+    x_packed = out_packed;
     if (layer_out)
       HIP_TRY(hipMemcpyAsync((u16*)layer_out + (size_t)l * M * h, x, (size_t)M * h * 2,
                              hipMemcpyDeviceToDevice, st));
