@@ -172,6 +172,11 @@ int main() {
     cfg("qkv x4 NW4 TW4 D2", gemm_decode_kernel<1, 1, 4, 4, 2, EPI_PARTIAL, DN_EXACT>, 4, 4);
     cfg("qkv x4 NW2 TW4 D4", gemm_decode_kernel<1, 1, 2, 4, 4, EPI_PARTIAL, DN_EXACT>, 2, 4);
   }
+  // fragment-packed activations / residual stream (the span's decode layout)
+  run("gateup exact packed", [&](u16* w) { launch_gemm(A, h, w, M, I, h, C, I, nullptr, 0, EPI_SILU, nullptr, 0, nullptr, nullptr, &ex, nullptr, GEMM_PACK_A | GEMM_PACK_C); });
+  run("qkv split2 exact packed", [&](u16* w) { launch_gemm_decode_partial(A, h, w, M, qkvN, h, 2, part, nullptr, ex, 0, GEMM_PACK_A); });
+  run("o resid + ssq_out packed", [&](u16* w) { launch_gemm(A, h, w, M, h, h, C, h, R, h, EPI_RESID, nullptr, 0, nullptr, nullptr, nullptr, ssq_out, GEMM_PACK_A | GEMM_PACK_R | GEMM_PACK_C); });
+  run("down resid + ssq_out packed", [&](u16* w) { launch_gemm(act, I, w, M, h, I, C, h, R, h, EPI_RESID, nullptr, 0, nullptr, nullptr, nullptr, ssq_out, GEMM_PACK_A | GEMM_PACK_R | GEMM_PACK_C); });
   run("down resid + ssq_out", [&](u16* w) { launch_gemm(act, I, w, M, h, I, C, h, R, h, EPI_RESID, nullptr, 0, nullptr, nullptr, nullptr, ssq_out); });
   return 0;
 }

@@ -57,8 +57,8 @@ __global__ __launch_bounds__(512) void read_kernel(const u32x4* __restrict__ p, 
 // ROWMAJOR: the activations as the engine stores them, 16 rows of K bf16 (lane l reads row
 // l % 16, 16 B at k-offset 8 (l / 16) of each 32-wide k-tile); otherwise fragment-packed
 // (each k-tile's 1 KiB contiguous, as the weights)
-template <bool WITH_A, int TW, int DEPTH, bool ROWMAJOR = false>
-__global__ __launch_bounds__(512) void read_wa_kernel(const u32x4* __restrict__ p, const u32x4* __restrict__ act,
+template <bool WITH_A, int TW, int DEPTH, bool ROWMAJOR = false, int NWT = NW>
+__global__ __launch_bounds__(NWT * 64) void read_wa_kernel(const u32x4* __restrict__ p, const u32x4* __restrict__ act,
                                                       int64_t tiles_per_wg, unsigned* __restrict__ sink) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const u32x4* base = p + blockIdx.x * tiles_per_wg * 64 + lane;
@@ -68,11 +68,11 @@ __global__ __launch_bounds__(512) void read_wa_kernel(const u32x4* __restrict__ 
   constexpr int ASTEP = ROWMAJOR ? 4 : 64;
   u32x4 acc = {0u, 0u, 0u, 0u};
   const int64_t nb = tiles_per_wg / TW;
-  for (int64_t b0 = wave; b0 < nb; b0 += (int64_t)NW * DEPTH) {
+  for (int64_t b0 = wave; b0 < nb; b0 += (int64_t)NWT * DEPTH) {
     u32x4 v[DEPTH][TW], a[DEPTH][TW];
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
-      const int64_t b = b0 + d * NW;
+      const int64_t b = b0 + d * NWT;
       if (b < nb) {
 #pragma unroll
         for (int u = 0; u < TW; ++u) {
@@ -199,6 +199,24 @@ int main() {
   u32x4* act;
   CHECK(hipMalloc((void**)&act, (size_t)ta * 1024));
   CHECK(hipMemset(act, 3, (size_t)ta * 1024));
+  // W-only floors in each decode GEMV's own grid shape (packed A beside W where it reads one)
+  for (int rep = 0; rep < 2; ++rep) {
+    time("o shape: 256 WG x 8w, 128 KiB, W", [&](int r, unsigned) {
+      hipLaunchKernelGGL((read_wa_kernel<false, 4, 3>), dim3(256), dim3(512), 0, 0, B[r], act, 128, sink);
+    });
+    time("o shape: + packed A", [&](int r, unsigned) {
+      hipLaunchKernelGGL((read_wa_kernel<true, 4, 3>), dim3(256), dim3(512), 0, 0, B[r], act, 128, sink);
+    });
+    time("qkv shape: 768 WG x 4w, 64 KiB, W", [&](int r, unsigned) {
+      hipLaunchKernelGGL((read_wa_kernel<false, 4, 3, false, 4>), dim3(768), dim3(256), 0, 0, A[r], act, 64, sink);
+    });
+    time("qkv shape: + packed A", [&](int r, unsigned) {
+      hipLaunchKernelGGL((read_wa_kernel<true, 4, 3, false, 4>), dim3(768), dim3(256), 0, 0, A[r], act, 64, sink);
+    });
+    time("gate/up shape: 768 WG x 4w, 256 KiB, W", [&](int r, unsigned) {
+      hipLaunchKernelGGL((read_wa_kernel<false, 8, 2, false, 4>), dim3(768), dim3(256), 0, 0, A[r], act, 256, sink);
+    });
+  }
   for (int rep = 0; rep < 2; ++rep) {
     time("B as GEMV reads W   (TW4 D3)", [&](int r, unsigned) {
       hipLaunchKernelGGL((read_wa_kernel<false, 4, 3>), dim3(G), dim3(512), 0, 0, B[r], act, tb, sink);
