@@ -89,7 +89,20 @@ struct DecodeFuse {
   // non-zero: the output is written fragment-packed (common.h packed_index) with this row
   // length (H * 128) for the o projection's decode GEMV; zero: row-major
   int64_t pack_ld;
+  // decode kernel: bytes of each wave's q staging slot in dynamic LDS (0: per-lane q loads)
+  int qs_bytes;
 };
+
+// q staging (fused decode attention): the workgroup's q sources -- the n_rep heads' q/k/v
+// values (ksl fp32 slices, or bf16 rows), the q-norm weight and the token's cos/sin rows --
+// are loaded by the wave's 64 lanes as one image (<= QS_MAXC 16-B pieces per lane) BEFORE its
+// K/V ring prologue, written to the wave's LDS slot after it, and each lane then reads the
+// 32 dims it needs.  vmcnt retires in order: the per-lane loads the q arithmetic used to issue
+// behind the ring's 32 loads waited for all of them (probe: -2.1 us per launch without q).
+constexpr int QS_MAXC = 5;  // pieces per lane: n_rep <= 4 heads x <= 2 slices (4 KiB) + 512 B
+__host__ __device__ inline int q_stage_bytes(int n_rep, const float* part, int ksl) {
+  return (part ? ksl * n_rep * 512 : n_rep * 256) + 512;
+}
 
 // 8 consecutive q/k/v values of row `tok` starting at column `col` (fp32, bf16-rounded)
 __device__ __forceinline__ void qkv8(const DecodeFuse& f, int M, int tok, int col, float (&x)[8]) {
@@ -226,6 +239,11 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
   }
 }
 
+// ATTN_PROBE (lab builds only): 1 = the fused decode kernel skips its q prologue
+#ifndef ATTN_PROBE
+#define ATTN_PROBE 0
+#endif
+
 template <int NW, bool FUSED>
 __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16* __restrict__ kv, const AttnBatch& b,
                                                  int H, int KV, int nc_req, float scale_log2, int n_chunks_max,
@@ -275,6 +293,38 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
     decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
     vm_wait<0>();
   }
+  // q staging: pieces c = lane + 64 i of this wave's image (unconditional loads, out-of-image
+  // pieces clamped to piece 0, so the waits stay counted)
+  extern __shared__ __attribute__((aligned(16))) char qs_lds[];
+  const bool qstage = FUSED && fz.qs_bytes > 0;
+  const int q_part_bytes = fz.part ? fz.ksl * n_rep * 512 : n_rep * 256;
+  u16x8 qsr[QS_MAXC];
+  if constexpr (FUSED) {
+    if (qstage) {
+      const int pos = lim;  // a decode token sits at its cached length (positions[tok] = ctx - 1)
+#pragma unroll
+      for (int i = 0; i < QS_MAXC; ++i) {
+        int off = (lane + 64 * i) * 16;
+        off = off < fz.qs_bytes ? off : 0;
+        const char* src;
+        if (off < q_part_bytes) {
+          if (fz.part) {
+            const int sl = off / (n_rep * 512), rem = off - sl * n_rep * 512;
+            const int hh = rem >> 9, dd = (rem & 511) >> 2;
+            src = (const char*)(fz.part + ((int64_t)sl * b.M + tok) * fz.ldqkv + (g * n_rep + hh) * HEAD_DIM + dd);
+          } else {
+            const int hh = off >> 8, e = (off & 255) >> 1;
+            src = (const char*)(fz.qkv + (int64_t)tok * fz.ldqkv + (g * n_rep + hh) * HEAD_DIM + e);
+          }
+        } else {
+          const int a = (off - q_part_bytes) >> 4;  // 0..15 q-norm weight, 16..23 cos, 24..31 sin
+          src = a < 16 ? (const char*)(fz.qn_w + 8 * a)
+                       : (const char*)((a < 24 ? fz.cos_t : fz.sin_t) + (int64_t)pos * 64 + 8 * ((a - 16) & 7));
+        }
+        qsr[i] = *(const u16x8*)src;
+      }
+    }
+  }
   auto load_item = [&](auto ST, int uu) {
     constexpr int st = decltype(ST)::value;
     const bf16x8* kb = kaddr(uu);
@@ -284,21 +334,85 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
 #pragma unroll
     for (int i = 0; i < 8; ++i) vf[st][i] = __builtin_nontemporal_load(vb + i * 64);
   };
-  if (has_item) load_item(std::integral_constant<int, 0>{}, u);
-  // stage 1 unconditionally (a wave with one item loads it twice): an issue guarded by a
-  // branch makes hipcc's waitcnt pass merge the paths and drain the ring (vmcnt(0))
-  if (has_item) load_item(std::integral_constant<int, 1>{}, u1 < u_end ? u1 : u);
-  if (writer && !tok_early) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
+  // both stages unconditionally (a wave with one item loads it twice, a wave with none loads
+  // the chunk's first item): an issue guarded by a branch makes hipcc's waitcnt pass merge
+  // the paths and drain the ring (vmcnt(0))
+  load_item(std::integral_constant<int, 0>{}, has_item ? u : u_begin);
+  load_item(std::integral_constant<int, 1>{}, u1 < u_end ? u1 : (has_item ? u : u_begin));
   bf16x8 qf[4];
   if constexpr (FUSED) {
     const int hh = hn < n_rep ? hn : 0;
-    q_norm_rope_frags(fz, b.M, tok, b.positions[tok], g * n_rep + hh, lane, qf);
+    if (qstage) {
+      char* qs = qs_lds + wave * fz.qs_bytes;
+#pragma unroll
+      for (int i = 0; i < QS_MAXC; ++i)
+        if ((lane + 64 * i) * 16 < fz.qs_bytes) *(u16x8*)(qs + (lane + 64 * i) * 16) = qsr[i];
+      // this wave's own LDS slot: its stores are read back by its own lanes only
+      const int d0 = 8 * (lane >> 4);
+      float x[4][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (fz.part) {
+          const float* p0 = (const float*)(qs + hh * 512) + d0 + ks * 32;
+          f32x4 a0 = *(const f32x4*)p0, a1 = *(const f32x4*)(p0 + 4), b0 = a0 * 0.f, b1 = a1 * 0.f;
+          if (fz.ksl == 2) {
+            const float* p1 = (const float*)(qs + (n_rep + hh) * 512) + d0 + ks * 32;
+            b0 = *(const f32x4*)p1;
+            b1 = *(const f32x4*)(p1 + 4);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // slice order as qkv8: 0 + s0 + s1
+            x[ks][j] = rbf(0.f + a0[j] + b0[j]);
+            x[ks][4 + j] = rbf(0.f + a1[j] + b1[j]);
+          }
+        } else {
+          const u16x8 r = *(const u16x8*)(qs + hh * 256 + (d0 + ks * 32) * 2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[ks][j] = bf2f(r[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += x[ks][j] * x[ks][j];
+      }
+      const float inv = 1.0f / sqrtf(sum_q4(ss) / 128.0f + fz.eps);
+      const u16* aux = (const u16*)(qs + q_part_bytes);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const u16x8 wv = *(const u16x8*)(aux + d0 + ks * 32);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[ks][j] = rbf(bf2f(wv[j]) * rbf(x[ks][j] * inv));
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int dc = d0 + (ks & 1) * 32;
+        const u16x8 cv = *(const u16x8*)(aux + 128 + dc);
+        const u16x8 sv = *(const u16x8*)(aux + 192 + dc);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float rot = ks < 2 ? -x[ks + 2][j] : x[ks - 2][j];
+          qf[ks][j] = (__bf16)(rbf(x[ks][j] * bf2f(cv[j])) + rbf(rot * bf2f(sv[j])));
+        }
+      }
+    } else
+#if ATTN_PROBE == 1  // timing probe only (wrong output): no q prologue
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = (__bf16)(0.01f * (float)((lane + ks + j + hh) & 7));
+#else
+    {
+      q_norm_rope_frags(fz, b.M, tok, b.positions[tok], g * n_rep + hh, lane, qf);
+    }
+#endif
   } else {
     const int hh = hn < n_rep ? hn : 0;
     const u16* qp = q + ((int64_t)tok * H + g * n_rep + hh) * HEAD_DIM + 8 * (lane >> 4);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qf[ks] = *(const bf16x8*)(qp + ks * 32);
   }
+  // the writer's token K/V when none of its first two items holds the token: its stores land
+  // before the ring refills with the token's half page (item(): vm_wait before that issue)
+  if (writer && !tok_early) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
   float m_i = -INFINITY, l_i = 0.f;
   f32x4 o[8];
 #pragma unroll
@@ -504,17 +618,25 @@ size_t attn_decode_ws_bytes(int B, int H, int max_ctx) {
 
 template <bool FUSED>
 static void attn_decode_go(const u16* q, u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
-                           float* ws, hipStream_t s, const DecodeFuse& fz) {
+                           float* ws, hipStream_t s, const DecodeFuse& fz_in) {
   int nw, nc;
   decode_shape(b.B, KV, b.max_ctx, &nw, &nc);
   unsigned* counters = (unsigned*)ws;
   float* part = (float*)((char*)ws + DECODE_COUNTER_BYTES);
+  DecodeFuse fz = fz_in;
+  const int n_rep = H / KV;
+  const int qsb = q_stage_bytes(n_rep, fz.part, fz.ksl);
+  fz.qs_bytes = (FUSED && n_rep <= 4 && (!fz.part || (fz.ksl <= 2 && !fz.ssq)) && qsb <= QS_MAXC * 1024 &&
+                 !env_int("INFERD_ATTN_QLANES"))
+                    ? qsb
+                    : 0;
+  const unsigned lds = (unsigned)(nw * fz.qs_bytes);
   if (nw == 8)
-    hipLaunchKernelGGL((attn_decode_kernel<8, FUSED>), dim3(nc, KV, b.B), dim3(512), 0, s, q, kv_layer, b, H, KV, nc,
-                       scale * LOG2E, nc, counters, part, out, fz);
+    hipLaunchKernelGGL((attn_decode_kernel<8, FUSED>), dim3(nc, KV, b.B), dim3(512), lds, s, q, kv_layer, b, H, KV,
+                       nc, scale * LOG2E, nc, counters, part, out, fz);
   else
-    hipLaunchKernelGGL((attn_decode_kernel<4, FUSED>), dim3(nc, KV, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, nc,
-                       scale * LOG2E, nc, counters, part, out, fz);
+    hipLaunchKernelGGL((attn_decode_kernel<4, FUSED>), dim3(nc, KV, b.B), dim3(256), lds, s, q, kv_layer, b, H, KV,
+                       nc, scale * LOG2E, nc, counters, part, out, fz);
 }
 
 // explicit (waves, chunks) shape, for tools/attn_lab.hip sweeps
