@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const u16* __restrict__ x,
                                                       const int32_t* __restrict__ row_index,
                                                       int row_sub, const u16* __restrict__ w,
                                                       u16* __restrict__ y, int64_t ldy, int N,
-                                                      float eps) {
+                                                      float eps, int pack) {
   __shared__ float red[4];
   int row = blockIdx.x;
   int src_row = row_index ? row_index[row] - row_sub : row;
@@ -155,23 +155,25 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const u16* __restrict__ x,
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(wp[j]) * rbf(v[c][j] * inv));
-      *(u16x8*)(y + (int64_t)row * ldy + ci * 8) = o;
+      // pack: y fragment-packed (common.h packed_index; 8 aligned columns stay contiguous)
+      *(u16x8*)(y + (pack ? packed_index(row, ci * 8, ldy) : (int64_t)row * ldy + ci * 8)) = o;
     }
   }
 }
 
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
-                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s) {
+                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out) {
+  const int pk = pack_out ? 1 : 0;
   int ch = (N / 8 + 255) / 256;
   dim3 g(M), b(256);
   if (ch <= 1)
-    hipLaunchKernelGGL(rmsnorm_kernel<1>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps);
+    hipLaunchKernelGGL(rmsnorm_kernel<1>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk);
   else if (ch <= 2)
-    hipLaunchKernelGGL(rmsnorm_kernel<2>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps);
+    hipLaunchKernelGGL(rmsnorm_kernel<2>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk);
   else if (ch <= 4)
-    hipLaunchKernelGGL(rmsnorm_kernel<4>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps);
+    hipLaunchKernelGGL(rmsnorm_kernel<4>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk);
   else
-    hipLaunchKernelGGL(rmsnorm_kernel<8>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps);
+    hipLaunchKernelGGL(rmsnorm_kernel<8>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk);
 }
 
 // ------------------------------------------------------------------ rope table

@@ -514,7 +514,7 @@ static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   using C = DecodeCfg<MT, S>;
   constexpr int T = decode_threads<C::NW, NORM>();
-  if constexpr (NORM != DN_FOLD && EPI != EPI_ARGMAX) {
+  if constexpr (NORM != DN_FOLD) {
     if (a.pack & GEMM_PACK_A) {
       if (a.KT % C::TW == 0)
         hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, true>), dim3(a.n_tiles),

@@ -37,7 +37,7 @@ void launch_weightgen(u16* dst, int64_t n, uint64_t key, float scale, float cent
 void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s, const u16* colscale = nullptr);
 void launch_unpack(const u16* src, int N, int K, u16* dst, hipStream_t s);
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
-                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s);
+                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out = false);
 void launch_rope_table(const float* inv_freq, int max_pos, u16* cos_t, u16* sin_t, hipStream_t s);
 void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positions,
                             const int32_t* slots, const u16* qn_w, const u16* kn_w,

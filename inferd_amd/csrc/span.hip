@@ -230,7 +230,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->attn, ((Mx + 15) & ~(size_t)15) * H * HEAD_DIM * 2);  // decode: whole packed tiles
   SALLOC(s->act, ((Mx + 15) & ~(size_t)15) * I * 2);  // decode: whole 16-row packed tiles
   SALLOC(s->h, ((Mx + 15) & ~(size_t)15) * h * 2);  // decode: whole packed tiles
-  SALLOC(s->last, (size_t)c.max_seqs * h * 2);
+  SALLOC(s->last, (((size_t)c.max_seqs + 15) & ~(size_t)15) * h * 2);  // whole packed tiles
   s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
@@ -593,9 +593,12 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     if (B > 64) return fail(INFERD_ERR_ARG, "lm_head argmax supports <= 64 sequences per call");
     // last row of each sequence: seq_start[b+1] - 1
     pe = s->prof_begin(PROF_LMHEAD, st);
-    launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st);
+    // the normed last rows go to the lm_head GEMV fragment-packed (its A operand only; the
+    // logits it may also store stay row-major)
+    const bool pk_last = pack_act() && h % 32 == 0;
+    launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st, pk_last);
     launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
-                s->argmax_partial, st);
+                s->argmax_partial, st, nullptr, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0);
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
     s->prof_end(pe, st);
   }
