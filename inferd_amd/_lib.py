@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libinferd_span.so")
+# INFERD_LIB: another build of the same library (A/B timing runs of tools/ builds only)
+LIB_PATH = os.environ.get("INFERD_LIB") or os.path.join(_HERE, "libinferd_span.so")
 
 INFERD_OK = 0
 INFERD_ERR_ARG, INFERD_ERR_NOMEM = 1, 4

@@ -236,6 +236,23 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
     __builtin_amdgcn_sched_barrier(0);
   };
   static_assert(!FULL_PROLOGUE || PADDED, "the full prologue issues unguarded");
+  // EPI_RESID: the residual elements this thread's epilogue adds (thread p < MT*64: rows
+  // mt*16 + 4*(ln>>4) + r, column nt*16 + (ln&15)), loaded before the weight stream so the
+  // epilogue at the kernel's tail does not wait a memory round trip for them
+  u16 rpre[4] = {0, 0, 0, 0};
+  if constexpr (EPI == EPI_RESID) {
+    const int p = threadIdx.x;
+    if (p < MT * 64) {
+      const int mt = p >> 6, ln = p & 63;
+      const int col = nt * 16 + (ln & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + 4 * (ln >> 4) + r;
+        if (row < M)
+          rpre[r] = g.R[(g.pack & GEMM_PACK_R) ? packed_index(row, col, g.ldr) : (int64_t)row * g.ldr + col];
+      }
+    }
+  }
   float rr[MT];  // DN_EXACT: r of row mt*16 + (lane & 15)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) rr[mt] = 1.0f;
@@ -480,8 +497,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
     } else if constexpr (EPI == EPI_RESID) {
       // all lanes take part in the 16-lane ssq reduction: rows >= M contribute zero
       const bool live = row < M;
-      const int64_t ri = (g.pack & GEMM_PACK_R) ? packed_index(row, col, g.ldr) : (int64_t)row * g.ldr + col;
-      const u16 ob = live ? f2bf(rbf(v[0][r]) + bf2f(g.R[ri])) : (u16)0;
+      const u16 ob = live ? f2bf(rbf(v[0][r]) + bf2f(rpre[r])) : (u16)0;
       if (live) g.C[(g.pack & GEMM_PACK_C) ? packed_index(row, col, g.ldc) : (int64_t)row * g.ldc + col] = ob;
       if (g.ssq_out) {
         const float q = row16_sum(bf2f(ob) * bf2f(ob));
