@@ -557,3 +557,50 @@ def test_partitioned_qwen2_from_hf_checkpoint_and_converted_parts(tmp_path):
         assert o0["hidden_meta"] == syn["hidden_meta"]
         assert PartitionedQwen2("tiny", 2, 1, paths[1]).forward(o0)["next_token_id"] == tok
     record("stage_files_from_checkpoints", hf_safetensors=True, reference_pickles_inert=True)
+
+
+# ------------------------------------------------------------------ config 2: one full span
+def test_config2_q06_full_span_prefill_and_64_cached_steps():
+    """BASELINE config 2: Qwen3-0.6B as ONE span (all 28 layers, embed + lm_head) on the GPU,
+    peaked profile.  A 512-token prompt: every layer's hidden states against the bf16 oracle
+    (TOL_SPAN) and, at the span's output, no further from fp32 arithmetic than the bf16 oracle
+    itself (NOISE_RATIO; every layer's three distances are recorded); then 64 free-running cached greedy steps (SpanRuntime sessions, one token per
+    call, Qwen3Server.send semantics) against the oracle's cached forward: identical ids on
+    every step, every oracle margin above twice the measured logit error."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = R.CONFIGS["qwen3-0.6b"]
+    s = SpanRuntime(MODELS["qwen3-0.6b"], 0, d.layers, has_embed=True, has_lm_head=True, device=DEV,
+                    max_positions=1024, kv_pages=16, max_tokens=512, max_seqs=1)
+    s.init_synthetic(SEED, profile="peaked")
+    b16 = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa", profile="peaked")
+    prompt = torch.randint(0, d.vocab, (512,), generator=torch.Generator().manual_seed(2))
+    out = s.forward([("c2", 512)], ids=prompt.to(DEV), want_hidden=False, want_next_ids=True, want_logits=True,
+                    want_layers=True)
+    got_layers = out["layers"].cpu()
+    ref16, ref32 = [], []
+    b16.forward(prompt[None], per_layer=ref16)
+    b32 = R.RefSpan(d, SEED, 0, d.layers - 1, True, False, torch.float32, "sdpa", profile="peaked")
+    b32.forward(prompt[None], per_layer=ref32)
+    layers = []
+    for i in range(d.layers):
+        e16, e32, noise = errs(got_layers[i], ref16[i][0]), errs(got_layers[i], ref32[i][0]), errs(ref16[i][0], ref32[i][0])
+        layers.append({"layer": i, "vs_bf16_ref": e16, "vs_fp32": e32, "bf16_ref_vs_fp32": noise})
+        assert span_ok(e16), (i, e16)
+    assert e32["rms_rel"] <= NOISE_RATIO * noise["rms_rel"], (e32, noise)  # the span's output
+    del ref32, b32
+    lg_ref = b16.forward_cached("c2", prompt[None])[0, -1]
+    steps = []
+    for step in range(64):
+        gid = int(out["next_ids"][0])
+        rid, margin = int(torch.argmax(lg_ref)), R.top2_margin(lg_ref)
+        e_lg = errs(out["logits"][0], lg_ref)
+        steps.append({"step": step, "gpu": gid, "ref": rid, "margin": margin, "logit_err": e_lg})
+        assert gid == rid, (step, gid, rid, margin, e_lg)
+        assert margin > 2 * e_lg["max_abs"], (step, margin, e_lg)
+        nxt = torch.tensor([gid])
+        lg_ref = b16.forward_cached("c2", nxt[None])[0, -1]
+        out = s.forward([("c2", 1)], ids=nxt.to(DEV), want_hidden=False, want_next_ids=True, want_logits=True)
+    s.check_errors()
+    print(f"config 2: 28 layers at T=512 within span tolerance and the bf16 noise floor; 64/64 cached greedy "
+          f"steps identical, smallest margin {min(x['margin'] for x in steps):.2f}")
+    record("config2_q06_full_span_T512_64_cached", agree=64, layers=layers, steps=steps)
