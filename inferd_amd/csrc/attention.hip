@@ -239,7 +239,9 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
   }
 }
 
-// ATTN_PROBE (lab builds only): 1 = the fused decode kernel skips its q prologue
+// ATTN_PROBE (lab builds only): 1 = the fused decode kernel skips its q prologue; 2 = the
+// prefill kernel's P*V MFMAs take the page's K fragments (already in registers) as their V
+// operand, i.e. half the LDS fragment reads per page (timing only, wrong output)
 #ifndef ATTN_PROBE
 #define ATTN_PROBE 0
 #endif
@@ -702,6 +704,11 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
       for (int nb = 0; nb < 2; ++nb)
         sc[nb][tb] = mfma16(kf, qf[nb][ks], ks ? sc[nb][tb] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
+#if ATTN_PROBE == 2
+  bf16x8 kkeep[4];
+#pragma unroll
+  for (int tb = 0; tb < 4; ++tb) kkeep[tb] = *(const bf16x8*)(lds + (tb * 4 + 3) * 1024 + lane * 16);
+#endif
   bf16x8 pf[2][2];
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) {
@@ -748,7 +755,11 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int db = 0; db < 8; ++db) {
+#if ATTN_PROBE == 2
+      const bf16x8 vf = kkeep[(kt * 8 + db) & 3];
+#else
       const bf16x8 vf = *(const bf16x8*)(lds + 16384 + (kt * 8 + db) * 1024 + lane * 16);
+#endif
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) o[nb][db] = mfma16(vf, pf[nb][kt], o[nb][db]);
     }
