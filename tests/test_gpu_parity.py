@@ -398,9 +398,12 @@ def _spawn(target, args_list):
 
 
 @pytest.mark.timeout(1200)
-@pytest.mark.parametrize("sizes", [[9, 9, 9, 9], [5, 27, 4]], ids=["config3_even4", "config4_uneven3"])
+@pytest.mark.parametrize("sizes", [[9, 9, 9, 9], [5, 27, 4], [6, 12, 12, 6], [2, 3, 5, 6, 6, 6, 5, 3]],
+                         ids=["config3_even4", "config4_uneven3", "config4_uneven4", "config4_uneven8"])
 def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes):
-    """BASELINE configs 3 (Qwen3-8B, 4 even spans) and 4 (the uneven [5, 27, 4] split) on the
+    """BASELINE configs 3 (Qwen3-8B, 4 even spans) and 4 (SURVEY §8(d)'s uneven splits
+    [5, 27, 4], [6, 12, 12, 6] and, as the 8-stage ring the driver's 8-GPU run uses,
+    [2, 3, 5, 6, 6, 6, 5, 3]) on the
     real HIP spans: world ranks sharing this box's GPU (hand-offs through gloo), 16 sequences
     per microbatch prefilled with 2048 tokens, 4 decode steps as captured-graph replays.  The
     greedy ids fed back to stage 0 equal a single 36-layer span's, and the first stage
