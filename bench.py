@@ -108,6 +108,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-layers", type=int, default=2, help="layers timed by the CPU baseline sample")
     p.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing pass")
+    p.add_argument("--no-prefill-line", action="store_true",
+                   help="N=1 decode runs: skip the config-5 prefill measurement added to the JSON line")
     p.add_argument("--profile-steps", type=int, default=8, help="eager event-instrumented decode steps")
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
     p.add_argument("--spans", default="", help="comma-separated layers per stage (BASELINE config 4: an uneven, "
@@ -132,27 +134,31 @@ def prefill_flops(d, n_layers: int, B: int, T: int) -> float:
 
 
 def run_prefill(args):
+    """`--mode prefill`: the config-5 line alone."""
+    print(json.dumps(prefill_line(args, args.steps, args.warmup, torch.device("cuda", 0))), flush=True)
+
+
+def prefill_line(args, steps: int, warmup: int, dev) -> dict:
     """Config 5: one pipeline stage of Qwen3-32B (8 of 64 layers) prefilling B x 8k tokens.
     Per-GPU work of the 8-stage pipeline; the hand-off is one 8k x 5120 bf16 tensor."""
     from inferd_amd.runtime import MODELS, SpanRuntime
     d = MODELS["qwen3-32b" if args.model == "qwen3-8b" else args.model]
     B, T, L = args.prefill_batch, args.prefill_len, args.prefill_layers
-    dev = torch.device("cuda", 0)
     span = SpanRuntime(d, 8, L, has_embed=False, has_lm_head=False, kv_pages=B * (T // 64 + 2) + 4,
                        max_tokens=B * T, max_seqs=max(B, 1), max_positions=T + 64, device=dev)
     span.init_synthetic(args.seed)
     x = (torch.randn(B * T, d.hidden, device=dev) * 0.5).to(torch.bfloat16)
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         span.forward([(None, T)] * B, x=x, want_hidden=True)
     # K prefill calls back to back between two synchronizes (same bracket as the decode
     # timing): each call's host work (page reservation, batch descriptor, H2D of its
     # metadata) is inside the timed region and overlaps the previous call's kernels
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         span.forward([(None, T)] * B, x=x, want_hidden=True)
     torch.cuda.synchronize()
-    t = (time.perf_counter() - t0) / args.steps
+    t = (time.perf_counter() - t0) / steps
     fl = prefill_flops(d, L, B, T)
     span.profile_start(1 << 12)
     span.forward([(None, T)] * B, x=x, want_hidden=True)
@@ -165,10 +171,11 @@ def run_prefill(args):
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
     tr = latest_traffic("prefill", f"{d.name}-prefill-{L}layers-T{T}") if B == 1 else None
     traffic = None if tr is None else tr.get(dom)
-    print(json.dumps({
+    del span
+    return {
         "metric": "prefill tokens/sec, Qwen3-32B 8-layer span (one of 8 pipeline stages)",
-        "value": round(B * T / t, 1), "unit": "tokens/s", "n_gpus": 1, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True,
+        "value": round(B * T / t, 1), "unit": "tokens/s", "n_gpus": 1, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(t * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic hidden states + counter-generated synthetic weights",
         "config": {"workload": f"qwen3-32b layers 8-{8 + L - 1}, prefill {B} x {T} tokens",
@@ -178,7 +185,7 @@ def run_prefill(args):
                      "traffic_kernel": dom,
                      "alg_flops_per_step": fl},
         "kernels": kernels,
-        "peaks_measured": measured_peaks(dev)}), flush=True)
+        "peaks_measured": measured_peaks(dev)}
 
 
 def stage_split(d, n: int, B: int, ctx: int, how: str = "balanced"):
@@ -470,6 +477,12 @@ def main():
             "backend": None if not dist else dist.get_backend(),
         }
         out["peaks_measured"] = measured_peaks(dev)
+        if world == 1 and not args.no_prefill_line:
+            # BASELINE config 5 in the same run (the driver's default bench call times it too)
+            st.release()
+            pf = prefill_line(args, 8, 2, dev)
+            out["prefill_config5"] = {k: pf[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup",
+                                                         "config", "roofline", "kernels")}
         if world == 1 and not args.no_cpu_baseline:
             st.release()
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)
