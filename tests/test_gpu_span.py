@@ -401,3 +401,47 @@ def test_config3_q8b_layer_b16_ctx2048_decode_graph():
             worst = max(worst, e)
             assert e < TOL_REL, (k, b, e)
         print(f"decode step {k} (ctx {T + k + 1}): worst rel err {worst:.2e}")
+
+
+def test_q8b_decode_ragged_contexts_vs_oracle():
+    """Ragged decode batch at Qwen3-8B dims (one layer): 16 sequences whose cached lengths sit
+    on and around page boundaries (1 .. 1500 tokens: 63/64/65, 127/128/129, 255/256/257 ...),
+    so the decode attention sees 1..24 pages per sequence, chunk counts below the requested
+    one, half-page items cut by the length mask and the writer's token on either side of a
+    page edge; 3 eager decode steps then 3 decode-graph replays (each step crosses the edges
+    of the 63/127/255-token sequences), every sequence's hidden state against the oracle's
+    cached forward (Qwen3Server.send semantics)."""
+    from inferd_amd.runtime import DecodeGraph
+    d = R.CONFIGS["qwen3-8b"]
+    lens = [1, 2, 33, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 700, 1000, 1500]
+    B, layer = len(lens), 3
+    s = span("qwen3-8b", layer, 1, False, False, kv_pages=sum(n // 64 + 2 for n in lens) + 8, max_tokens=1600,
+             max_seqs=B, max_positions=1600)
+    oracle = R.RefSpan(d, SEED, layer, layer, False, False, torch.bfloat16, "sdpa")
+    gen = torch.Generator().manual_seed(31)
+    sess = [f"r{i}" for i in range(B)]
+    for sid, n in zip(sess, lens):
+        x0 = (torch.randn(1, n, d.hidden, generator=gen) * 0.5).to(torch.bfloat16)
+        s.forward([(sid, n)], x=x0[0].to(DEV))
+        oracle.forward_cached(sid, x0)
+    worst = 0.0
+    xin = torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV)
+    hout = torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV)
+    for step in range(6):
+        xs = (torch.randn(B, d.hidden, generator=gen) * 0.5).to(torch.bfloat16)
+        if step < 3:
+            got = s.forward([(sid, 1) for sid in sess], x=xs.to(DEV))["hidden"].cpu()
+        else:
+            if step == 3:
+                g = DecodeGraph(s, sess, 3, x=xin, hidden_out=hout)
+            xin.copy_(xs.to(DEV))
+            g.launch()
+            torch.cuda.synchronize()
+            got = hout.cpu()
+        for b in range(B):
+            ref = oracle.forward_cached(sess[b], xs[b].reshape(1, 1, -1))[0, 0]
+            e = rel_err(got[b], ref)
+            worst = max(worst, e)
+            assert e < TOL_REL, (step, lens[b], e)
+    s.check_errors()
+    print(f"ragged decode, 16 sequences of 1..1500 cached tokens, 6 steps: worst rel err {worst:.2e}")
