@@ -6,12 +6,12 @@ Workload (BASELINE.json configs[2], the metric's config): Qwen3-8B, batch 16 dec
 microbatch of 16 sequences through all 36 layers + final norm + lm_head + greedy argmax.
 
   N = 1 : the whole model is one span on one GPU.
-  N > 1 : the 36 layers are split into N spans, one per GPU/rank, balanced by each stage's
-          algorithmic decode bytes (the last stage also streams the 1.24 GB lm_head, ~2.4
-          layers' worth): [19,17], [9,10,10,7], [4,5,5,5,5,5,5,2] at N = 2/4/8 (`--split even`
-          gives [18,18] ... [5,5,5,5,4,4,4,4]); N microbatches of 16 sequences are in flight; hidden states move
-          stage -> stage with RCCL send/recv over xGMI, greedy ids return last -> first.
-          Per-GPU work is fixed as N grows ("scaling": "weak").
+  N > 1 : the 36 layers are split into N even spans, one per GPU/rank -- BASELINE config 3:
+          [18,18], [9,9,9,9], [5,5,5,5,4,4,4,4] at N = 2/4/8 (`--split balanced` prices each
+          stage by its algorithmic decode bytes, the last stage also streaming the 1.24 GB
+          lm_head: [19,17], [9,10,10,7], [4,5,5,5,5,5,5,2]); N microbatches of 16 sequences are in
+          flight; hidden states move stage -> stage with RCCL send/recv over xGMI, greedy ids
+          return last -> first.  Per-GPU work is fixed as N grows ("scaling": "weak").
 
 Before timing: every sequence is prefilled with 2048 tokens through the real prefill
 path (untimed; its rate is reported as `prefill`), so the KV cache holds real K/V.
@@ -114,9 +114,9 @@ def parse():
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
     p.add_argument("--spans", default="", help="comma-separated layers per stage (BASELINE config 4: an uneven, "
                                                 "balance.py-like split, e.g. 5,27,4); overrides --split")
-    p.add_argument("--split", choices=("balanced", "even"), default="balanced",
-                   help="stage layer counts: balanced = min-max of per-stage decode bytes (lm_head priced "
-                        "on the last stage), even = counts differing by at most one")
+    p.add_argument("--split", choices=("balanced", "even"), default="even",
+                   help="stage layer counts: even = counts differing by at most one (BASELINE config 3, the "
+                        "default), balanced = min-max of per-stage decode bytes (lm_head priced on the last stage)")
     p.add_argument("--mode", choices=("decode", "prefill"), default="decode",
                    help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline)")
     p.add_argument("--prefill-layers", type=int, default=8)
@@ -138,7 +138,7 @@ def run_prefill(args):
     print(json.dumps(prefill_line(args, args.steps, args.warmup, torch.device("cuda", 0))), flush=True)
 
 
-def prefill_line(args, steps: int, warmup: int, dev) -> dict:
+def prefill_line(args, steps: int, warmup: int, dev, peaks: bool = True) -> dict:
     """Config 5: one pipeline stage of Qwen3-32B (8 of 64 layers) prefilling B x 8k tokens.
     Per-GPU work of the 8-stage pipeline; the hand-off is one 8k x 5120 bf16 tensor."""
     from inferd_amd.runtime import MODELS, SpanRuntime
@@ -185,14 +185,14 @@ def prefill_line(args, steps: int, warmup: int, dev) -> dict:
                      "traffic_kernel": dom,
                      "alg_flops_per_step": fl},
         "kernels": kernels,
-        "peaks_measured": measured_peaks(dev)}
+        "peaks_measured": measured_peaks(dev) if peaks else None}
 
 
-def stage_split(d, n: int, B: int, ctx: int, how: str = "balanced"):
-    """Layer ranges per stage.  "balanced" (default): inferd_amd.pipeline.balanced_split with
-    each stage priced by its algorithmic decode bytes (HBM-bound), so the last stage, which
-    also streams the 1.24 GB lm_head, gets fewer layers; "even": layer counts differing by
-    at most one."""
+def stage_split(d, n: int, B: int, ctx: int, how: str = "even"):
+    """Layer ranges per stage.  "even" (default, BASELINE config 3): layer counts differing by
+    at most one; "balanced": inferd_amd.pipeline.balanced_split with each stage priced by its
+    algorithmic decode bytes (HBM-bound), so the last stage, which also streams the 1.24 GB
+    lm_head, gets fewer layers."""
     if how == "even":
         return even_split(d.layers, n)
     kb = kernel_bytes(d, B, ctx)
@@ -397,6 +397,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    tick = st.tick_stats
     # ---- per-kernel HIP-event timings: the same decode kernels launched eagerly (events
     # cannot be timed inside a replayed graph); right after the timed region, same cache state
     prof = None if args.no_profile else st.profile_decode(args.profile_steps)
@@ -468,8 +469,12 @@ def main():
                 "tick_ms": round(ms_per_step / n_mb, 4),
                 "bubble_frac": round(1 - sum(stage_ms) / (world * max(stage_ms)), 4) if max(stage_ms) > 0 else None,
                 "handoff_ms_per_tick": round(ms_per_step / n_mb - max(stage_ms), 4),
+                "host_us_per_tick_rank0": tick["host_us_per_tick"],
+                "exchange_us_per_tick_rank0": tick["exchange_us_per_tick"],
                 "note": "compute from event-timed eager kernels (slightly above in-graph time); tick = "
-                        "ms_per_step / microbatches; handoff = tick - slowest stage"},
+                        "ms_per_step / microbatches; handoff = tick - slowest stage; host_us = rank 0's host "
+                        "time per tick outside the stage exchange (graph launch, page-table advance, "
+                        "schedule), exchange_us = its batch_isend_irecv + wait"},
             "prefill": {"tokens": n_mb * B * ctx, "seconds": round(t_prefill, 3),
                         "tokens_per_s": round(n_mb * B * ctx / t_prefill, 1)},
             "cpu_baseline": None,
@@ -481,8 +486,13 @@ def main():
             # BASELINE config 5 in the same run (the driver's default bench call times it too)
             st.release()
             pf = prefill_line(args, 8, 2, dev)
-            out["prefill_config5"] = {k: pf[k] for k in ("metric", "value", "unit", "ms_per_step", "steps", "warmup",
-                                                         "config", "roofline", "kernels")}
+            keep = ("metric", "value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "kernels")
+            out["prefill_config5"] = {k: pf[k] for k in keep}
+            # config 5 batched (B in {1, 4}): four 8k prompts per call
+            args.prefill_batch = 4
+            pf = prefill_line(args, 4, 1, dev, peaks=False)
+            args.prefill_batch = 1
+            out["prefill_config5_b4"] = {k: pf[k] for k in keep}
         if world == 1 and not args.no_cpu_baseline:
             st.release()
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)

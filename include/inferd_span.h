@@ -108,12 +108,8 @@ int inferd_span_init_synthetic(InferdSpan* span, uint64_t seed, void* stream);
  * q_proj k_proj v_proj o_proj q_norm k_norm input_layernorm post_attention_layernorm
  * gate_proj up_proj down_proj | embed_tokens norm lm_head.  Projections are packed into
  * the device fragment layout (fused [q;k;v] and [gate;up]).  The RMSNorms run at the
- * reference's rounding points (bf16(w * bf16(x * rsqrt(mean(x^2) + eps)))), so weights may
- * be set in any order.  Only a span created with INFERD_NORM_FOLD=1 (A/B builds of the
- * folded norm: input_layernorm folded into q/k/v_proj and post_attention_layernorm into
- * gate/up_proj at pack time, W[n][k] * w[k]) needs a layer's norm weight set BEFORE the
- * projections that consume it: there re-setting a norm weight marks those projections
- * stale and forward returns INFERD_ERR_STATE until they are set again. */
+ * reference's rounding points (bf16(w * bf16(x * rsqrt(mean(x^2) + eps)))) from the norm
+ * weights as set, so weights may be set in any order. */
 int inferd_span_set_weight(InferdSpan* span, int32_t layer, const char* name,
                            const void* src, int64_t rows, int64_t cols, void* stream);
 
@@ -139,7 +135,8 @@ int inferd_span_forward(InferdSpan* span, const InferdBatch* batch, const int32_
 int inferd_span_lm_head(InferdSpan* span, const void* x, int32_t rows, void* logits, void* stream);
 
 /* Decode graphs.  Captures one span forward of `batch` (same arguments as
- * inferd_span_forward) into a HIP graph.  With advance = 1 the graph starts with a
+ * inferd_span_forward; `logits`, last span only, optional: bf16 [n_seqs][vocab] last-row
+ * logits of every replay) into a HIP graph.  With advance = 1 the graph starts with a
  * device-side scheduler step: for every sequence b the new token goes to position
  * ctx_lens[b], its slot comes from the block table, and ctx_lens[b] grows by one -- the
  * batch arrays are mutated in place, so repeated launches walk the sequences forward one
@@ -150,7 +147,7 @@ int inferd_span_lm_head(InferdSpan* span, const void* x, int32_t rows, void* log
 typedef struct InferdGraph InferdGraph;
 int inferd_span_graph_capture(InferdSpan* span, const InferdBatch* batch, int32_t advance,
                               const int32_t* ids, const void* x_in, void* x_out, int32_t* next_ids,
-                              void* stream, InferdGraph** out);
+                              void* logits, void* stream, InferdGraph** out);
 int inferd_graph_launch(InferdGraph* graph, void* stream);
 void inferd_graph_destroy(InferdGraph* graph);
 /* Sticky device error flags, read and cleared (synchronises the device).  Bit 0: a token id
@@ -189,6 +186,9 @@ void inferd_kv_destroy(InferdKvTable* table);
 int inferd_kv_reserve(InferdKvTable* table, uint64_t seq, int32_t n_new);
 /* n tokens of `seq` are now in the cache (within its reserved pages) */
 int inferd_kv_advance(InferdKvTable* table, uint64_t seq, int32_t n);
+/* the same for n_seqs sequences at once (a decode graph replay advances every sequence of its
+ * batch by one token: one call per replay instead of one per sequence); all or nothing */
+int inferd_kv_advance_many(InferdKvTable* table, const uint64_t* seqs, int32_t n_seqs, int32_t n);
 /* drop `seq` and return its pages (absent: no-op) */
 int inferd_kv_release(InferdKvTable* table, uint64_t seq);
 /* cached length (-1: absent) and reserved page count of `seq` */

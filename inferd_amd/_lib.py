@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # INFERD_LIB: another build of the same library (A/B timing runs of tools/ builds only)
 LIB_PATH = os.environ.get("INFERD_LIB") or os.path.join(_HERE, "libinferd_span.so")
 
+ABI_VERSION = 2   # inferd_abi_version() of the header this table binds
 INFERD_OK = 0
 INFERD_ERR_ARG, INFERD_ERR_NOMEM = 1, 4
 EPI_NONE, EPI_RESID, EPI_SILU = 0, 1, 2
@@ -47,7 +48,8 @@ SIGNATURES = {
     "inferd_span_profile_start": (C.c_int, [c_p, c_i32]),
     "inferd_span_profile_stop": (C.c_int, [c_p, C.POINTER(C.c_double), C.POINTER(c_i32), c_i32]),
     "inferd_span_lm_head": (C.c_int, [c_p, c_p, c_i32, c_p, c_p]),
-    "inferd_span_graph_capture": (C.c_int, [c_p, C.POINTER(Batch), c_i32, c_p, c_p, c_p, c_p, c_p, C.POINTER(c_p)]),
+    "inferd_span_graph_capture": (C.c_int, [c_p, C.POINTER(Batch), c_i32, c_p, c_p, c_p, c_p, c_p, c_p,
+                                            C.POINTER(c_p)]),
     "inferd_graph_launch": (C.c_int, [c_p, c_p]),
     "inferd_graph_destroy": (None, [c_p]),
     "inferd_span_error_flags": (C.c_int, [c_p, C.POINTER(c_i32)]),
@@ -66,6 +68,7 @@ SIGNATURES = {
     "inferd_kv_destroy": (None, [c_p]),
     "inferd_kv_reserve": (C.c_int, [c_p, c_u64, c_i32]),
     "inferd_kv_advance": (C.c_int, [c_p, c_u64, c_i32]),
+    "inferd_kv_advance_many": (C.c_int, [c_p, C.POINTER(c_u64), c_i32, c_i32]),
     "inferd_kv_release": (C.c_int, [c_p, c_u64]),
     "inferd_kv_query": (C.c_int, [c_p, c_u64, C.POINTER(c_i32), C.POINTER(c_i32)]),
     "inferd_kv_pages": (C.c_int, [c_p, c_u64, C.POINTER(c_i32), c_i32]),
@@ -88,6 +91,9 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"libinferd_span.so not built ({path}); run __graft_entry__.build()")
     lib = C.CDLL(path)
+    lib.inferd_abi_version.restype = C.c_int
+    if lib.inferd_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{path}: ABI version {lib.inferd_abi_version()}, this binding needs {ABI_VERSION}; rebuild")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

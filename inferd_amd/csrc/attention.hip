@@ -80,12 +80,9 @@ struct DecodeFuse {
   const u16* sin_t;
   float eps;
   // split-K q/k/v (launch_gemm_decode_partial): value = bf16(sum_s part[s]) -- the same
-  // rounding point as the unsplit GEMM's epilogue (with ssq, the folded-norm A/B path:
-  // bf16(sum_s part[s] * rsqrt(sum_s ssq[s] / K + eps)))
+  // rounding point as the unsplit GEMM's epilogue
   const float* part;  // [ksl][M][ldqkv]
-  const float* ssq;   // [ksl][M]
   int ksl;
-  int K;
   // non-zero: the output is written fragment-packed (common.h packed_index) with this row
   // length (H * 128) for the o projection's decode GEMV; zero: row-major
   int64_t pack_ld;
@@ -109,21 +106,17 @@ __device__ __forceinline__ void qkv8(const DecodeFuse& f, int M, int tok, int co
   if (f.part) {
     // all slices' loads issued together (predicated, unrolled to the maximum slice count)
     f32x4 pa[4], pb[4];
-    float ps[4];
 #pragma unroll
     for (int sl = 0; sl < 4; ++sl) {
       if (sl < f.ksl) {
         const f32x4* p = (const f32x4*)(f.part + ((int64_t)sl * M + tok) * f.ldqkv + col);
         pa[sl] = p[0];
         pb[sl] = p[1];
-        ps[sl] = f.ssq ? f.ssq[sl * M + tok] : 0.f;
       } else {
         pa[sl] = pb[sl] = f32x4{0.f, 0.f, 0.f, 0.f};
-        ps[sl] = 0.f;
       }
     }
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float ss = 0.f;
 #pragma unroll
     for (int sl = 0; sl < 4; ++sl) {  // fixed slice order (zeros past ksl add exactly)
 #pragma unroll
@@ -131,16 +124,10 @@ __device__ __forceinline__ void qkv8(const DecodeFuse& f, int M, int tok, int co
         acc[j] += pa[sl][j];
         acc[4 + j] += pb[sl][j];
       }
-      ss += ps[sl];
     }
-    if (f.ssq) {  // folded norm (A/B): the slices summed raw rows
-      const float inv = 1.0f / sqrtf(ss / (float)f.K + f.eps);
+    // the slices were normed (DN_EXACT): bf16 output of the projection
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = rbf(acc[j] * inv);
-    } else {      // the slices were normed (DN_EXACT): bf16 output of the projection
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = rbf(acc[j]);
-    }
+    for (int j = 0; j < 8; ++j) x[j] = rbf(acc[j]);
   } else {
     const u16x8 r = *(const u16x8*)(f.qkv + (int64_t)tok * f.ldqkv + col);
 #pragma unroll
@@ -239,12 +226,8 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
   }
 }
 
-// ATTN_PROBE (lab builds only): 1 = the fused decode kernel skips its q prologue; 2 = the
-// prefill kernel's P*V MFMAs take the page's K fragments (already in registers) as their V
-// operand, i.e. half the LDS fragment reads per page (timing only, wrong output)
-#ifndef ATTN_PROBE
-#define ATTN_PROBE 0
-#endif
+// (the ATTN_PROBE timing builds -- no q prologue / K fragments as the P*V operand -- live in
+// the round-2 tree, git 6a90f3d, with tools/attn_lab.hip)
 
 template <int NW, bool FUSED>
 __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16* __restrict__ kv, const AttnBatch& b,
@@ -395,17 +378,9 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
           qf[ks][j] = (__bf16)(rbf(x[ks][j] * bf2f(cv[j])) + rbf(rot * bf2f(sv[j])));
         }
       }
-    } else
-#if ATTN_PROBE == 1  // timing probe only (wrong output): no q prologue
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ks][j] = (__bf16)(0.01f * (float)((lane + ks + j + hh) & 7));
-#else
-    {
+    } else {
       q_norm_rope_frags(fz, b.M, tok, b.positions[tok], g * n_rep + hh, lane, qf);
     }
-#endif
   } else {
     const int hh = hn < n_rep ? hn : 0;
     const u16* qp = q + ((int64_t)tok * H + g * n_rep + hh) * HEAD_DIM + 8 * (lane >> 4);
@@ -592,14 +567,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
                               blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-static int env_int(const char* name) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : 0;
-}
-
-// (waves per workgroup, chunks per (seq, kv head)) for a decode batch
-static void decode_shape(int B, int KV, int max_ctx, int* nw, int* nc) {
-  static const int env_nw = env_int("INFERD_ATTN_NW"), env_nc = env_int("INFERD_ATTN_NC");
+// (waves per workgroup, chunks per (seq, kv head)) for a decode batch; env_nw / env_nc: the
+// span's INFERD_ATTN_NW / INFERD_ATTN_NC (AttnBatch knobs, 0 = this default)
+static void decode_shape(int B, int KV, int max_ctx, int env_nw, int env_nc, int* nw, int* nc) {
   const int np = (max_ctx + KV_PAGE - 1) / KV_PAGE;
   const int S = B * KV;
   int w = (S * 8 <= 2048 && np < 96) ? 8 : 4;
@@ -622,14 +592,13 @@ template <bool FUSED>
 static void attn_decode_go(const u16* q, u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
                            float* ws, hipStream_t s, const DecodeFuse& fz_in) {
   int nw, nc;
-  decode_shape(b.B, KV, b.max_ctx, &nw, &nc);
+  decode_shape(b.B, KV, b.max_ctx, b.nw, b.nc, &nw, &nc);
   unsigned* counters = (unsigned*)ws;
   float* part = (float*)((char*)ws + DECODE_COUNTER_BYTES);
   DecodeFuse fz = fz_in;
   const int n_rep = H / KV;
   const int qsb = q_stage_bytes(n_rep, fz.part, fz.ksl);
-  fz.qs_bytes = (FUSED && n_rep <= 4 && (!fz.part || (fz.ksl <= 2 && !fz.ssq)) && qsb <= QS_MAXC * 1024 &&
-                 !env_int("INFERD_ATTN_QLANES"))
+  fz.qs_bytes = (FUSED && n_rep <= 4 && (!fz.part || fz.ksl <= 2) && qsb <= QS_MAXC * 1024 && !b.qlanes)
                     ? qsb
                     : 0;
   const unsigned lds = (unsigned)(nw * fz.qs_bytes);
@@ -661,10 +630,9 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 
 void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
                               const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
-                              float scale, u16* out, float* ws, hipStream_t s, const float* part,
-                              const float* ssq, int ksl, int K, bool pack_out) {
-  const DecodeFuse fz = {qkv, ldqkv, qn_w, kn_w, cos_t, sin_t, eps, part, ssq, ksl, K,
-                         pack_out ? (int64_t)H * HEAD_DIM : 0};
+                              float scale, u16* out, float* ws, hipStream_t s, const float* part, int ksl,
+                              bool pack_out) {
+  const DecodeFuse fz = {qkv, ldqkv, qn_w, kn_w, cos_t, sin_t, eps, part, ksl, pack_out ? (int64_t)H * HEAD_DIM : 0};
   attn_decode_go<true>(nullptr, kv_layer, b, H, KV, scale, out, ws, s, fz);
 }
 
@@ -704,11 +672,6 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
       for (int nb = 0; nb < 2; ++nb)
         sc[nb][tb] = mfma16(kf, qf[nb][ks], ks ? sc[nb][tb] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
-#if ATTN_PROBE == 2
-  bf16x8 kkeep[4];
-#pragma unroll
-  for (int tb = 0; tb < 4; ++tb) kkeep[tb] = *(const bf16x8*)(lds + (tb * 4 + 3) * 1024 + lane * 16);
-#endif
   bf16x8 pf[2][2];
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb) {
@@ -755,11 +718,7 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int db = 0; db < 8; ++db) {
-#if ATTN_PROBE == 2
-      const bf16x8 vf = kkeep[(kt * 8 + db) & 3];
-#else
       const bf16x8 vf = *(const bf16x8*)(lds + 16384 + (kt * 8 + db) * 1024 + lane * 16);
-#endif
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) o[nb][db] = mfma16(vf, pf[nb][kt], o[nb][db]);
     }
@@ -774,7 +733,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
                                                            const u16* __restrict__ kv,
                                                            AttnBatch b, int H, int KV,
                                                            float scale_log2,
-                                                           u16* __restrict__ out, int order, DecodeFuse fz) {
+                                                           u16* __restrict__ out, int order) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 32768];
   const int bseq = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -808,13 +767,9 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
     valid[nb] = row < T;
     tokrow[nb] = t0 + (valid[nb] ? row : T - 1);
     lim[nb] = b.positions[tokrow[nb]];
-    if (fz.qkv) {  // q-norm + RoPE from the raw q/k/v row (the separate kernel did K/V only)
-      q_norm_rope_frags(fz, b.M, tokrow[nb], lim[nb], h, lane, qf[nb]);
-    } else {
-      const u16* qp = q + ((int64_t)tokrow[nb] * H + h) * HEAD_DIM + 8 * (lane >> 4);
+    const u16* qp = q + ((int64_t)tokrow[nb] * H + h) * HEAD_DIM + 8 * (lane >> 4);
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
-    }
+    for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
   }
   // pages: up to the workgroup's last row; a wave computes up to its own last row and
   // masks only pages that reach past its smallest row limit
@@ -825,24 +780,26 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wave_min_lim = min(wave_min_lim, __shfl_xor(wave_min_lim, o));
   const int n_pages = wg_last / KV_PAGE + 1;
-  // K/V staging by buffer_load ... lds: one wave-uniform descriptor over the layer's pool, the
-  // page's byte offset (from a scalar load of the block table) and the piece offsets in SGPRs,
-  // lane * 16 the only VGPR -- the per-piece 64-bit address arithmetic of global_load_lds was
-  // ~60 VALU per page per wave.  A page's K block is followed by its V block (common.h
-  // kv_block), so its 32 pieces are one contiguous 32 KiB run.
+  // K/V staging by buffer_load ... lds: one wave-uniform descriptor per page (its 64-bit base
+  // from a scalar load of the block table, in SGPRs), the piece offsets in SGPRs, lane * 16 the
+  // only VGPR -- the per-piece 64-bit address arithmetic of global_load_lds was ~60 VALU per
+  // page per wave.  A page's K block is followed by its V block (common.h kv_block), so its 32
+  // pieces are one contiguous 32 KiB run: the descriptor covers exactly that run, whatever the
+  // pool size (a single descriptor over the whole pool with 32-bit page offsets wrapped past
+  // page ~8192 at 8 kv heads).
   typedef const __attribute__((address_space(4))) int* cptr;
   typedef __attribute__((address_space(3))) void* lds_ptr;
   const cptr bt = (cptr)(b.block_table + (int64_t)bseq * b.max_pages);
-  const __amdgpu_buffer_rsrc_t kv_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)kv, 0, 0x7fffffff, 0x00020000);
   const int swave = __builtin_amdgcn_readfirstlane(wave);
   auto stage = [&](int buf, int pi) {
-    const int kb = (int)(kv_block(bt[pi], 0, g, KV) * 2);
+    const __amdgpu_buffer_rsrc_t pg_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(kv + kv_block(bt[pi], 0, g, KV)), 0, 2 * KV_BLOCK_ELEMS * 2, 0x00020000);
     char* base = lds + buf * 32768;
 #pragma unroll
     for (int pc = 0; pc < 8; ++pc) {
       const int piece = swave * 8 + pc;  // 0..15 K tiles, 16..31 V tiles
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(kv_rsrc, (lds_ptr)(base + piece * 1024), 16, lane * 16,
-                                               kb + piece * 1024, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(pg_rsrc, (lds_ptr)(base + piece * 1024), 16, lane * 16, piece * 1024, 0,
+                                               0);
     }
   };
   float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
@@ -878,13 +835,10 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   }
 }
 
-void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
-                         float scale, u16* out, hipStream_t s, const u16* qkv, int64_t ldqkv, const u16* qn_w,
-                         const u16* cos_t, const u16* sin_t, float eps) {
+void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
+                         hipStream_t s) {
   const int n = (b.max_q_len + 127) / 128 * H;
-  const char* e = getenv("INFERD_ATTN_ORDER");
-  const int order = (e && *e) ? atoi(e) : (n % 8 == 0 ? 1 : 0);
-  const DecodeFuse fz = {qkv, ldqkv, qn_w, nullptr, cos_t, sin_t, eps, nullptr, nullptr, 0, 0};
+  const int order = b.order >= 0 ? b.order : (n % 8 == 0 ? 1 : 0);  // the span's INFERD_ATTN_ORDER
   hipLaunchKernelGGL(attn_prefill_kernel, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out,
-                     (order == 1 && n % 8 == 0) ? 1 : 0, fz);
+                     (order == 1 && n % 8 == 0) ? 1 : 0);
 }

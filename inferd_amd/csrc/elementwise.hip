@@ -34,10 +34,8 @@ void launch_weightgen(u16* dst, int64_t n, uint64_t key, float scale, float cent
 }
 
 // ------------------------------------------------------------------ fragment packing
-// one thread per 16-byte chunk: chunk c = (nt*KT + kt)*64 + lane.  With colscale, each
-// element becomes bf16(W[n][k] * colscale[k]) (fp32 product, one RNE rounding).
-__global__ void pack_kernel(const u16* __restrict__ src, int64_t ld, int N, int K,
-                            u16* __restrict__ dst, const u16* __restrict__ colscale) {
+// one thread per 16-byte chunk: chunk c = (nt*KT + kt)*64 + lane
+__global__ void pack_kernel(const u16* __restrict__ src, int64_t ld, int N, int K, u16* __restrict__ dst) {
   int KT = K / 32;
   int64_t nchunks = (int64_t)(N / 16) * KT * 64;
   int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -49,43 +47,15 @@ __global__ void pack_kernel(const u16* __restrict__ src, int64_t ld, int N, int 
     int64_t nt = tile / KT;
     int64_t row = nt * 16 + (lane & 15);
     int col = kt * 32 + 8 * (lane >> 4);
-    u16x8 v = *(const u16x8*)(src + row * ld + col);
-    if (colscale) {
-      const u16x8 w = *(const u16x8*)(colscale + col);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = f2bf(bf2f(v[j]) * bf2f(w[j]));
-    }
-    *(u16x8*)(dst + c * 8) = v;
+    *(u16x8*)(dst + c * 8) = *(const u16x8*)(src + row * ld + col);
   }
 }
 
-void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s, const u16* colscale) {
+void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s) {
   int64_t nchunks = (int64_t)(N / 16) * (K / 32) * 64;
   int64_t blocks = (nchunks + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, ld, N, K, dst, colscale);
-}
-
-// rs[row] = 1 / sqrt(mean(x[row]^2) + eps): the row scale of a folded-RMSNorm GEMM (prefill)
-__global__ __launch_bounds__(256) void row_inv_rms_kernel(const u16* __restrict__ x, int64_t ldx, int K, float eps,
-                                                          float* __restrict__ rs) {
-  __shared__ float red[4];
-  const u16* xr = x + (int64_t)blockIdx.x * ldx;
-  float t = 0.f;
-  for (int c = threadIdx.x; c < K / 8; c += 256) {
-    const u16x8 p = *(const u16x8*)(xr + c * 8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) t = fmaf(bf2f(p[j]), bf2f(p[j]), t);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
-  __syncthreads();
-  if (threadIdx.x == 0) rs[blockIdx.x] = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + eps);
-}
-
-void launch_row_inv_rms(const u16* x, int64_t ldx, int M, int K, float eps, float* rs, hipStream_t s) {
-  hipLaunchKernelGGL(row_inv_rms_kernel, dim3(M), dim3(256), 0, s, x, ldx, K, eps, rs);
+  hipLaunchKernelGGL(pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, ld, N, K, dst);
 }
 
 // inverse (tests / debugging): packed -> row-major
@@ -202,9 +172,9 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
     const u16* __restrict__ qkv, int64_t ldqkv, const int32_t* __restrict__ positions,
     const int32_t* __restrict__ slots, const u16* __restrict__ qn_w, const u16* __restrict__ kn_w,
     const u16* __restrict__ cos_t, const u16* __restrict__ sin_t, u16* __restrict__ q_out,
-    u16* __restrict__ kv_layer, int H, int KV, float eps, int head0) {
+    u16* __restrict__ kv_layer, int H, int KV, float eps) {
   int tok = blockIdx.y;
-  int hh = head0 + blockIdx.x * 16 + (threadIdx.x >> 4);
+  int hh = blockIdx.x * 16 + (threadIdx.x >> 4);
   int c = threadIdx.x & 15;  // dims 8c .. 8c+7
   int nheads = H + 2 * KV;
   bool active = hh < nheads;
@@ -271,13 +241,10 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kv_kernel(
 void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positions,
                             const int32_t* slots, const u16* qn_w, const u16* kn_w,
                             const u16* cos_t, const u16* sin_t, u16* q_out, u16* kv_layer, int M,
-                            int H, int KV, float eps, hipStream_t s, bool skip_q) {
-  // skip_q: K and V heads only (the prefill attention normalises and rotates q itself)
-  const int head0 = skip_q ? H : 0;
-  const int nheads = H + 2 * KV - head0;
-  dim3 g((nheads + 15) / 16, M);
+                            int H, int KV, float eps, hipStream_t s) {
+  dim3 g((H + 2 * KV + 15) / 16, M);
   hipLaunchKernelGGL(qk_norm_rope_kv_kernel, g, dim3(256), 0, s, qkv, ldqkv, positions, slots,
-                     qn_w, kn_w, cos_t, sin_t, q_out, kv_layer, H, KV, eps, head0);
+                     qn_w, kn_w, cos_t, sin_t, q_out, kv_layer, H, KV, eps);
 }
 
 // ------------------------------------------------------------------ embedding gather

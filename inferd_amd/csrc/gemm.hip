@@ -41,9 +41,6 @@ __device__ __forceinline__ float row16_sum(float v) {
 // ============================================================ decode (M <= 64) kernel
 // RMSNorm modes of the decode GEMV (NORM template argument, kernels.h DN_*):
 //  DN_NONE  A used as is;
-//  DN_FOLD  folded norm (INFERD_NORM_FOLD=1, A/B only): the norm weight was folded into the
-//           packed W at pack time; rsqrt(mean(A^2) + eps) (sums of squares from the A
-//           fragments) multiplies the fp32 accumulator;
 //  DN_EXACT Qwen3RMSNorm at the reference rounding points (qwen3_server_module.py:19-25):
 //           A' = bf16(w * bf16(A * r)), r = 1 / sqrt(sum_p ssq_in[p][row] / K + eps) from the
 //           per-tile sums of squares the producer wrote (ssq_out below), applied to each A
@@ -61,11 +58,9 @@ struct DecodeArgs {
   float eps;                 // NORM: RMSNorm epsilon
   // EPI_PARTIAL (K split over gridDim.y slices, reduced by the consumer): slice y covers
   // k-tiles [y * KT / gridDim.y, (y + 1) * KT / gridDim.y); it writes its fp32 accumulator
-  // to part[y][row][col] (row stride ldp) and, with DN_FOLD, its rows' sums of squares to
-  // ssq[y][row] -- both unscaled.
+  // to part[y][row][col] (row stride ldp).
   float* part;
   int64_t ldp;
-  float* ssq;
   // DN_EXACT: producer partial sums of squares ssq_in[p * MP + row] (MP = M rounded up to a
   // multiple of 4: one part's rows are contiguous), p < n_parts, and the
   // norm weight [K]
@@ -81,14 +76,8 @@ struct DecodeArgs {
 };
 
 #define DECODE_NORM_MAXK 8192  // DN_EXACT: K of one workgroup (hidden <= 8192)
-// tools/decode_gemv_lab.hip builds this file with DN_PROBE set to time the parts of DN_EXACT
-// (1: no row-scale work, 2: no A-fragment normalisation, 3: no norm wave, 4: the usual D-1
-// stage prologue, 5: weights before activations in a stage, 6: no sum-of-squares loads,
-// 7: no norm-weight loads, 8: the streaming waves do not wait for the row scales -- timing
-// only, its output is wrong); the library builds it with 0
-#ifndef DN_PROBE
-#define DN_PROBE 0
-#endif
+// (the timing probes of the DN_EXACT parts live in tools/decode_gemv_lab.hip's build of the
+// round-2 tree, git 6a90f3d: DN_PROBE=1..8)
 
 // DN_EXACT workgroups carry one extra "norm wave" (wave NW): it alone loads and reduces the
 // row sums of squares and stages the norm weight, so the NW streaming waves issue their whole
@@ -97,7 +86,7 @@ struct DecodeArgs {
 // stages behind them, since vmcnt retires in order; so does __syncthreads: +3-4 us per launch)
 template <int NORM>
 constexpr bool dn_norm_wave() {
-  return NORM == DN_EXACT && DN_PROBE != 3;
+  return NORM == DN_EXACT;
 }
 template <int NW, int NORM>
 constexpr int decode_threads() {
@@ -117,7 +106,6 @@ template <int MT, int S, int NW, int TW, int D, int EPI, int NORM, bool APK = fa
 __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
-  __shared__ float sm_ss[NORM == DN_FOLD ? NW : 1][MT * 16];
   __shared__ __attribute__((aligned(16))) float sm_r[NORM == DN_EXACT ? 64 : 4];
   // DN_EXACT (dynamic LDS, dn_lds_bytes): this workgroup's K range of the norm weight as loaded
   // (bf16, sm_wb, KT * 32) and, for one-stream kernels, as fp32 (sm_w: saves the streaming
@@ -173,9 +161,6 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   for (int s = 0; s < S; ++s)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[s][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ssq[MT];  // DN_FOLD: this lane's share of sum(x^2) of row mt*16 + (lane & 15)
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) ssq[mt] = 0.f;
 
   const int nb = KT / TW;  // batches (the dispatcher guarantees KT % TW == 0)
   const int swave = __builtin_amdgcn_readfirstlane(wave);
@@ -186,10 +171,9 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   // DN_EXACT: a stage's activation fragments are issued BEFORE its weights, so the
   // normalisation of A can run as soon as A (L2) lands, while the weight bytes (HBM) are
   // still in flight (vmcnt retires in issue order)
-  constexpr bool A_FIRST = NORM == DN_EXACT && DN_PROBE != 5;
-  constexpr bool FULL_PROLOGUE = NORM == DN_EXACT && DN_PROBE != 4;
+  constexpr bool A_FIRST = NORM == DN_EXACT;
+  constexpr bool FULL_PROLOGUE = NORM == DN_EXACT;
   constexpr bool PADDED = NORM == DN_EXACT;
-  static_assert(!APK || NORM != DN_FOLD, "packed A: not with the folded-norm A/B path");
   constexpr int AKS = APK ? 512 : 32;  // elements between consecutive k-tiles of one lane's A
   constexpr int AKB = 2 * AKS;         // the same in bytes (buffer-load offsets)
   auto issue = [&](auto stage, int bb) {
@@ -273,18 +257,14 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       // the norm weight goes to LDS by LDS-DMA, the sums of squares to registers (sixteen
       // LDS-DMA loads made hipcc's waitcnt pass drain the streaming waves' ring)
       f32x4 v[16];
-      if constexpr (DN_PROBE != 1) {
-        if constexpr (DN_PROBE != 7)
-          for (int c = lane; c < KT * 4; c += 64)
-            __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8),
-                                             (void*)(sm_wb + (c - lane) * 8), 16, 0, 0);
+      for (int c = lane; c < KT * 4; c += 64)
+        __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8), (void*)(sm_wb + (c - lane) * 8),
+                                         16, 0, 0);
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-          v[i] = DN_PROBE == 6 ? f32x4{1.f, 1.f, 1.f, 1.f}
-                               : *(const f32x4*)(g.ssq_in + min(p0 + i * PPW, g.n_parts - 1) * MP + 4 * quad);
-      }
+      for (int i = 0; i < 16; ++i)
+        v[i] = *(const f32x4*)(g.ssq_in + min(p0 + i * PPW, g.n_parts - 1) * MP + 4 * quad);
       raw_barrier();  // #1: the row-scale loads are out; the streaming waves may issue theirs
-      if constexpr (DN_PROBE != 1) {
+      {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (W_F32)
         for (int c = lane; c < KT * 4; c += 64) {
@@ -315,7 +295,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
         // the norm weight and sm_r stores complete before the barrier releases the others
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
-      if constexpr (DN_PROBE != 8) raw_barrier();  // #2: row scales and norm weight in LDS
+      raw_barrier();  // #2: row scales and norm weight in LDS
     } else {
       raw_barrier();  // #1
       // prologue: all D stages (the step-0 issue of stage D-1 would wait behind barrier #2;
@@ -325,11 +305,9 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       }(std::make_integer_sequence<int, FULL_PROLOGUE ? D : D - 1>{});
       // a barrier that does not drain vmcnt: __syncthreads() would first wait for every
       // weight load just issued
-      if constexpr (DN_PROBE != 8) raw_barrier();  // #2
-      if constexpr (DN_PROBE != 1) {
+      raw_barrier();  // #2
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) rr[mt] = sm_r[mt * 16 + (lane & 15)];
-      }
+      for (int mt = 0; mt < MT; ++mt) rr[mt] = sm_r[mt * 16 + (lane & 15)];
     }
   } else if (nbw > 0) {
     // prologue: stages 0..D-2 (all D with FULL_PROLOGUE)
@@ -354,7 +332,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       // keep the issued loads ahead of the MFMAs (the scheduler would otherwise
       // interleave them to save registers, leaving few loads in flight)
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (NORM == DN_EXACT && DN_PROBE != 2) {
+      if constexpr (NORM == DN_EXACT) {
 #pragma unroll
         for (int u = 0; u < TW; ++u) {
           const int wo = (min(b, nb - 1) * TW + u) * 32 + 8 * (lane >> 4);
@@ -387,16 +365,6 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
         for (int s = 0; s < S; ++s)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) acc[s][mt] = mfma16(av[d][u][mt], wv[d][s][u], acc[s][mt]);
-      if constexpr (NORM == DN_FOLD) {
-#pragma unroll
-        for (int u = 0; u < TW; ++u)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const u16x8 xv = __builtin_bit_cast(u16x8, av[d][u][mt]);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) ssq[mt] = fmaf(bf2f(xv[j]), bf2f(xv[j]), ssq[mt]);
-          }
-      }
       __builtin_amdgcn_sched_barrier(0);
       b += NW;
       if (b >= nb) fin = true;
@@ -424,16 +392,6 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) red[wave][(s * MT + mt) * 64 + lane] = acc[s][mt];
   }
-  if constexpr (NORM == DN_FOLD) {
-    // lanes l, l^16, l^32, l^48 hold the four k-quarters of row (l & 15)
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      float t = ssq[mt];
-      t += __shfl_xor(t, 16);
-      t += __shfl_xor(t, 32);
-      if (lane < 16) sm_ss[wave][mt * 16 + lane] = t;
-    }
-  }
   __syncthreads();
   // thread p < MT*64 owns (mt, lane ln) of every stream s: rows mt*16 + 4*(ln>>4) + r, col ln&15
   const int p = threadIdx.x;
@@ -455,29 +413,8 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       const int row = mt * 16 + 4 * (ln >> 4) + r;
       if (row >= M) continue;
       g.part[((int64_t)blockIdx.y * M + row) * g.ldp + col] = v[0][r];
-      if constexpr (NORM == DN_FOLD) {
-        if (nt == 0 && (ln & 15) == 0) {
-          float t = 0.f;
-#pragma unroll
-          for (int w = 0; w < NW; ++w) t += sm_ss[w][row];
-          g.ssq[blockIdx.y * M + row] = t;
-        }
-      }
     }
     return;
-  }
-  if constexpr (NORM == DN_FOLD) {
-    // folded RMSNorm: out = rsqrt(mean(x^2) + eps) * (x @ (W * w)^T)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rr2 = mt * 16 + 4 * (ln >> 4) + r;
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) t += sm_ss[w][rr2];
-      const float inv = 1.0f / sqrtf(t / (float)(g.KT * 32) + g.eps);
-#pragma unroll
-      for (int s = 0; s < S; ++s) v[s][r] *= inv;
-    }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -530,16 +467,14 @@ static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   using C = DecodeCfg<MT, S>;
   constexpr int T = decode_threads<C::NW, NORM>();
-  if constexpr (NORM != DN_FOLD) {
-    if (a.pack & GEMM_PACK_A) {
-      if (a.KT % C::TW == 0)
-        hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, true>), dim3(a.n_tiles),
-                           dim3(T), (dn_lds_bytes<NORM, S>(a.KT)), s, a);
-      else
-        hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM, true>), dim3(a.n_tiles), dim3(T),
-                           (dn_lds_bytes<NORM, S>(a.KT)), s, a);
-      return;
-    }
+  if (a.pack & GEMM_PACK_A) {
+    if (a.KT % C::TW == 0)
+      hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, true>), dim3(a.n_tiles), dim3(T),
+                         (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+    else
+      hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM, true>), dim3(a.n_tiles), dim3(T),
+                         (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+    return;
   }
   if (a.KT % C::TW == 0)
     hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM>), dim3(a.n_tiles), dim3(T),
@@ -564,9 +499,9 @@ static void decode_mt(const DecodeArgs& a, hipStream_t s) {
 // q/k/v projection of a decode step with K split over `kslices` workgroup slices and the
 // reduction left to the consumer (launch_attn_decode_fused): with NW = 4 the 384 x 2
 // workgroups of Qwen3-8B sit 3 per CU, every CU streaming the same bytes.  `norm` selects
-// the RMSNorm mode: DN_EXACT (ssq_in / n_parts / norm_w), DN_FOLD (writes ssq) or none.
+// the RMSNorm mode: DN_EXACT (ssq_in / n_parts / norm_w) or none.
 void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
-                                float* part, float* ssq, const DecodeNorm& norm, hipStream_t s, int pack) {
+                                float* part, const DecodeNorm& norm, hipStream_t s, int pack) {
   DecodeArgs a = {};
   a.A = A;
   a.lda = lda;
@@ -577,7 +512,6 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
   a.eps = norm.eps;
   a.part = part;
   a.ldp = N;
-  a.ssq = ssq;
   a.ssq_in = norm.ssq_in;
   a.n_parts = norm.n_parts;
   a.norm_w = norm.w;
@@ -589,8 +523,6 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
   else if (norm.mode == DN_EXACT)
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT>), grid,
                        dim3(decode_threads<4, DN_EXACT>()), (dn_lds_bytes<DN_EXACT, 1>(a.KT / kslices)), s, a);
-  else if (norm.mode == DN_FOLD)
-    hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_FOLD>), grid, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_NONE>), grid, dim3(256), 0, s, a);
 }
@@ -603,8 +535,7 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_tiled_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
-    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    const float* __restrict__ rs) {
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M) {
   // LDS: 2 buffers x (A 16 KiB + B 16 KiB), one array (guide §5 trap 4a)
   __shared__ __attribute__((aligned(16))) char lds[2 * 32768];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -705,20 +636,19 @@ __global__ __launch_bounds__(256) void gemm_tiled_kernel(
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wr * 64 + mt * 16 + 4 * (lane >> 4) + r;
       if (row >= M) continue;
-      const float sc = rs ? rs[row] : 1.0f;  // folded RMSNorm row scale
       if constexpr (EPI == EPI_SILU) {
 #pragma unroll
         for (int nt = 0; nt < 2; ++nt) {
           const int col = n0 + wc * 32 + nt * 16 + (lane & 15);
-          float g = rbf(acc[mt][nt][r] * sc);
-          float u = rbf(acc[mt][nt + 2][r] * sc);
+          float g = rbf(acc[mt][nt][r]);
+          float u = rbf(acc[mt][nt + 2][r]);
           C[(int64_t)row * ldc + col] = f2bf(rbf(silu_f(g)) * u);
         }
       } else {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const int col = n0 + wc * 64 + nt * 16 + (lane & 15);
-          float o = acc[mt][nt][r] * sc;
+          float o = acc[mt][nt][r];
           if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(R[(int64_t)row * ldr + col]);
           C[(int64_t)row * ldc + col] = f2bf(o);
         }
@@ -792,8 +722,8 @@ __device__ __forceinline__ void tile_order(const SplitTail& st, int grid_m, int 
 template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
-    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    const float* __restrict__ rs, int grid_m, int grid_n, SplitTail st) {
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M, int grid_m, int grid_n,
+    SplitTail st) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 65536];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
@@ -1022,7 +952,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   for (int i = 0; i < 8; ++i) {
     const int row = m0 + wr * 128 + i * 16 + (lane & 15);
     if (row >= M) continue;
-    const float sc = rs ? rs[row] : 1.0f;
     if constexpr (EPI == EPI_SILU) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
@@ -1030,8 +959,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
         u16x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float gg = rbf(acc[i][nt][r] * sc);
-          const float uu = rbf(acc[i][4 + nt][r] * sc);
+          const float gg = rbf(acc[i][nt][r]);
+          const float uu = rbf(acc[i][4 + nt][r]);
           v[r] = f2bf(rbf(silu_f(gg)) * uu);
         }
         *(u16x4*)(C + (int64_t)row * ldc + col) = v;
@@ -1045,7 +974,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
         if constexpr (EPI == EPI_RESID) rr = *(const u16x4*)(R + (int64_t)row * ldr + col);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float o = acc[i][j][r] * sc;
+          float o = acc[i][j][r];
           if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(rr[r]);
           v[r] = f2bf(o);
         }
@@ -1064,7 +993,7 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 // l^16, l^32, l^48) hold all 128 dims, and dims d and d + 64 (RoPE's rotate_half pair) sit
 // in the same lane (nt and nt + 4).
 __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const QkvEpilogue& e, int row0, int hd, int M,
-                                             const float* __restrict__ rs, int lane) {
+                                             int lane) {
   const int q4 = lane >> 4;  // dims 4*q4 .. 4*q4+3 of every 16-dim tile
   if (hd < e.H + e.KV) {
     const bool isq = hd < e.H;
@@ -1075,14 +1004,12 @@ __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const Qkv
     // per-row operands up front, the cos/sin rows two-deep: the loads of row i+1 are in
     // flight while row i computes (dependent per-row loads were the epilogue's cost)
     int pos[8], slot[8];
-    float scv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int row = row0 + 16 * i + (lane & 15);
       const int rowc = row < M ? row : M - 1;
       pos[i] = e.positions[rowc];
       slot[i] = isq ? 0 : e.slots[rowc];
-      scv[i] = rs ? rs[rowc] : 1.0f;
     }
     u16x4 cvb[2][4], svb[2][4];
     auto load_cs = [&](int i, int bsel) {
@@ -1097,14 +1024,13 @@ __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const Qkv
     for (int i = 0; i < 8; ++i) {
       if (i + 1 < 8) load_cs(i + 1, (i + 1) & 1);
       const int row = row0 + 16 * i + (lane & 15);
-      const float sc = scv[i];
       float x[8][4];
       float ss = 0.f;
 #pragma unroll
       for (int nt = 0; nt < 8; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          x[nt][r] = rbf(acc[i][nt][r] * sc);  // the bf16 projection output
+          x[nt][r] = rbf(acc[i][nt][r]);  // the bf16 projection output
           ss = fmaf(x[nt][r], x[nt][r], ss);
         }
       ss += __shfl_xor(ss, 16);
@@ -1145,20 +1071,14 @@ __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const Qkv
   } else {  // v head: the bf16 projection output, scattered into the V^T tile layout
     const int g = hd - e.H - e.KV;
     int slots[8];
-    float scv[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int rowc = min(row0 + 16 * i + (lane & 15), M - 1);
-      slots[i] = e.slots[rowc];
-      scv[i] = rs ? rs[rowc] : 1.0f;
-    }
+    for (int i = 0; i < 8; ++i) slots[i] = e.slots[min(row0 + 16 * i + (lane & 15), M - 1)];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int row = row0 + 16 * i + (lane & 15);
       if (row >= M) continue;
       const int slot = slots[i];
       if (slot < 0) continue;
-      const float sc = scv[i];
       const int page = slot >> 6, s = slot & 63;
       u16* blk = e.kv_layer + kv_block(page, 1, g, e.KV);
       const int kt = s >> 5, tp = s & 31;
@@ -1169,7 +1089,7 @@ __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const Qkv
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int ln = 4 * q4 + r + 16 * gg;  // d & 15 = 4 q4 + r, d >> 4 = nt
-          blk[((kt * 8 + nt) * 64 + ln) * 8 + jj] = f2bf(acc[i][nt][r] * sc);
+          blk[((kt * 8 + nt) * 64 + ln) * 8 + jj] = f2bf(acc[i][nt][r]);
         }
     }
   }
@@ -1187,20 +1107,19 @@ __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const Qkv
 template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,
-    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M,
-    const float* __restrict__ rs, int grid_m, int grid_n, SplitTail st, int nunits, QkvEpilogue qe) {
+    u16* __restrict__ C, int64_t ldc, const u16* __restrict__ R, int64_t ldr, int M, int grid_m, int grid_n,
+    SplitTail st, int nunits, QkvEpilogue qe) {
   __shared__ __attribute__((aligned(16))) char lds[2 * 65536 + 16];  // + the split ticket
   typedef __attribute__((address_space(3))) void* lds_ptr;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  // vector-memory operations per wave in one epilogue (+8 row-scale loads when rs)
+  // vector-memory operations per wave in one epilogue
   constexpr int EPI_OPS = EPI == EPI_SILU ? 32 : EPI == EPI_RESID ? 128 : 64;
   const __amdgpu_buffer_rsrc_t c_rsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, (int)((int64_t)M * ldc * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t r_rsrc =
       __builtin_amdgcn_make_buffer_rsrc((void*)R, 0, R ? (int)((int64_t)M * ldr * 2) : 0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rs_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)rs, 0, rs ? M * 4 : 0, 0x00020000);
 
   struct Unit {
     int m0, n0, nK, slice, nsl, sidx;
@@ -1353,8 +1272,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     // previous epilogue's EPI_OPS (fewer only when a split slice drained with vmcnt(0))
     if (first || EPI == EPI_QKV) {  // EPI_QKV: its epilogue's count varies by head kind
       vm_wait<16>();
-    } else if (rs) {
-      vm_wait<(16 + EPI_OPS + 8 < 63 ? 16 + EPI_OPS + 8 : 63)>();
     } else {
       vm_wait<(16 + EPI_OPS < 63 ? 16 + EPI_OPS : 63)>();
     }
@@ -1384,15 +1301,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     acc_fence();
 
     if constexpr (EPI == EPI_QKV) {
-      qkv_epilogue(acc, qe, u.m0 + wr * 128, (u.n0 >> 7) + wc, M, rs, lane);
+      qkv_epilogue(acc, qe, u.m0 + wr * 128, (u.n0 >> 7) + wc, M, lane);
     } else {  // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
       // buffer loads/stores: rows >= M are issued and dropped by the range check, so the
       // epilogue's vector-memory count is fixed (EPI_OPS) and the next unit's wait is exact
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int row = u.m0 + wr * 128 + i * 16 + (lane & 15);
-        float sc = 1.0f;
-        if (rs) sc = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_rsrc, row * 4, 0, 0));
         if constexpr (EPI == EPI_SILU) {
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
@@ -1400,8 +1315,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
             u16x4 o;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float gg = rbf(acc[i][nt][r] * sc);
-              const float uu = rbf(acc[i][4 + nt][r] * sc);
+              const float gg = rbf(acc[i][nt][r]);
+              const float uu = rbf(acc[i][4 + nt][r]);
               o[r] = f2bf(rbf(silu_f(gg)) * uu);
             }
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o), c_rsrc, (row * (int)ldc + col) * 2, 0,
@@ -1418,7 +1333,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
                                                                                    0, 0));
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float x = acc[i][j][r] * sc;
+              float x = acc[i][j][r];
               if constexpr (EPI == EPI_RESID) x = rbf(x) + bf2f(rr[r]);
               o[r] = f2bf(x);
             }
@@ -1442,26 +1357,20 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
   }
 }
 
-static int env_or(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
-
 static void w4_launch(int epi, int grid, hipStream_t s, const u16* A, int64_t lda, const u16* Wp, int KT, int ntw,
-                      u16* C, int64_t ldc, const u16* R, int64_t ldr, int M, const float* rs, int gm, int gn,
-                      const SplitTail& st) {
+                      u16* C, int64_t ldc, const u16* R, int64_t ldr, int M, int gm, int gn, const SplitTail& st) {
   switch (epi) {
     case EPI_NONE:
       hipLaunchKernelGGL((gemm_w4_kernel<EPI_NONE>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
-                         M, rs, gm, gn, st);
+                         M, gm, gn, st);
       break;
     case EPI_RESID:
       hipLaunchKernelGGL((gemm_w4_kernel<EPI_RESID>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                         ldr, M, rs, gm, gn, st);
+                         ldr, M, gm, gn, st);
       break;
     default:
       hipLaunchKernelGGL((gemm_w4_kernel<EPI_SILU>), dim3(grid), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R,
-                         ldr, M, rs, gm, gn, st);
+                         ldr, M, gm, gn, st);
       break;
   }
 }
@@ -1481,43 +1390,38 @@ static int w4p_grid(int units) {
   return ncu[dev] & ~7;
 }
 
+// The tail split's fixed maximum: each XCD cuts its last `rem` tiles into 32 / rem slices, so
+// rem * split = 32 slices of a 256x256 fp32 tile per XCD, and 2 x 8 x rem <= 512 tickets.
+#define SPLIT_WS_BYTES ((size_t)8 * 32 * 65536 * sizeof(float))
+#define SPLIT_CNT_N 512
+
+int gemm_ws_alloc(GemmWs* w) {
+  if (!w->split) return hipSuccess;
+  hipError_t e = hipMalloc((void**)&w->ws, SPLIT_WS_BYTES);
+  if (e == hipSuccess) e = hipMalloc((void**)&w->cnt, SPLIT_CNT_N * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(w->cnt, 0, SPLIT_CNT_N * sizeof(unsigned));
+  return (int)e;
+}
+
 void gemm_ws_free(GemmWs* w) {
   if (!w) return;
   if (w->ws) (void)hipFree(w->ws);
   if (w->cnt) (void)hipFree(w->cnt);
-  *w = GemmWs{};
+  w->ws = nullptr;
+  w->cnt = nullptr;
 }
 
 // Tail-split plan for `tiles` 256x256 tiles of nK K-steps on 8 XCDs x 32 CUs (one workgroup
-// per CU), with its fp32 partials and tickets in the caller's (span's) workspace: allocated
-// zeroed and grown on demand, never inside a graph capture (no workspace, or capturing: no
-// split).  INFERD_GEMM_SPLIT=0 disables it (A/B).
-static SplitTail plan_split_tail(int tiles, int nK, GemmWs* w, hipStream_t s) {
+// per CU), with its fp32 partials and tickets in the caller's (span's) preallocated workspace
+// (no workspace, or split = 0: no split).  Nothing here allocates, so it is capture-safe.
+static SplitTail plan_split_tail(int tiles, int nK, const GemmWs* w) {
   SplitTail st = {1, 0, 0, 0, nullptr, nullptr};
-  if (!w || env_or("INFERD_GEMM_SPLIT", 1) == 0) return st;
+  if (!w || !w->split || !w->ws || !w->cnt) return st;
   if (tiles % 8) return st;
   const int per = tiles / 8, rem = per % 32;
   if (rem == 0 || 32 % rem) return st;
   const int split = 32 / rem;
   if (split > 8 || nK % split || nK / split < 3) return st;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return st;
-  const size_t bytes = (size_t)8 * rem * split * 65536 * sizeof(float);
-  if (bytes > w->ws_bytes) {
-    if (w->ws) (void)hipFree(w->ws);
-    w->ws = nullptr;
-    w->ws_bytes = 0;
-    if (hipMalloc((void**)&w->ws, bytes) != hipSuccess) return st;
-    w->ws_bytes = bytes;
-  }
-  if (2 * 8 * rem > w->cnt_n) {
-    if (w->cnt) (void)hipFree(w->cnt);
-    w->cnt = nullptr;
-    w->cnt_n = 0;
-    if (hipMalloc((void**)&w->cnt, 2 * 8 * rem * sizeof(unsigned)) != hipSuccess) return st;
-    if (hipMemsetAsync(w->cnt, 0, 2 * 8 * rem * sizeof(unsigned), s) != hipSuccess) return st;
-    w->cnt_n = 2 * 8 * rem;
-  }
   st.split = split;
   st.tiles_per_xcd = per;
   st.full_per_xcd = per - rem;
@@ -1540,21 +1444,16 @@ bool gemm_uses_tiled(int M, int N, int K, int epi) {
 }
 
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
-                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
-                 const RowNorm* fold, GemmWs* ws, const DecodeNorm* dn, float* ssq_out, int pack) {
+                 const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s, const GemmWs* ws,
+                 const DecodeNorm* dn, float* ssq_out, int pack) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
   const bool tiled = gemm_uses_tiled(M, N, K, epi);
-  const float* rs = nullptr;
-  if (fold && tiled) {
-    launch_row_inv_rms(A, lda, M, K, fold->eps, fold->rs_ws, s);
-    rs = fold->rs_ws;
-  }
   if (tiled && use_w4(M, N, K, epi)) {
     const int ncols = (epi == EPI_SILU) ? 128 : 256;
     const int gm = (M + 255) / 256, gn = N / ncols;
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
-    const SplitTail st = plan_split_tail(gm * gn, K / 64, ws, s);
+    const SplitTail st = plan_split_tail(gm * gn, K / 64, ws);
     const int grid = st.split > 1 ? 8 * st.units_per_xcd : gm * gn;
     // w4p addresses C / R through 32-bit buffer offsets
     const bool fits32 = (int64_t)(M + 256) * ldc * 2 < 0x7fffffff && (!R || (int64_t)(M + 256) * ldr * 2 < 0x7fffffff);
@@ -1563,20 +1462,20 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
       switch (epi) {
         case EPI_NONE:
           hipLaunchKernelGGL(gemm_w4p_kernel<EPI_NONE>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
-                             M, rs, gm, gn, st, grid, QkvEpilogue{});
+                             M, gm, gn, st, grid, QkvEpilogue{});
           break;
         case EPI_RESID:
           hipLaunchKernelGGL(gemm_w4p_kernel<EPI_RESID>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
-                             M, rs, gm, gn, st, grid, QkvEpilogue{});
+                             M, gm, gn, st, grid, QkvEpilogue{});
           break;
         default:
           hipLaunchKernelGGL(gemm_w4p_kernel<EPI_SILU>, dim3(g), dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr,
-                             M, rs, gm, gn, st, grid, QkvEpilogue{});
+                             M, gm, gn, st, grid, QkvEpilogue{});
           break;
       }
       return;
     }
-    w4_launch(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs, gm, gn, st);  // tail split
+    w4_launch(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, gm, gn, st);  // tail split
     return;
   }
   if (tiled) {
@@ -1585,20 +1484,20 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     const int ntw = (epi == EPI_SILU) ? 2 * n_tiles : n_tiles;
     switch (epi) {
       case EPI_NONE:
-        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_NONE>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
+        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_NONE>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
         break;
       case EPI_RESID:
-        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_RESID>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
+        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_RESID>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
         break;
       default:
-        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_SILU>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, rs);
+        hipLaunchKernelGGL(gemm_tiled_kernel<EPI_SILU>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
         break;
     }
     return;
   }
   // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail; the
   // DN_EXACT norm and the ssq_out partials are defined for M <= 64 only)
-  const int mode = fold ? DN_FOLD : (dn ? dn->mode : DN_NONE);
+  const int mode = dn ? dn->mode : DN_NONE;
   if ((mode == DN_EXACT || ssq_out) && M > 64) return;
   for (int m0 = 0; m0 < M; m0 += 64) {
     DecodeArgs a = {};
@@ -1613,21 +1512,13 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     a.R = R ? R + (int64_t)m0 * ldr : nullptr;
     a.ldr = ldr;
     a.keys = keys;
-    a.eps = fold ? fold->eps : (dn ? dn->eps : 0.f);
+    a.eps = dn ? dn->eps : 0.f;
     a.ssq_out = (epi == EPI_RESID) ? ssq_out : nullptr;
     a.pack = pack;
     if (mode == DN_EXACT) {
       a.ssq_in = dn->ssq_in;
       a.n_parts = dn->n_parts;
       a.norm_w = dn->w;
-    }
-    if (mode == DN_FOLD) {
-      switch (epi) {
-        case EPI_NONE: decode_mt<EPI_NONE, DN_FOLD>(a, s); break;
-        case EPI_SILU: decode_mt<EPI_SILU, DN_FOLD>(a, s); break;
-        default: return;  // the span folds norms into the NONE (qkv) and SILU (gate/up) GEMMs only
-      }
-    } else if (mode == DN_EXACT) {
       switch (epi) {
         case EPI_NONE: decode_mt<EPI_NONE, DN_EXACT>(a, s); break;
         case EPI_SILU: decode_mt<EPI_SILU, DN_EXACT>(a, s); break;
@@ -1685,11 +1576,10 @@ void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
 // launch_gemm's persistent whole-tile path with the EPI_QKV epilogue: q/k RMSNorm + RoPE to
 // q_out and the K cache, V to the cache (what launch_qk_norm_rope_kv does from a stored q/k/v
 // row).  Needs that path: the 4-wave persistent kernel selected, no tail split, 32-bit C offsets
-// (C is unused here) and one head per wave column (N = (H + 2 KV) * 128).
-// INFERD_FUSE_QKV_EPI=0 keeps the two-kernel path (A/B).
-bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const RowNorm* norm,
-                           const QkvEpilogue& e, hipStream_t s) {
-  if (env_or("INFERD_FUSE_QKV_EPI", 1) == 0) return false;
+// (C is unused here) and one head per wave column (N = (H + 2 KV) * 128).  The span skips it
+// (two-kernel path, A/B) when created with INFERD_FUSE_QKV_EPI=0.
+bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const QkvEpilogue& e,
+                           hipStream_t s) {
   if (!gemm_uses_tiled(M, N, K, EPI_NONE) || !use_w4(M, N, K, EPI_NONE)) return false;
   if (N != (e.H + 2 * e.KV) * HEAD_DIM) return false;
   const int gm = (M + 255) / 256, gn = N / 256;
@@ -1702,13 +1592,8 @@ bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int 
       if (split <= 8 && nK % split == 0 && nK / split >= 3) return false;
     }
   }
-  const float* rs = nullptr;
-  if (norm) {
-    launch_row_inv_rms(A, lda, M, K, norm->eps, norm->rs_ws, s);
-    rs = norm->rs_ws;
-  }
   const SplitTail st = {1, 0, 0, 0, nullptr, nullptr};
   hipLaunchKernelGGL(gemm_w4p_kernel<EPI_QKV>, dim3(w4p_grid(tiles)), dim3(256), 0, s, A, lda, Wp, K / 32, N / 16,
-                     (u16*)nullptr, (int64_t)0, (const u16*)nullptr, (int64_t)0, M, rs, gm, gn, st, tiles, e);
+                     (u16*)nullptr, (int64_t)0, (const u16*)nullptr, (int64_t)0, M, gm, gn, st, tiles, e);
   return true;
 }

@@ -33,8 +33,7 @@ struct QkvEpilogue {
 
 // elementwise.hip
 void launch_weightgen(u16* dst, int64_t n, uint64_t key, float scale, float center, hipStream_t s);
-// colscale (optional, bf16 [K]): packs bf16(W[n][k] * colscale[k]) (a folded RMSNorm weight)
-void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s, const u16* colscale = nullptr);
+void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s);
 void launch_unpack(const u16* src, int N, int K, u16* dst, hipStream_t s);
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
                     u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out = false);
@@ -42,7 +41,7 @@ void launch_rope_table(const float* inv_freq, int max_pos, u16* cos_t, u16* sin_
 void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positions,
                             const int32_t* slots, const u16* qn_w, const u16* kn_w,
                             const u16* cos_t, const u16* sin_t, u16* q_out, u16* kv_layer, int M,
-                            int H, int KV, float eps, hipStream_t s, bool skip_q = false);
+                            int H, int KV, float eps, hipStream_t s);
 void launch_embed(const int32_t* ids, const u16* table, int M, int N, int vocab, u16* out,
                   int32_t* err, hipStream_t s);
 void launch_argmax_decode(const unsigned long long* keys, int B, int32_t* ids, hipStream_t s);
@@ -53,16 +52,8 @@ void launch_decode_advance(int32_t* positions, int32_t* slots, int32_t* ctx_lens
 // packed weight holds 2N rows ([gate; up]).  For EPI_ARGMAX `partial` receives
 // (N/16) x M keys and `amax_keys` the per-row reduction (M <= 64).
 bool gemm_uses_tiled(int M, int N, int K, int epi);
-// Folded RMSNorm (INFERD_NORM_FOLD=1, kept for A/B against the exact path): Wp was packed with
-// the norm weight folded in (W[n][k] * w[k]); the GEMM reads the RAW activations and scales
-// each output row by rsqrt(mean(A_row^2) + eps) -- computed in-kernel from the A fragments on
-// the decode path, by a row kernel into rs_ws [M] floats on the tiled (prefill) path.
-struct RowNorm {
-  float eps;
-  float* rs_ws;
-};
 // RMSNorm modes of the decode (M <= 64) GEMV
-enum { DN_NONE = 0, DN_FOLD = 1, DN_EXACT = 2 };
+enum { DN_NONE = 0, DN_EXACT = 2 };
 // DN_EXACT: Qwen3RMSNorm at the reference's rounding points applied to A inside the GEMV,
 // A' = bf16(w * bf16(A * r)), r = 1 / sqrt(sum_p ssq_in[p * MP + row] / K + eps) (MP = M rounded
 // up to a multiple of 4: compact parts, so a wave's loads cover whole cache lines): the row sums
@@ -75,22 +66,23 @@ struct DecodeNorm {
   int n_parts;
   const u16* w;
 };
-// Per-span GEMM workspace: the prefill tail split's fp32 partials and tickets, grown on
-// demand outside graph captures (one workspace per span, so spans on different streams never
-// share tickets).
+// Per-span GEMM workspace: the prefill tail split's fp32 partials and tickets, allocated once
+// at span creation (gemm_ws_alloc: the split's fixed maximum, 8 XCDs x 32 slices of a 256x256
+// fp32 tile = 64 MiB, and 512 zeroed tickets), so a forward call never allocates and a graph
+// capture may contain the split (one workspace per span: spans on different streams never
+// share tickets).  split = 0 disables the tail split (INFERD_GEMM_SPLIT=0, read at creation).
 struct GemmWs {
   float* ws = nullptr;
-  size_t ws_bytes = 0;
   unsigned* cnt = nullptr;
-  int cnt_n = 0;
+  int split = 1;
 };
+int gemm_ws_alloc(GemmWs* w);  // hipError_t as int
 void gemm_ws_free(GemmWs* w);
 // ssq_out (EPI_RESID, M <= 64): per 16-column tile sums of squares of the stored outputs,
 // [N/16][64] floats -- the DecodeNorm input of the next normed GEMV.
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
-                 const RowNorm* fold = nullptr, GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr,
-                 float* ssq_out = nullptr, int pack = 0);
+                 const GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr, float* ssq_out = nullptr, int pack = 0);
 // launch_gemm `pack` bits (decode path, M <= 64 only; common.h packed_index): A is read
 // fragment-packed / the EPI_SILU or EPI_RESID output C is written so / the EPI_RESID residual
 // R is read so
@@ -98,14 +90,12 @@ enum { GEMM_PACK_A = 1, GEMM_PACK_C = 2, GEMM_PACK_R = 4 };
 // prefill q/k/v projection fused with q/k RMSNorm + RoPE and the K/V cache write (the
 // persistent GEMM's epilogue); returns false, launching nothing, where that body does not
 // apply (the caller then runs launch_gemm + launch_qk_norm_rope_kv)
-bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const RowNorm* fold,
-                           const QkvEpilogue& e, hipStream_t s);
-// decode q/k/v with K split over `kslices` (M <= 16): part [kslices][M][N] fp32 (and with
-// DN_FOLD ssq [kslices][M] fp32); the fused decode attention reduces them
+bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const QkvEpilogue& e,
+                           hipStream_t s);
+// decode q/k/v with K split over `kslices` (M <= 16): part [kslices][M][N] fp32; the fused
+// decode attention reduces them
 void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
-                                float* part, float* ssq, const DecodeNorm& norm, hipStream_t s, int pack = 0);
-// rs[row] = 1 / sqrt(mean(x[row][:K]^2) + eps)
-void launch_row_inv_rms(const u16* x, int64_t ldx, int M, int K, float eps, float* rs, hipStream_t s);
+                                float* part, const DecodeNorm& norm, hipStream_t s, int pack = 0);
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
                           int32_t* ids, hipStream_t s);
 
@@ -120,6 +110,10 @@ struct AttnBatch {
   int M;
   int max_q_len;
   int max_ctx;
+  // launch shape knobs (the span's, read once at inferd_span_create; 0 = the measured default):
+  // decode waves per workgroup / chunks per (sequence, kv head), per-lane q loads instead of
+  // the staged q image, prefill block order (-1 default, 0 head-major, 1 XCD-grouped)
+  int nw = 0, nc = 0, qlanes = 0, order = -1;
 };
 // q [M][H][128] bf16 -> out [M][H*128] bf16.  kv_layer: this layer's pool base.
 void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
@@ -128,20 +122,15 @@ void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, i
 // launch_qk_norm_rope_kv + launch_attn_decode on the decode path): qkv is the raw
 // [M][(H+2KV)*128] projection output.
 // With `part` non-null the q/k/v come from launch_gemm_decode_partial's fp32 K-slices
-// (part [ksl][M][ldqkv], K = hidden) instead of the bf16 rows `qkv`; ssq [ksl][M] (folded
-// norm) scales their sum by rsqrt(sum ssq / K + eps), null means the slices were normed.
+// (part [ksl][M][ldqkv], already normed) instead of the bf16 rows `qkv`.
 // pack_out: `out` is written fragment-packed (common.h packed_index, whole 16-row tiles).
 void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, const u16* kn_w, const u16* cos_t,
                               const u16* sin_t, float eps, u16* kv_layer, const AttnBatch& b, int H, int KV,
                               float scale, u16* out, float* ws, hipStream_t s, const float* part = nullptr,
-                              const float* ssq = nullptr, int ksl = 0, int K = 0, bool pack_out = false);
+                              int ksl = 0, bool pack_out = false);
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx);
-// With qkv non-null the kernel applies the q-norm + RoPE itself from the raw q/k/v rows
-// (qkv [M][ldqkv], q ignored); launch_qk_norm_rope_kv then only needs skip_q = true.
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
-                         float scale, u16* out, hipStream_t s, const u16* qkv = nullptr, int64_t ldqkv = 0,
-                         const u16* qn_w = nullptr, const u16* cos_t = nullptr, const u16* sin_t = nullptr,
-                         float eps = 0.f);
+                         float scale, u16* out, hipStream_t s);
 
 // sets the thread-local message of inferd_last_error() and returns `code` (span.hip)
 int inferd_fail(int code, const std::string& msg);

@@ -98,6 +98,22 @@ extern "C" int inferd_kv_advance(InferdKvTable* t, uint64_t seq, int32_t n) {
   return INFERD_OK;
 }
 
+extern "C" int inferd_kv_advance_many(InferdKvTable* t, const uint64_t* seqs, int32_t n_seqs, int32_t n) {
+  if (!t || n < 0 || n_seqs < 0 || (n_seqs > 0 && !seqs)) return inferd_fail(INFERD_ERR_ARG, "kv_advance_many: bad argument");
+  std::vector<InferdKvTable::Seq*> ss(n_seqs);
+  for (int32_t i = 0; i < n_seqs; ++i) {  // validate all first: all or nothing
+    auto it = t->seqs.find(seqs[i]);
+    if (it == t->seqs.end()) return inferd_fail(INFERD_ERR_ARG, "kv_advance_many: sequence not reserved");
+    if ((int64_t)it->second.length + n > (int64_t)it->second.pages.size() * P)
+      return inferd_fail(INFERD_ERR_ARG, "kv_advance_many: past the reserved pages");
+    for (int32_t j = 0; j < i; ++j)
+      if (ss[j] == &it->second) return inferd_fail(INFERD_ERR_ARG, "kv_advance_many: a sequence may appear only once");
+    ss[i] = &it->second;
+  }
+  for (auto* q : ss) q->length += n;
+  return INFERD_OK;
+}
+
 extern "C" int inferd_kv_release(InferdKvTable* t, uint64_t seq) {
   if (!t) return inferd_fail(INFERD_ERR_ARG, "kv_release: null table");
   auto it = t->seqs.find(seq);

@@ -44,7 +44,7 @@ int inferd_fail(int code, const std::string& msg) { return fail(code, msg); }
   } while (0)
 
 extern "C" const char* inferd_last_error(void) { return g_err.c_str(); }
-extern "C" int inferd_abi_version(void) { return 1; }
+extern "C" int inferd_abi_version(void) { return 2; }
 
 namespace {
 
@@ -57,12 +57,7 @@ struct LayerW {
   u16* post_ln = nullptr;
   u16* q_norm = nullptr;
   u16* k_norm = nullptr;
-  // The RMSNorm weights are folded into the packed projections that consume them
-  // (in_ln -> q/k/v, post_ln -> gate/up; see gemm.hip RowNorm).  A projection packed
-  // before its norm weight was (re)set is stale: forward refuses to run.
-  uint32_t stale = 0;
 };
-enum { STALE_Q = 1, STALE_K = 2, STALE_V = 4, STALE_GATE = 8, STALE_UP = 16 };
 
 // tensor ids shared with oracle/weightgen.py
 enum { T_Q = 0, T_K, T_V, T_O, T_QN, T_KN, T_INLN, T_POSTLN, T_GATE, T_UP, T_DOWN };
@@ -77,6 +72,39 @@ enum { PROF_NORM = 0, PROF_QKV, PROF_ROPE, PROF_ATTN, PROF_O, PROF_GATEUP, PROF_
 
 uint64_t tensor_key(uint64_t seed, uint32_t tid) {
   return splitmix64(((seed & 0xFFFFFFFFull) << 32) | (uint64_t)tid);
+}
+
+// A/B and lab settings, read from the environment once, at inferd_span_create (never on the
+// forward path).  Defaults are the measured optimum.
+struct Knobs {
+  bool fuse_decode_rope = true;  // INFERD_FUSE_DECODE_ROPE=0: separate qk_norm_rope_kv launch on decode
+  bool pack_act = true;          // INFERD_PACK_ACT=0: row-major decode activations
+  int qkv_split = 2;             // INFERD_QKV_SPLIT: decode q/k/v K-slices (reduced by the attention)
+  bool fuse_qkv_epi = true;      // INFERD_FUSE_QKV_EPI=0: prefill q/k norm + RoPE + cache write as a launch
+  int gemm_split = 1;            // INFERD_GEMM_SPLIT=0: no prefill tail split
+  int attn_nw = 0, attn_nc = 0;  // INFERD_ATTN_NW / _NC: decode attention shape (0: default)
+  int attn_qlanes = 0;           // INFERD_ATTN_QLANES=1: per-lane q loads in the fused decode attention
+  int attn_order = -1;           // INFERD_ATTN_ORDER: prefill block order (-1: default)
+};
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
+Knobs knobs_from_env() {
+  Knobs k;
+  k.fuse_decode_rope = env_int("INFERD_FUSE_DECODE_ROPE", 1) != 0;
+  k.pack_act = env_int("INFERD_PACK_ACT", 1) != 0;
+  k.qkv_split = env_int("INFERD_QKV_SPLIT", 2);
+  if (k.qkv_split < 1 || k.qkv_split > QKV_KSL_MAX) k.qkv_split = 1;
+  k.fuse_qkv_epi = env_int("INFERD_FUSE_QKV_EPI", 1) != 0;
+  k.gemm_split = env_int("INFERD_GEMM_SPLIT", 1) != 0;
+  k.attn_nw = env_int("INFERD_ATTN_NW", 0);
+  k.attn_nc = env_int("INFERD_ATTN_NC", 0);
+  k.attn_qlanes = env_int("INFERD_ATTN_QLANES", 0);
+  k.attn_order = env_int("INFERD_ATTN_ORDER", -1);
+  return k;
 }
 
 }  // namespace
@@ -96,18 +124,16 @@ struct InferdSpan {
       *last = nullptr;
   float* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
-  // RMSNorm: exact (default; the reference's rounding points) or folded (INFERD_NORM_FOLD=1 at
-  // span creation, A/B).  Exact on the decode GEMV path (<= 64 rows): the o and down GEMVs
-  // write per-tile row sums of squares of their outputs (ssq_post / ssq_in, [hidden/16][MP], MP = rows rounded up to 4, <= 64),
-  // and the gate/up and next layer's q/k/v GEMVs normalise their A fragments from them;
-  // otherwise (a span's first layer, prefill) rmsnorm_kernel writes the normed rows to xn.
-  bool norm_fold = false;
+  Knobs knobs;
+  // RMSNorms at the reference's rounding points (qwen3_server_module.py:19-25).  On the decode
+  // GEMV path (<= 64 rows) the o and down GEMVs write per-tile row sums of squares of their
+  // outputs (ssq_post / ssq_in, [hidden/16][MP], MP = rows rounded up to 4, <= 64), and the
+  // gate/up and next layer's q/k/v GEMVs normalise their A fragments from them; otherwise (a
+  // span's first layer, prefill) rmsnorm_kernel writes the normed rows to xn.
   float* ssq_in = nullptr;
   float* ssq_post = nullptr;
-  GemmWs gws;              // prefill tail-split workspace (per span: spans never share tickets)
-  float* rs_ws = nullptr;  // folded-norm row scales of the prefill GEMMs [max_tokens]
+  GemmWs gws;                 // prefill tail-split workspace (per span: spans never share tickets)
   float* qkv_part = nullptr;  // decode split-K q/k/v partials [QKV_KSL_MAX][16][qkv_rows]
-  float* qkv_ssq = nullptr;   // and their row sums of squares [QKV_KSL_MAX][16]
   unsigned long long* argmax_partial = nullptr;
   int32_t* err = nullptr;
   std::vector<void*> allocs;
@@ -165,12 +191,10 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
     return fail(INFERD_ERR_ARG, "bad span sizes");
   if (c.has_lm_head && c.max_seqs > 64)
     return fail(INFERD_ERR_ARG, "a span with lm_head takes max_seqs <= 64 (the greedy argmax is per call of <= 64 rows)");
+  if (c.kv_pages > (1 << 24)) return fail(INFERD_ERR_ARG, "kv_pages must be <= 2^24");
   InferdSpan* s = new InferdSpan();
   s->cfg = c;
-  {
-    const char* e = getenv("INFERD_NORM_FOLD");
-    s->norm_fold = e && *e == '1';
-  }
+  s->knobs = knobs_from_env();
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
   s->layers.resize(c.n_layers);
   int rc = 0;
@@ -237,9 +261,11 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->ssq_in, (size_t)(h / 16) * 64 * 4);
   SALLOC(s->ssq_post, (size_t)(h / 16) * 64 * 4);
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
-  SALLOC(s->rs_ws, (size_t)c.max_tokens * 4);
   SALLOC(s->qkv_part, (size_t)QKV_KSL_MAX * 16 * s->qkv_rows() * 4);
-  SALLOC(s->qkv_ssq, (size_t)QKV_KSL_MAX * 16 * 4);
+  // the prefill tail split's workspace, once (a forward never allocates): only spans whose
+  // calls can reach the 256x256 GEMMs (>= 512 rows) need it
+  s->gws.split = s->knobs.gemm_split && c.max_tokens >= 512;
+  if (gemm_ws_alloc(&s->gws) != (int)hipSuccess) return bail(fail(INFERD_ERR_HIP, "tail-split workspace allocation failed"));
   SALLOC(s->err, 256);
   if (hipMemset(s->err, 0, 4) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(INFERD_ERR_HIP, "init sync failed"));
@@ -257,9 +283,6 @@ struct Target {
   int packed;     // 1: fragment-pack at n-tile offset
   int64_t rows, cols;
   uint32_t tid_idx;
-  const u16* fold = nullptr;  // norm weight folded into this projection at pack time
-  uint32_t stale_bit = 0;     // this projection's STALE_* bit
-  uint32_t marks = 0;         // a norm weight: projections it makes stale
 };
 
 int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t);
@@ -274,13 +297,7 @@ int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
     return fail(INFERD_ERR_ARG, std::string("unknown/unowned global weight ") + name);
   }
   if (layer >= c.n_layers) return fail(INFERD_ERR_ARG, "layer index out of span");
-  const int rc = resolve_layer(s, layer, name, t);
-  if (!rc && !s->norm_fold) {  // exact norms: nothing is folded, no order between weights
-    t->fold = nullptr;
-    t->stale_bit = 0;
-    t->marks = 0;
-  }
-  return rc;
+  return resolve_layer(s, layer, name, t);
 }
 
 int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t) {
@@ -288,17 +305,17 @@ int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t) {
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
   LayerW& L = s->layers[layer];
   const int64_t qrows = (int64_t)H * HEAD_DIM, kvrows = (int64_t)KV * HEAD_DIM;
-  if (!strcmp(name, "q_proj")) { *t = {L.qkv, 1, qrows, h, T_Q, L.in_ln, STALE_Q}; return 0; }
-  if (!strcmp(name, "k_proj")) { *t = {L.qkv + qrows * h, 1, kvrows, h, T_K, L.in_ln, STALE_K}; return 0; }
-  if (!strcmp(name, "v_proj")) { *t = {L.qkv + (qrows + kvrows) * h, 1, kvrows, h, T_V, L.in_ln, STALE_V}; return 0; }
+  if (!strcmp(name, "q_proj")) { *t = {L.qkv, 1, qrows, h, T_Q}; return 0; }
+  if (!strcmp(name, "k_proj")) { *t = {L.qkv + qrows * h, 1, kvrows, h, T_K}; return 0; }
+  if (!strcmp(name, "v_proj")) { *t = {L.qkv + (qrows + kvrows) * h, 1, kvrows, h, T_V}; return 0; }
   if (!strcmp(name, "o_proj")) { *t = {L.o, 1, h, qrows, T_O}; return 0; }
-  if (!strcmp(name, "gate_proj")) { *t = {L.gateup, 1, I, h, T_GATE, L.post_ln, STALE_GATE}; return 0; }
-  if (!strcmp(name, "up_proj")) { *t = {L.gateup + (int64_t)I * h, 1, I, h, T_UP, L.post_ln, STALE_UP}; return 0; }
+  if (!strcmp(name, "gate_proj")) { *t = {L.gateup, 1, I, h, T_GATE}; return 0; }
+  if (!strcmp(name, "up_proj")) { *t = {L.gateup + (int64_t)I * h, 1, I, h, T_UP}; return 0; }
   if (!strcmp(name, "down_proj")) { *t = {L.down, 1, h, I, T_DOWN}; return 0; }
   if (!strcmp(name, "q_norm")) { *t = {L.q_norm, 0, 1, HEAD_DIM, T_QN}; return 0; }
   if (!strcmp(name, "k_norm")) { *t = {L.k_norm, 0, 1, HEAD_DIM, T_KN}; return 0; }
-  if (!strcmp(name, "input_layernorm")) { *t = {L.in_ln, 0, 1, h, T_INLN, nullptr, 0, STALE_Q | STALE_K | STALE_V}; return 0; }
-  if (!strcmp(name, "post_attention_layernorm")) { *t = {L.post_ln, 0, 1, h, T_POSTLN, nullptr, 0, STALE_GATE | STALE_UP}; return 0; }
+  if (!strcmp(name, "input_layernorm")) { *t = {L.in_ln, 0, 1, h, T_INLN}; return 0; }
+  if (!strcmp(name, "post_attention_layernorm")) { *t = {L.post_ln, 0, 1, h, T_POSTLN}; return 0; }
   return fail(INFERD_ERR_ARG, std::string("unknown layer weight ") + name);
 }
 // packed sub-blocks start at an n-tile boundary: offset rows*K elements == (rows/16)*KT*512
@@ -314,14 +331,10 @@ extern "C" int inferd_span_set_weight(InferdSpan* s, int32_t layer, const char* 
                                     std::to_string(t.rows) + "x" + std::to_string(t.cols));
   hipStream_t st = (hipStream_t)stream;
   if (t.packed)
-    launch_pack((const u16*)src, cols, (int)rows, (int)cols, t.dst, st, t.fold);
+    launch_pack((const u16*)src, cols, (int)rows, (int)cols, t.dst, st);
   else
     HIP_TRY(hipMemcpyAsync(t.dst, src, rows * cols * 2, hipMemcpyDeviceToDevice, st));
   LAUNCH_CHECK();
-  if (layer >= 0) {
-    LayerW& L = s->layers[layer];
-    L.stale = (L.stale | t.marks) & ~t.stale_bit;
-  }
   return INFERD_OK;
 }
 
@@ -334,7 +347,6 @@ extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* st
   if (c.has_lm_head && (int64_t)c.vocab * c.hidden > biggest) biggest = (int64_t)c.vocab * c.hidden;
   u16* tmp = nullptr;
   HIP_TRY(hipMalloc((void**)&tmp, biggest * 2));
-  // norm weights first: they are folded into the projections packed after them
   static const char* layer_names[] = {"input_layernorm", "post_attention_layernorm", "q_norm", "k_norm",
                                       "q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj",
                                       "down_proj"};
@@ -349,11 +361,10 @@ extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* st
     const int64_t n = t.rows * t.cols;
     if (t.packed) {
       launch_weightgen(tmp, n, key, scale, center, st);
-      launch_pack(tmp, t.cols, (int)t.rows, (int)t.cols, t.dst, st, t.fold);
+      launch_pack(tmp, t.cols, (int)t.rows, (int)t.cols, t.dst, st);
     } else {
       launch_weightgen(t.dst, n, key, scale, center, st);
     }
-    if (layer >= 0) s->layers[layer].stale = (s->layers[layer].stale | t.marks) & ~t.stale_bit;
     return INFERD_OK;
   };
   int rc = 0;
@@ -386,8 +397,13 @@ static int check_batch(const InferdSpan* s, const InferdBatch* b) {
   return INFERD_OK;
 }
 
-static AttnBatch to_attn(const InferdBatch* b) {
+// the attention's view of a batch; `kn` (a span's knobs) sets its launch-shape overrides
+static AttnBatch to_attn(const InferdBatch* b, const Knobs& kn = Knobs{}) {
   AttnBatch a;
+  a.nw = kn.attn_nw;
+  a.nc = kn.attn_nc;
+  a.qlanes = kn.attn_qlanes;
+  a.order = kn.attn_order;
   a.seq_start = b->seq_start;
   a.positions = b->positions;
   a.ctx_lens = b->ctx_lens;
@@ -400,37 +416,6 @@ static AttnBatch to_attn(const InferdBatch* b) {
   return a;
 }
 
-// INFERD_FUSE_DECODE_ROPE=0 restores the separate qk_norm_rope_kv launch on decode steps
-// (A/B and parity checks); read at capture/launch time.
-// INFERD_FUSE_PREFILL_ROPE=1 moves the prefill q-norm + RoPE into the attention kernel's
-// q load (the separate kernel then does K/V only).  Off by default: measured equal at
-// Qwen3-32B / 8k (the kernel saved 0.055 ms, the attention prologue grew by 0.047 ms).
-static bool fuse_prefill_rope() {
-  const char* e = getenv("INFERD_FUSE_PREFILL_ROPE");
-  return e && *e == '1';
-}
-
-static bool fuse_decode_rope() {
-  const char* e = getenv("INFERD_FUSE_DECODE_ROPE");
-  return !(e && *e == '0');
-}
-
-// Decode MLP: the SwiGLU activations go from gate/up to down fragment-packed (gemm.hip
-// packed_index); INFERD_PACK_ACT=0 keeps them row-major (A/B and the bit-exactness test).
-static bool pack_act() {
-  const char* e = getenv("INFERD_PACK_ACT");
-  return !(e && *e == '0');
-}
-
-// Decode q/k/v GEMM K-slices (reduced inside the fused attention); INFERD_QKV_SPLIT=1 keeps
-// the single-pass bf16 GEMM.  Needs M <= 16 and K/32 divisible by 4 * slices.
-static int qkv_split(int K) {
-  const char* e = getenv("INFERD_QKV_SPLIT");
-  int k = e && *e ? atoi(e) : 2;
-  if (k < 1 || k > QKV_KSL_MAX || (K / 32) % (4 * k)) k = 1;
-  return k;
-}
-
 extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const int32_t* ids,
                                    const void* x_in, void* x_out, int32_t* next_ids, void* logits,
                                    void* layer_out, void* stream) {
@@ -438,6 +423,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   int rc = check_batch(s, b);
   if (rc) return rc;
   const InferdSpanConfig& c = s->cfg;
+  const Knobs& kn = s->knobs;
   hipStream_t st = (hipStream_t)stream;
   const int M = b->n_tokens, B = b->n_seqs;
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
@@ -454,91 +440,76 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   }
   if (c.n_layers == 0 && x_out && x != x_out)
     HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
-  const AttnBatch ab = to_attn(b);
-  for (int l = 0; l < c.n_layers; ++l)
-    if (s->layers[l].stale)
-      return fail(INFERD_ERR_STATE, "layer " + std::to_string(l) +
-                                        ": a projection was packed before its RMSNorm weight was set "
-                                        "(set input_layernorm / post_attention_layernorm first, then re-set "
-                                        "q/k/v_proj / gate/up_proj)");
-  // RMSNorms (qwen3_server_module.py:19-25, :173-176): see InferdSpan::norm_fold.  gemv: every
+  const AttnBatch ab = to_attn(b, kn);
+  // RMSNorms (qwen3_server_module.py:19-25, :173-176): see InferdSpan::ssq_in.  gemv: every
   // projection of this call is a decode GEMV (<= 64 rows), so the o / down GEMVs can hand the
   // next norm its row sums of squares.
-  const bool fold = s->norm_fold;
   const bool gemv = M <= 64;
-  const RowNorm rn = {c.rms_eps, s->rs_ws};
-  const RowNorm* rfold = fold ? &rn : nullptr;
   const int n_parts = h / 16;
   // decode: the residual stream between layers (and h1 inside a layer) fragment-packed
   // (common.h packed_index) for the GEMVs that read it; the input and the last layer's
   // output stay row-major, and so does every layer's output when layer_out asks for them
-  const bool pkx = gemv && !fold && pack_act() && !layer_out && h % 128 == 0 && I % 128 == 0;
+  const bool pkx = gemv && kn.pack_act && !layer_out && h % 128 == 0 && I % 128 == 0;
   bool x_packed = false;  // x (this layer's input) is fragment-packed
   long pe = -1;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
     u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
-    const bool fused = b->decode && fuse_decode_rope();
-    const int ksl = (fused && M <= 16) ? qkv_split(h) : 1;
+    const bool fused = b->decode && kn.fuse_decode_rope;
+    // decode q/k/v K-slices (reduced inside the fused attention): M <= 16 and K/32 divisible
+    // by 4 * slices
+    int ksl = (fused && M <= 16) ? kn.qkv_split : 1;
+    if ((h / 32) % (4 * ksl)) ksl = 1;
     // ---- input_layernorm -> q/k/v projection
     const u16* a_in = x;
-    DecodeNorm dn = {fold ? (int)DN_FOLD : (int)DN_NONE, c.rms_eps, nullptr, 0, nullptr};
-    if (!fold) {
-      if (gemv && l > 0) {
-        dn = {DN_EXACT, c.rms_eps, s->ssq_in, n_parts, W.in_ln};
-      } else {
-        pe = s->prof_begin(PROF_NORM, st);
-        launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
-        s->prof_end(pe, st);
-        a_in = s->xn;
-      }
+    DecodeNorm dn = {DN_NONE, c.rms_eps, nullptr, 0, nullptr};
+    if (gemv && l > 0) {
+      dn = {DN_EXACT, c.rms_eps, s->ssq_in, n_parts, W.in_ln};
+    } else {
+      pe = s->prof_begin(PROF_NORM, st);
+      launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
+      s->prof_end(pe, st);
+      a_in = s->xn;
     }
     pe = s->prof_begin(PROF_QKV, st);
     // prefill: q/k norm + RoPE and the K/V cache write in the projection's epilogue when
     // the persistent GEMM runs it (else the separate qk_norm_rope_kv launch below)
     bool qkv_done = false;
     if (ksl > 1) {
-      launch_gemm_decode_partial(a_in, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, fold ? s->qkv_ssq : nullptr, dn, st,
+      launch_gemm_decode_partial(a_in, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, dn, st,
                                  (x_packed && a_in == x) ? GEMM_PACK_A : 0);
     } else {
-      if (!b->decode && !fuse_prefill_rope()) {
+      if (!b->decode && kn.fuse_qkv_epi) {
         const QkvEpilogue qe = {b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t, s->sin_t, s->q, kv_l,
                                 H, KV, c.rms_eps};
-        qkv_done = launch_gemm_qkv_fused(a_in, h, W.qkv, M, qkvN, h, rfold, qe, st);
+        qkv_done = launch_gemm_qkv_fused(a_in, h, W.qkv, M, qkvN, h, qe, st);
       }
       if (!qkv_done)
-        launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, rfold, &s->gws, &dn,
+        launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &s->gws, &dn,
                     nullptr, (x_packed && a_in == x) ? GEMM_PACK_A : 0);
     }
     s->prof_end(pe, st);
     // decode: the attention output goes to the o projection's GEMV fragment-packed
-    const bool pk_o = fused && gemv && pack_act() && !gemm_uses_tiled(M, h, H * HEAD_DIM, EPI_RESID);
+    const bool pk_o = fused && gemv && kn.pack_act && !gemm_uses_tiled(M, h, H * HEAD_DIM, EPI_RESID);
     if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
       if (ksl > 1)
         launch_attn_decode_fused(nullptr, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
-                                 scale, s->attn, s->attn_ws, st, s->qkv_part, fold ? s->qkv_ssq : nullptr, ksl, h,
-                                 pk_o);
+                                 scale, s->attn, s->attn_ws, st, s->qkv_part, ksl, pk_o);
       else
         launch_attn_decode_fused(s->qkv, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
-                                 scale, s->attn, s->attn_ws, st, nullptr, nullptr, 0, 0, pk_o);
+                                 scale, s->attn, s->attn_ws, st, nullptr, 0, pk_o);
       s->prof_end(pe, st);
     } else {
-      // prefill: the attention kernel applies the q-norm + RoPE itself; this launch then
-      // only normalises / rotates K and writes K/V to the cache
-      const bool fq = !b->decode && fuse_prefill_rope();
       if (!qkv_done) {
         pe = s->prof_begin(PROF_ROPE, st);
-        launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t,
-                               s->sin_t, s->q, kv_l, M, H, KV, c.rms_eps, st, fq);
+        launch_qk_norm_rope_kv(s->qkv, qkvN, b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t, s->sin_t, s->q,
+                               kv_l, M, H, KV, c.rms_eps, st);
         s->prof_end(pe, st);
       }
       pe = s->prof_begin(PROF_ATTN, st);
       if (b->decode)
         launch_attn_decode(s->q, kv_l, ab, H, KV, scale, s->attn, s->attn_ws, st);
-      else if (fq)
-        launch_attn_prefill(nullptr, kv_l, ab, H, KV, scale, s->attn, st, s->qkv, qkvN, W.q_norm, s->cos_t,
-                            s->sin_t, c.rms_eps);
       else
         launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
       s->prof_end(pe, st);
@@ -552,34 +523,32 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     const bool out_packed = pkx && l < c.n_layers - 1;
     u16* h1 = (pkx && ((x == s->h && !x_packed) || (out == s->h && !out_packed))) ? s->xn : s->h;
     pe = s->prof_begin(PROF_O, st);
-    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, nullptr,
-                &s->gws, nullptr, (gemv && !fold) ? s->ssq_post : nullptr,
+    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
+                gemv ? s->ssq_post : nullptr,
                 (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (pkx ? GEMM_PACK_C : 0));
     s->prof_end(pe, st);
     // ---- post_attention_layernorm -> gate/up (+SwiGLU)
     const u16* m_in = h1;
-    DecodeNorm dm = {fold ? (int)DN_FOLD : (int)DN_NONE, c.rms_eps, nullptr, 0, nullptr};
-    if (!fold) {
-      if (gemv) {
-        dm = {DN_EXACT, c.rms_eps, s->ssq_post, n_parts, W.post_ln};
-      } else {
-        pe = s->prof_begin(PROF_NORM, st);
-        launch_rmsnorm(h1, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
-        s->prof_end(pe, st);
-        m_in = s->xn;
-      }
+    DecodeNorm dm = {DN_NONE, c.rms_eps, nullptr, 0, nullptr};
+    if (gemv) {
+      dm = {DN_EXACT, c.rms_eps, s->ssq_post, n_parts, W.post_ln};
+    } else {
+      pe = s->prof_begin(PROF_NORM, st);
+      launch_rmsnorm(h1, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
+      s->prof_end(pe, st);
+      m_in = s->xn;
     }
     pe = s->prof_begin(PROF_GATEUP, st);
     // decode (the GEMV path): act goes between gate/up and down fragment-packed
     const int pk =
-        (gemv && pack_act() && !gemm_uses_tiled(M, I, h, EPI_SILU) && !gemm_uses_tiled(M, h, I, EPI_RESID)) ? 1 : 0;
-    launch_gemm(m_in, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, rfold, &s->gws, &dm,
-                nullptr, (pk ? GEMM_PACK_C : 0) | ((pkx && m_in == h1) ? GEMM_PACK_A : 0));
+        (gemv && kn.pack_act && !gemm_uses_tiled(M, I, h, EPI_SILU) && !gemm_uses_tiled(M, h, I, EPI_RESID)) ? 1 : 0;
+    launch_gemm(m_in, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, &s->gws, &dm, nullptr,
+                (pk ? GEMM_PACK_C : 0) | ((pkx && m_in == h1) ? GEMM_PACK_A : 0));
     s->prof_end(pe, st);
     // ---- x = h1 + down(act)
     pe = s->prof_begin(PROF_DOWN, st);
-    launch_gemm(s->act, I, W.down, M, h, I, out, h, h1, h, EPI_RESID, nullptr, st, nullptr, &s->gws, nullptr,
-                (gemv && !fold) ? s->ssq_in : nullptr,
+    launch_gemm(s->act, I, W.down, M, h, I, out, h, h1, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
+                gemv ? s->ssq_in : nullptr,
                 (pk ? GEMM_PACK_A : 0) | (pkx ? GEMM_PACK_R : 0) | (out_packed ? GEMM_PACK_C : 0));
     s->prof_end(pe, st);
     x = out;
@@ -595,10 +564,10 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pe = s->prof_begin(PROF_LMHEAD, st);
     // the normed last rows go to the lm_head GEMV fragment-packed (its A operand only; the
     // logits it may also store stay row-major)
-    const bool pk_last = pack_act() && h % 32 == 0;
+    const bool pk_last = kn.pack_act && h % 32 == 0;
     launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st, pk_last);
     launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
-                s->argmax_partial, st, nullptr, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0);
+                s->argmax_partial, st, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0);
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
     s->prof_end(pe, st);
   }
@@ -616,7 +585,7 @@ extern "C" int inferd_span_lm_head(InferdSpan* s, const void* x, int32_t rows, v
   hipStream_t st = (hipStream_t)stream;
   launch_rmsnorm((const u16*)x, c.hidden, nullptr, 0, s->final_norm, s->xn, c.hidden, rows, c.hidden, c.rms_eps, st);
   launch_gemm(s->xn, c.hidden, s->lm_head, rows, c.vocab, c.hidden, (u16*)logits, c.vocab, nullptr, 0, EPI_NONE,
-              nullptr, st, nullptr, &s->gws);
+              nullptr, st, &s->gws);
   LAUNCH_CHECK();
   return INFERD_OK;
 }
@@ -632,8 +601,8 @@ struct InferdGraph {
 };
 
 extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, int32_t advance, const int32_t* ids,
-                                         const void* x_in, void* x_out, int32_t* next_ids, void* stream,
-                                         InferdGraph** out) {
+                                         const void* x_in, void* x_out, int32_t* next_ids, void* logits,
+                                         void* stream, InferdGraph** out) {
   if (!s || !b || !out) return fail(INFERD_ERR_ARG, "null argument");
   if (!stream) return fail(INFERD_ERR_ARG, "graph capture needs a non-null stream");
   if (advance && !b->decode) return fail(INFERD_ERR_ARG, "advance needs a decode batch");
@@ -644,7 +613,7 @@ extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, in
   if (advance)
     launch_decode_advance((int32_t*)b->positions, (int32_t*)b->slots, (int32_t*)b->ctx_lens, b->block_table,
                           b->max_pages, b->n_seqs, s->err, st);
-  rc = inferd_span_forward(s, b, ids, x_in, x_out, next_ids, nullptr, nullptr, stream);
+  rc = inferd_span_forward(s, b, ids, x_in, x_out, next_ids, logits, nullptr, stream);
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(st, &g);
   if (rc) {
@@ -763,10 +732,17 @@ extern "C" int inferd_gemm(const void* a, const void* w, void* c, const void* r,
   if (!a || !w || !c || m <= 0 || n % 16 || k % 32) return fail(INFERD_ERR_ARG, "gemm needs n%16==0, k%32==0");
   if (epi < 0 || epi > 2) return fail(INFERD_ERR_ARG, "bad epilogue");
   if (epi == INFERD_EPI_RESID && !r) return fail(INFERD_ERR_ARG, "resid epilogue needs R");
-  // the op API's own tail-split workspace (per host thread; spans keep theirs)
+  // the op API's own tail-split workspace (per host thread, allocated on its first use;
+  // spans keep theirs); INFERD_GEMM_SPLIT=0 runs this call without the split (tests)
   static thread_local GemmWs op_ws;
+  if (!op_ws.ws) {
+    op_ws.split = 1;
+    if (gemm_ws_alloc(&op_ws) != (int)hipSuccess) return fail(INFERD_ERR_HIP, "tail-split workspace allocation failed");
+  }
+  GemmWs call_ws = op_ws;
+  call_ws.split = env_int("INFERD_GEMM_SPLIT", 1) != 0;
   launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr,
-              (hipStream_t)stream, nullptr, &op_ws);
+              (hipStream_t)stream, &call_ws);
   LAUNCH_CHECK();
   return INFERD_OK;
 }

@@ -26,6 +26,8 @@ executor.
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 from .runtime import KV_PAGE, DecodeGraph, ModelDims, SpanRuntime
@@ -83,11 +85,14 @@ class SpanExecutor:
         self.has_embed, self.has_lm_head = span.has_embed, span.has_lm_head
         self.graphs = []
 
-    def prefill(self, sessions, n_tokens, ids=None, x=None, want_ids=False):
-        """`sessions` each get n_tokens new tokens (ids on the first span, x otherwise)."""
+    def prefill(self, sessions, n_tokens, ids=None, x=None, want_ids=False, want_logits=False):
+        """`sessions` each get n_tokens new tokens (ids on the first span, x otherwise).  Returns
+        the hidden rows, or (last span) the greedy ids -- with want_logits (ids, last-row logits)."""
         out = self.span.forward([(sid, n_tokens) for sid in sessions], ids=ids, x=x,
-                                want_hidden=not want_ids, want_next_ids=want_ids)
-        return out["next_ids"] if want_ids else out["hidden"]
+                                want_hidden=not want_ids, want_next_ids=want_ids, want_logits=want_logits)
+        if want_ids:
+            return (out["next_ids"], out["logits"]) if want_logits else out["next_ids"]
+        return out["hidden"]
 
     def prepare_decode(self, microbatches, n_steps, bufs):
         """Capture one decode graph per microbatch over its fixed buffers
@@ -122,7 +127,10 @@ class PipelineStage:
 
     def __init__(self, dims: ModelDims, rank: int, world: int, first_layer: int, n_layers: int, *,
                  device, seed: int, n_microbatches: int, batch: int, max_ctx: int, prefill_chunk: int = 2,
-                 executor=None, group=None):
+                 executor=None, group=None, profile: str = "random", want_logits: bool = False):
+        """profile: the synthetic weight profile (runtime.SpanRuntime.init_synthetic: "peaked"
+        for token-exact parity runs).  want_logits (last stage): every decode step's and the
+        prefill's last-row logits are kept, for parity checks against the oracle's."""
         assert n_microbatches == world, "the ring schedule keeps exactly one microbatch per stage in flight"
         self.dims, self.rank, self.world = dims, rank, world
         self.S = world
@@ -136,7 +144,7 @@ class PipelineStage:
                                kv_pages=n_microbatches * batch * pages_per_seq + 4,
                                max_tokens=max(prefill_chunk * max_ctx, batch), max_seqs=max(batch, prefill_chunk),
                                max_positions=max_ctx, device=self.device)
-            span.init_synthetic(seed)
+            span.init_synthetic(seed, profile)
             executor = SpanExecutor(span)
         self.ex = executor
         self.span = getattr(executor, "span", None)
@@ -148,7 +156,13 @@ class PipelineStage:
         self.h_in = [torch.zeros(batch, h, dtype=torch.bfloat16, device=dev) for _ in mb]
         self.h_out = [torch.zeros(batch, h, dtype=torch.bfloat16, device=dev) for _ in mb]
         self.ids_out = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
+        self.want_logits = want_logits and rank == world - 1
+        self.logits = [torch.zeros(batch, dims.vocab, dtype=torch.bfloat16, device=dev) for _ in mb] \
+            if self.want_logits else None
         self.step_base = 0   # decode steps already run (absolute step of the next decode call)
+        # host time per tick of the last decode() call, split into the hand-off (exchange wait
+        # included) and the rest (graph launch, page-table advance, schedule bookkeeping)
+        self.tick_stats = None
 
     @property
     def first(self):
@@ -160,12 +174,13 @@ class PipelineStage:
 
     def _bufs(self, m):
         """Fixed buffers of microbatch m for this stage's role."""
+        lg = {"logits": self.logits[m]} if self.want_logits else {}
         if self.S == 1:
-            return {"ids": self.ids[m], "x": None, "hidden_out": None, "next_ids": self.ids[m]}
+            return {"ids": self.ids[m], "x": None, "hidden_out": None, "next_ids": self.ids[m], **lg}
         if self.first:
             return {"ids": self.ids[m], "x": None, "hidden_out": self.h_out[m], "next_ids": None}
         if self.last:
-            return {"ids": None, "x": self.h_in[m], "hidden_out": None, "next_ids": self.ids_out[m]}
+            return {"ids": None, "x": self.h_in[m], "hidden_out": None, "next_ids": self.ids_out[m], **lg}
         return {"ids": None, "x": self.h_in[m], "hidden_out": self.h_out[m], "next_ids": None}
 
     def _exchange(self, send=None, send_to=None, recv=None, recv_from=None):
@@ -196,9 +211,11 @@ class PipelineStage:
         """prompts: per microbatch an int tensor [B, T] (read on the first stage only).
         Runs every microbatch's prompt through the pipeline in chunks of prefill_chunk
         sequences; leaves the first decode ids of every microbatch on stage 0.  `capture`
-        (a dict, non-last stages): receives this stage's output for the first chunk of
+        (a dict): on non-last stages it receives this stage's output for the first chunk of
         microbatch 0 -- its sequences 0 .. prefill_chunk-1, [chunk * T, h] -- as a CPU copy
-        (the stage-boundary hidden state parity tests compare with the oracle)."""
+        (the stage-boundary hidden state parity tests compare with the oracle); on the last
+        stage of a want_logits pipeline, capture["logits"][m] = microbatch m's last-row logits
+        [B, vocab] (CPU)."""
         S, T = self.S, prompts[0].shape[1]
         items = [(m, c) for m in range(self.n_mb) for c in range(0, self.B, self.prefill_chunk)]
         h = self.dims.hidden
@@ -221,12 +238,17 @@ class PipelineStage:
             if 0 <= i_cur < len(items):
                 m, c = items[i_cur]
                 sess = self.sessions[m][c:c + self.prefill_chunk]
+                wl = self.want_logits and capture is not None
+                kw = {"want_logits": True} if wl else {}
                 if self.first:
                     ids = prompts[m][c:c + len(sess)].reshape(-1).to(self.device, torch.int32)
-                    out = self.ex.prefill(sess, T, ids=ids, want_ids=self.last)
+                    out = self.ex.prefill(sess, T, ids=ids, want_ids=self.last, **kw)
                 else:
-                    out = self.ex.prefill(sess, T, x=bufs_in.pop(i_cur), want_ids=self.last)
+                    out = self.ex.prefill(sess, T, x=bufs_in.pop(i_cur), want_ids=self.last, **kw)
                 if self.last:
+                    if wl:
+                        out, lg = out
+                        capture.setdefault("logits_parts", {})[(m, c)] = lg.cpu()
                     ids_parts[(m, c)] = out
                 else:
                     bufs_out[i_cur] = out
@@ -235,6 +257,10 @@ class PipelineStage:
         if self.last:
             for m in range(self.n_mb):
                 first_ids[m] = torch.cat([ids_parts[(m, c)] for c in range(0, self.B, self.prefill_chunk)])
+            if capture is not None and "logits_parts" in capture:
+                parts = capture.pop("logits_parts")
+                capture["logits"] = [torch.cat([parts[(m, c)] for c in range(0, self.B, self.prefill_chunk)])
+                                     for m in range(self.n_mb)]
         # hand the first decode ids to stage 0
         if S == 1:
             for m in range(self.n_mb):
@@ -255,18 +281,26 @@ class PipelineStage:
         self.ex.prepare_decode(self.sessions, n_steps, [self._bufs(m) for m in range(self.n_mb)])
 
     @torch.no_grad()
-    def decode(self, n_steps: int, record=None):
+    def decode(self, n_steps: int, record=None, record_logits=None):
         """Run n_steps decode steps of every microbatch.  `record` (stage 0 only): list that
-        receives (absolute step, microbatch, ids tensor copy) of every input fed to the first span."""
+        receives (absolute step, microbatch, ids tensor copy) of every input fed to the first
+        span; `record_logits` (last stage of a want_logits pipeline): list that receives
+        (absolute step, microbatch, device copy of the step's last-row logits [B, vocab]).
+        Sets self.tick_stats: host microseconds per tick, hand-off (exchange) and the rest."""
         S = self.S
         n_items = n_steps * self.n_mb
+        t_x = 0.0
+        t0 = time.perf_counter()
         if S == 1:
             for i in range(n_items):
                 k, m = divmod(i, self.n_mb)
                 if record is not None:
                     record.append((self.step_base + k, m, self.ids[m].clone()))
                 self.ex.decode(m)
+                if record_logits is not None and self.want_logits:
+                    record_logits.append((self.step_base + k, m, self.logits[m].clone()))
             self.step_base += n_steps
+            self._tick_stats(n_items, time.perf_counter() - t0, 0.0)
             return
         for t in range(n_items + S):
             i_cur = t - self.rank
@@ -281,13 +315,22 @@ class PipelineStage:
                     recv = self.ids[j % self.n_mb]
             elif 0 <= i_cur < n_items:
                 recv = self.h_in[i_cur % self.n_mb]
+            tx = time.perf_counter()
             self._exchange(send, (self.rank + 1) % S, recv, (self.rank - 1) % S)
+            t_x += time.perf_counter() - tx
             if 0 <= i_cur < n_items:
                 k, m = divmod(i_cur, self.n_mb)
                 if self.first and record is not None:
                     record.append((self.step_base + k, m, self.ids[m].clone()))
                 self.ex.decode(m)
+                if record_logits is not None and self.want_logits:
+                    record_logits.append((self.step_base + k, m, self.logits[m].clone()))
         self.step_base += n_steps
+        self._tick_stats(n_items + S, time.perf_counter() - t0, t_x)
+
+    def _tick_stats(self, ticks, total_s, exchange_s):
+        self.tick_stats = {"ticks": ticks, "host_us_per_tick": round((total_s - exchange_s) / ticks * 1e6, 1),
+                           "exchange_us_per_tick": round(exchange_s / ticks * 1e6, 1)}
 
     def profile_decode(self, n_steps: int):
         """Per-kernel timings from eager (event-instrumented) decode steps on this stage,

@@ -169,10 +169,11 @@ class DecodeGraph:
     each session, reading `ids` (first span) or `x`, writing `hidden_out` and/or
     `next_ids` -- fixed device buffers chosen at capture.  `ids` and `next_ids` may alias
     (greedy feedback on a single-span model).  Pages for `n_steps` tokens are reserved
-    up front; launching more than n_steps times raises."""
+    up front; launching more than n_steps times raises.  `logits` (last span, optional): bf16
+    [sessions, vocab] receives every replay's last-row logits."""
 
     def __init__(self, span: "SpanRuntime", sessions, n_steps: int, ids=None, x=None, hidden_out=None,
-                 next_ids=None):
+                 next_ids=None, logits=None):
         self.span, self.n_steps, self.launched = span, n_steps, 0
         self.states = [span.reserve(sid, n_steps) for sid in sessions]
         B = len(self.states)
@@ -190,14 +191,15 @@ class DecodeGraph:
                                 max_pages=max_pages, decode=1, seq_start=base + 4 * o[0],
                                 positions=base + 4 * o[1], slots=base + 4 * o[2], ctx_lens=base + 4 * o[3],
                                 block_table=base + 4 * o[4])
-        self._keep = (ids, x, hidden_out, next_ids)
+        self._keep = (ids, x, hidden_out, next_ids, logits)
+        self._seqs = (C.c_uint64 * B)(*[st.seq for st in self.states])
         cur = torch.cuda.current_stream(span.device)
         cs = torch.cuda.Stream(span.device)
         cs.wait_stream(cur)
         g = _lib.c_p()
         with torch.cuda.device(span.device):
             _lib.check(span.lib.inferd_span_graph_capture(span.handle, self.batch, 1, _lib.ptr(ids), _lib.ptr(x),
-                                                          _lib.ptr(hidden_out), _lib.ptr(next_ids),
+                                                          _lib.ptr(hidden_out), _lib.ptr(next_ids), _lib.ptr(logits),
                                                           cs.cuda_stream, g))
         cur.wait_stream(cs)
         self.graph = g
@@ -208,8 +210,8 @@ class DecodeGraph:
         s = stream if stream is not None else torch.cuda.current_stream(self.span.device)
         _lib.check(self.span.lib.inferd_graph_launch(self.graph, s.cuda_stream))
         self.launched += 1
-        for st in self.states:
-            self.span.kv.advance(st.seq, 1)
+        # the host page table follows the device-side advance: one native call per replay
+        _lib.check(self.span.lib.inferd_kv_advance_many(self.span.kv.handle, self._seqs, len(self.states), 1))
 
     def __del__(self):
         g = getattr(self, "graph", None)
@@ -294,9 +296,8 @@ class SpanRuntime:
 
     def load_layer_state_dict(self, layer: int, sd: dict):
         """Keys as in Qwen3DecoderLayer (qwen3_server_module.py:165-176): self_attn.q_proj.weight ...
-        Norm weights are set first: the span folds them into the projections packed after."""
+        (any order: the span's RMSNorms read their weights as set)."""
         items = [(k.split(".")[-2] if k.endswith(".weight") else k, v) for k, v in sd.items()]
-        items.sort(key=lambda kv: 0 if kv[0].endswith("norm") else 1)
         for leaf, v in items:
             self.set_weight(layer, leaf, v)
 

@@ -115,9 +115,36 @@ def tensor_spec(name: str) -> tuple[float, float]:
     return LINEAR_SCALE, 0.0
 
 
-def gen_tensor_bf16_bits(seed: int, tid: int, shape, name: str) -> np.ndarray:
+_CLIB = None
+
+
+def c_generator():
+    """oracle/libweightgen.so (oracle/weightgen.c, built by oracle/Makefile: the same values,
+    OpenMP over the host cores), or None when it is not built."""
+    global _CLIB
+    if _CLIB is None:
+        import ctypes
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libweightgen.so")
+        _CLIB = False
+        if os.path.exists(path):
+            lib = ctypes.CDLL(path)
+            lib.wg_bf16.restype = None
+            lib.wg_bf16.argtypes = [ctypes.c_uint64, ctypes.c_float, ctypes.c_float, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_void_p]
+            _CLIB = lib
+    return _CLIB or None
+
+
+def gen_tensor_bf16_bits(seed: int, tid: int, shape, name: str, use_c: bool = True) -> np.ndarray:
     scale, center = tensor_spec(name)
     n = int(np.prod(shape))
+    lib = c_generator() if use_c else None
+    if lib is not None:
+        out = np.empty(n, dtype=np.uint16)
+        lib.wg_bf16(tensor_key(seed, tid), float(np.float32(scale)), float(np.float32(center)), 0, n,
+                    out.ctypes.data)
+        return out.reshape(shape)
     return bf16_rne_bits(uniform_fp32(seed, tid, n, scale, center)).reshape(shape)
 
 

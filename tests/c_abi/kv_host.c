@@ -63,6 +63,15 @@ int main(void) {
   CHECK(host[5] == 1 * 64 + 36 && host[6] == 2 * 64, "slots: session 17 page 1 offset 36, session 42 page 2");
   CHECK(host[7] == 101 && host[8] == 1, "ctx_lens");
   free(host);
+  /* a decode-graph replay advances its whole batch with one call, all or nothing */
+  CHECK(inferd_kv_advance_many(kv, seqs, 2, 1) == INFERD_OK, "advance_many: both sessions by one token");
+  inferd_kv_query(kv, s17, &len, &np);
+  CHECK(len == 101, "session 17 at 101 cached tokens");
+  inferd_kv_query(kv, s42, &len, &np);
+  CHECK(len == 1, "session 42 at 1 cached token");
+  CHECK(inferd_kv_advance_many(kv, seqs, 2, 64) == INFERD_ERR_ARG, "advance_many past the pages is refused");
+  inferd_kv_query(kv, s17, &len, &np);
+  CHECK(len == 101, "nothing advanced on failure");
 
   /* errors: a session twice in one batch, unreserved tokens, an exhausted pool */
   seqs[1] = s17;

@@ -99,10 +99,10 @@ class TupleShim(nn.Module):
         return out if isinstance(out, tuple) else (out,)
 
 
-def build_petals_stages(d, spans, dtype):
+def build_petals_stages(d, spans, dtype, profile="random"):
     """spans: list of (start, end).  Returns the reference stage modules."""
     cfg = hf_config(d)
-    g = R.gen_global_weights(d, SEED, dtype)
+    g = R.gen_global_weights(d, SEED, dtype, profile)
     embed = nn.Embedding(d.vocab, d.hidden).to(dtype)
     embed.weight.data.copy_(g["embed_tokens"])
     norm = HFQ.Qwen3RMSNorm(d.hidden, eps=d.eps).to(dtype)
@@ -209,6 +209,40 @@ def gen_tiny_petals():
     np.savez_compressed(os.path.join(OUT, "tiny_petals.npz"), **res)
 
 
+def gen_tiny_petals_peaked(steps=16):
+    """The tiny model with the peaked embed / lm_head profile (oracle/weightgen.py): large top-1
+    margins, so a GPU chain must reproduce EVERY id of the reference's own chain.  (1) the real
+    PartitionedQwen2.forward chain (fp32 codec), (2) the bf16 stage modules, both free-running
+    greedy with full recompute (send_message.py:46-60) for `steps` steps; the bf16 top-2 margins
+    are recorded."""
+    d = R.CONFIGS["tiny"]
+    rng = np.random.default_rng(17)
+    prompt = rng.integers(0, d.vocab, size=16).tolist()
+    res = {"prompt": np.array(prompt, dtype=np.int64)}
+    s0, s1 = build_petals_stages(d, [(0, 1), (2, 3)], torch.float32, "peaked")
+    n0, n1 = partitioned(0, 2, s0), partitioned(1, 2, s1)
+    ids = list(prompt)
+    for step in range(steps):
+        ids = n1.forward(n0.forward({"generated_ids": ids}))["generated_ids"]
+    res["fp32_greedy_ids"] = np.array(ids[len(prompt):], dtype=np.int64)
+    s0, s1 = build_petals_stages(d, [(0, 1), (2, 3)], torch.bfloat16, "peaked")
+    ids, margins = list(prompt), []
+    for step in range(steps):
+        with torch.no_grad():
+            T = len(ids)
+            m = PM.build_decoder_attention_mask(torch.ones((1, T), dtype=torch.long))
+            p = torch.arange(T).unsqueeze(0)
+            lg = s1(s0(torch.tensor([ids]), m, p), m, p)[0, -1]
+        top = torch.topk(lg.float(), 2).values
+        margins.append(float(top[0] - top[1]))
+        ids.append(int(torch.argmax(lg).item()))
+    res["bf16_greedy_ids"] = np.array(ids[len(prompt):], dtype=np.int64)
+    res["bf16_margins"] = np.array(margins, dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, "tiny_petals_peaked.npz"), **res)
+    print("tiny_petals_peaked: fp32", res["fp32_greedy_ids"].tolist(), "bf16", res["bf16_greedy_ids"].tolist(),
+          "min margin", min(margins))
+
+
 class _Server(QS.Qwen3Server):
     def _load_weights(self):  # no hub download: weights injected below
         pass
@@ -313,9 +347,14 @@ def gen_codec():
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
+    if len(sys.argv) > 1:   # named generators only, e.g. `make_golden.py tiny_petals_peaked`
+        for name in sys.argv[1:]:
+            globals()[f"gen_{name}"]()
+        sys.exit(0)
     gen_codec()
     gen_units()
     gen_tiny_petals()
+    gen_tiny_petals_peaked()
     gen_server("tiny_server", "tiny", 0, 3, 1, 8, 4, ((torch.float32, "fp32"), (torch.bfloat16, "bf16")), 21)
     gen_server("q06_layer", "qwen3-0.6b", 5, 5, 1, 8, 4, ((torch.float32, "fp32"), (torch.bfloat16, "bf16")), 22)
     gen_server("q8b_layer", "qwen3-8b", 7, 7, 2, 4, 2, ((torch.bfloat16, "bf16"),), 23)

@@ -4,8 +4,9 @@ Tolerance (stated once, used everywhere below): a bf16 hidden state H_gpu matche
 reference H_ref when  max|H_gpu - H_ref| <= TOL_REL * max|H_ref|  (per tensor), with
 TOL_REL = 2e-2 against the oracle run with the same attention semantics (sdpa) and
 3e-2 against the gRPC golden (eager attention rounds scores to bf16, the kernel keeps
-them in fp32).  Greedy tokens must be identical wherever the reference's top-1 margin
-exceeds MARGIN_FLOOR (in logit units); steps below it are reported, not silently passed.
+them in fp32).  Greedy tokens are checked on the "peaked" synthetic profile (large top-1
+margins, oracle/weightgen.py) on EVERY step, and every step's reference margin must exceed
+twice the measured logit error, so agreement is never luck and never skipped.
 """
 import pytest
 import torch
@@ -19,7 +20,6 @@ SEED = 1234
 DEV = "cuda"
 TOL_REL = 2e-2
 TOL_REL_EAGER = 3e-2
-MARGIN_FLOOR = 0.05
 
 
 def rel_err(a, b):
@@ -27,13 +27,17 @@ def rel_err(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
 
 
-def span(cfg, first, n, embed, lm, **kw):
+def span(cfg, first, n, embed, lm, profile="random", **kw):
     from inferd_amd.runtime import MODELS, SpanRuntime
     d = MODELS[cfg]
     s = SpanRuntime(d, first, n, has_embed=embed, has_lm_head=lm, device=DEV,
                     max_positions=kw.pop("max_positions", 8192), **kw)
-    s.init_synthetic(SEED)
+    s.init_synthetic(SEED, profile)
     return s
+
+
+def max_abs(a, b):
+    return (a.float().cpu() - b.float().cpu()).abs().max().item()
 
 
 def test_tiny_two_spans_vs_golden():
@@ -52,21 +56,32 @@ def test_tiny_two_spans_vs_golden():
     e = rel_err(o1["logits"][0], lg)
     print(f"tiny last-row logits rel err {e:.2e}")
     assert e < TOL_REL
-    # greedy full-recompute loop (send_message.py:46-60 semantics): 8 steps
-    ids = prompt.tolist()
+
+
+def test_tiny_two_spans_free_running_vs_reference_chain():
+    """The reference's OWN chain (tiny_petals_peaked.npz: the real PartitionedQwen2.forward
+    chain and its bf16 stage modules, peaked profile, 16 free-running greedy steps of full
+    recompute, send_message.py:46-60) against two HIP spans free-running the same protocol:
+    all 16 ids identical, and at every step the reference chain's margin exceeds twice the
+    engine's measured logit error (against the oracle on the same prefix)."""
+    g = load("tiny_petals_peaked.npz")
     ref_ids = g["bf16_greedy_ids"].tolist()
-    b0 = R.RefSpan(R.CONFIGS["tiny"], SEED, 0, 1, True, False)
-    b1 = R.RefSpan(R.CONFIGS["tiny"], SEED, 2, 3, False, True)
-    for step in range(8):
+    assert ref_ids == g["fp32_greedy_ids"].tolist()      # the reference chain agrees with itself
+    s0 = span("tiny", 0, 2, True, False, "peaked")
+    s1 = span("tiny", 2, 2, False, True, "peaked")
+    b0 = R.RefSpan(R.CONFIGS["tiny"], SEED, 0, 1, True, False, profile="peaked")
+    b1 = R.RefSpan(R.CONFIGS["tiny"], SEED, 2, 3, False, True, profile="peaked")
+    ids = g["prompt"].tolist()
+    for step, (rid, margin) in enumerate(zip(ref_ids, g["bf16_margins"].tolist())):
         x = torch.tensor(ids)
         h = s0.forward([(None, len(ids))], ids=x)["hidden"]
-        nid = int(s1.forward([(None, len(ids))], x=h, want_next_ids=True, want_hidden=False)["next_ids"][0])
-        ref_logits = b1.forward(b0.forward(x[None]))[0, -1]
-        margin = R.top2_margin(ref_logits)
-        print(f"step {step}: gpu {nid} ref {ref_ids[step]} margin {margin:.4f}")
-        if margin > MARGIN_FLOOR:
-            assert nid == ref_ids[step], step
-        ids.append(ref_ids[step])  # teacher-forced: every step compares the same prefix
+        o = s1.forward([(None, len(ids))], x=h, want_next_ids=True, want_logits=True, want_hidden=False)
+        nid = int(o["next_ids"][0])
+        err = max_abs(o["logits"][0], b1.forward(b0.forward(x[None]))[0, -1])
+        print(f"step {step}: gpu {nid} ref {rid} margin {margin:.3f} logit err {err:.3e}")
+        assert nid == rid, step
+        assert margin > 2 * err, (step, margin, err)
+        ids.append(nid)  # free-running: the GPU chain feeds back its own ids
 
 
 def test_q06_layer_cached_vs_golden():
@@ -100,17 +115,18 @@ def test_q8b_layer_batched_cached_vs_golden():
 def test_partitioned_qwen2_dict_protocol(tmp_path):
     """The node-facing API end to end: stage files written by the offline splitter, two
     PartitionedQwen2 stages chained through the reference's dict protocol (generated_ids ->
-    hidden_meta (bf16 wire codec) -> next_token_id), 8 greedy steps of full recompute as in
-    send_message.py:46-60, against the golden ids of the reference's own chain."""
+    hidden_meta (bf16 wire codec) -> next_token_id), 16 free-running greedy steps of full
+    recompute as in send_message.py:46-60, against EVERY id of the reference's own chain
+    (tiny_petals_peaked.npz, peaked profile)."""
     from inferd_amd.partitioned_models import PartitionedQwen2
     from inferd_amd.runtime import MODELS
     from inferd_amd.split_model import split
-    g = load("tiny_petals.npz")
+    g = load("tiny_petals_peaked.npz")
     d = R.CONFIGS["tiny"]
     cfg = {"model_name": "tiny", "parts_dir": str(tmp_path), "stages_count": 2,
            "stages": [{"name": "node0", "stage": 0, "start_layer": 0, "end_layer": 1},
                       {"name": "node1", "stage": 1, "start_layer": 2, "end_layer": 3}]}
-    glob = R.gen_global_weights(d, SEED)
+    glob = R.gen_global_weights(d, SEED, profile="peaked")
     attn = ("q_proj", "k_proj", "v_proj", "o_proj", "q_norm", "k_norm")
 
     def get_layer(i):
@@ -120,20 +136,16 @@ def test_partitioned_qwen2_dict_protocol(tmp_path):
     n0 = PartitionedQwen2("tiny", 2, 0, p0)
     n1 = PartitionedQwen2("tiny", 2, 1, p1)
     ids = g["prompt"].tolist()
-    ref_ids = g["bf16_greedy_ids"].tolist()
-    b0 = R.RefSpan(d, SEED, 0, 1, True, False)
-    b1 = R.RefSpan(d, SEED, 2, 3, False, True)
-    for step in range(8):
+    ref_ids = g["fp32_greedy_ids"].tolist()   # the real PartitionedQwen2.forward chain's
+    for step in range(len(ref_ids)):
         o0 = n0.forward({"generated_ids": ids})
         assert o0["hidden_meta"]["dtype"] == "bfloat16" and o0["generated_ids"] == ids
         o1 = n1.forward(o0)
-        margin = R.top2_margin(b1.forward(b0.forward(torch.tensor([ids])))[0, -1])
-        if margin > MARGIN_FLOOR:
-            assert o1["next_token_id"] == ref_ids[step], step
+        assert o1["next_token_id"] == ref_ids[step], step
         assert o1["generated_ids"] == ids + [o1["next_token_id"]]
-        ids = ids + [ref_ids[step]]
+        ids = o1["generated_ids"]                 # free-running
     # synthetic stage spec gives the same model without files
-    s0 = PartitionedQwen2("tiny", 2, 0, f"synthetic:{SEED}:tiny:0:1")
+    s0 = PartitionedQwen2("tiny", 2, 0, f"synthetic:{SEED}:tiny:0:1:peaked")
     h_file = n0.forward({"generated_ids": ids})["hidden_meta"]
     h_syn = s0.forward({"generated_ids": ids})["hidden_meta"]
     assert h_file == h_syn
@@ -166,10 +178,12 @@ def test_decode_graph_matches_eager():
 
 
 def test_q06_full_model_greedy_cached():
-    """Config 2: Qwen3-0.6B single full span, prefill 32 + cached greedy decode."""
+    """Config 2: Qwen3-0.6B single full span (peaked profile), prefill 32 + 12 cached greedy
+    decode steps teacher-forced on the oracle's ids: every id identical, every oracle margin
+    above twice the measured logit error."""
     d = R.CONFIGS["qwen3-0.6b"]
-    s = span("qwen3-0.6b", 0, d.layers, True, True)
-    oracle = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa")
+    s = span("qwen3-0.6b", 0, d.layers, True, True, "peaked")
+    oracle = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa", profile="peaked")
     prompt = torch.randint(0, d.vocab, (32,), generator=torch.Generator().manual_seed(5))
     ids = prompt.tolist()
     gpu_tokens, ref_tokens, margins = [], [], []
@@ -180,48 +194,32 @@ def test_q06_full_model_greedy_cached():
         rid = int(torch.argmax(lg_ref))
         m = R.top2_margin(lg_ref)
         e = rel_err(out["logits"][0], lg_ref)
+        ea = max_abs(out["logits"][0], lg_ref)
         gpu_tokens.append(gid)
         ref_tokens.append(rid)
         margins.append(m)
         print(f"step {step}: gpu {gid} ref {rid} margin {m:.4f} logits rel err {e:.2e}")
         assert e < 5e-2
-        if m > MARGIN_FLOOR:
-            assert gid == rid, step
+        assert gid == rid, step
+        assert m > 2 * ea, (step, m, ea)
         nxt = torch.tensor([rid])
         lg_ref = oracle.forward_cached("s", nxt[None])[0, -1]
         out = s.forward([("s", 1)], ids=nxt, want_next_ids=True, want_logits=True, want_hidden=False)
-    agree = sum(a == b for a, b in zip(gpu_tokens, ref_tokens))
-    print(f"greedy agreement {agree}/{len(gpu_tokens)}")
+    print(f"greedy agreement {len(gpu_tokens)}/{len(gpu_tokens)}, smallest margin {min(margins):.2f}")
 
 
-def test_norm_fold_order_enforced(monkeypatch):
-    """Folded-norm A/B spans (INFERD_NORM_FOLD=1) fold the RMSNorm weights into q/k/v and
-    gate/up at pack time: re-setting a norm weight after its projections leaves them stale and
-    forward must refuse (no silent use of the old fold); re-setting the projections restores
-    the exact synthetic span.  Exact-norm spans (the default) take weights in any order."""
-    from inferd_amd import _lib
-    monkeypatch.setenv("INFERD_NORM_FOLD", "1")
+def test_weights_any_order():
+    """The span's RMSNorms read their weights as set (reference rounding points, nothing folded
+    at pack time): re-setting input_layernorm after the projections changes the output, and
+    re-setting every weight restores the synthetic span bit for bit."""
     s = span("tiny", 0, 1, True, False)
     ids = torch.arange(8, dtype=torch.int32)
-    ref = s.forward([(None, 8)], ids=ids)["hidden"]
+    ref = s.forward([(None, 8)], ids=ids)["hidden"].cpu()
     d = s.dims
-    w_in = torch.ones(d.hidden, dtype=torch.bfloat16) * 1.05
-    s.set_weight(0, "input_layernorm", w_in)
-    with pytest.raises(RuntimeError, match="RMSNorm weight"):
-        s.forward([(None, 8)], ids=ids)
-    # restore: synthetic init packs norms first, then the projections
+    s.set_weight(0, "input_layernorm", torch.ones(d.hidden, dtype=torch.bfloat16) * 1.05)
+    assert not torch.equal(s.forward([(None, 8)], ids=ids)["hidden"].cpu(), ref)
     s.init_synthetic(SEED)
-    again = s.forward([(None, 8)], ids=ids)["hidden"]
-    assert torch.equal(again.cpu(), ref.cpu())
-    assert _lib.load() is not None
-    monkeypatch.setenv("INFERD_NORM_FOLD", "0")
-    e = span("tiny", 0, 1, True, False)
-    ref = e.forward([(None, 8)], ids=ids)["hidden"]
-    e.set_weight(0, "input_layernorm", w_in)
-    changed = e.forward([(None, 8)], ids=ids)["hidden"]
-    assert not torch.equal(changed.cpu(), ref.cpu())
-    e.init_synthetic(SEED)
-    assert torch.equal(e.forward([(None, 8)], ids=ids)["hidden"].cpu(), ref.cpu())
+    assert torch.equal(s.forward([(None, 8)], ids=ids)["hidden"].cpu(), ref)
 
 
 def test_decode_fused_rope_matches_separate(monkeypatch):
@@ -297,31 +295,6 @@ def test_config5_q32b_layer_prefill_vs_oracle():
         e = rel_err(out, oracle.forward_cached("p", xd)[0])
         print(f"32B layer decode {step}: rel err {e:.2e}")
         assert e < TOL_REL
-
-
-def test_prefill_fused_q_rope_matches_separate(monkeypatch):
-    """INFERD_FUSE_PREFILL_ROPE=1 (q-norm + RoPE inside the prefill attention, K/V-only norm
-    kernel) against the default separate kernel: one Qwen3-8B-dims layer, two ragged
-    prompts with a cached prefix, then a decode step."""
-    from inferd_amd.runtime import MODELS, SpanRuntime
-    d = MODELS["qwen3-8b"]
-    outs = []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("INFERD_FUSE_PREFILL_ROPE", fused)
-        s = SpanRuntime(d, 3, 1, has_embed=False, has_lm_head=False, device=DEV, max_positions=1024,
-                        kv_pages=32, max_tokens=512, max_seqs=4)
-        s.init_synthetic(SEED)
-        g = torch.Generator().manual_seed(4)
-        x0 = (torch.randn(200 + 77, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
-        x1 = (torch.randn(150, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
-        x2 = (torch.randn(2, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
-        h0 = s.forward([("a", 200), ("b", 77)], x=x0, want_hidden=True)["hidden"].cpu()
-        h1 = s.forward([("a", 150)], x=x1, want_hidden=True)["hidden"].cpu()
-        h2 = s.forward([("a", 1), ("b", 1)], x=x2, want_hidden=True)["hidden"].cpu()
-        outs.append(torch.cat([h0, h1, h2]))
-    e = rel_err(outs[0], outs[1])
-    print(f"fused vs separate prefill q-norm/rope: rel err {e:.2e}")
-    assert e < 2e-2
 
 
 def test_prefill_qkv_epilogue_matches_separate(monkeypatch):

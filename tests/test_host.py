@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 def test_library_loads_and_reports_version():
     from inferd_amd import _lib
     lib = _lib.load()
-    assert lib.inferd_abi_version() == 1
+    assert lib.inferd_abi_version() == _lib.ABI_VERSION == 2
     # error path without a GPU: a null config is rejected with a message
     h = _lib.c_p()
     rc = lib.inferd_span_create(None, h)
@@ -103,6 +103,14 @@ def test_kv_table_and_batch_descriptor():
         kv.build_batch([(2, 65)], "cpu")                    # pages not reserved
     with pytest.raises(RuntimeError):
         kv.advance(2, 65)                                   # past the reserved pages
+    # a decode-graph replay's host advance: one native call for the whole batch, all or nothing
+    keys = (ctypes.c_uint64 * 2)(1, 2)
+    assert kv.lib.inferd_kv_advance_many(kv.handle, keys, 2, 3) == 0
+    assert kv.query(1)[0] == 73 and kv.query(2)[0] == 3
+    assert kv.lib.inferd_kv_advance_many(kv.handle, keys, 2, 62) != 0  # sequence a: past its 2 pages
+    assert kv.query(1)[0] == 73 and kv.query(2)[0] == 3                 # nothing advanced
+    dup = (ctypes.c_uint64 * 2)(2, 2)
+    assert kv.lib.inferd_kv_advance_many(kv.handle, dup, 2, 1) != 0     # a sequence twice
     kv.release(1)
     assert kv.n_free == 9
     kv.reserve(4, 64)                                       # a's first page comes back first
@@ -151,6 +159,23 @@ def test_weightgen_numpy_known_values():
     assert v.dtype == np.float32 and np.all(np.abs(v) <= 1.0)
 
 
+def test_weightgen_c_matches_numpy():
+    """The oracle's C generator (oracle/weightgen.c, what the 8B / 32B oracle runs use) gives
+    the numpy definition's bf16 bits exactly: linear and norm tensors, a global tensor id, an
+    odd length."""
+    import subprocess
+    from oracle import weightgen as wg
+    if wg.c_generator() is None:
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+        wg._CLIB = None
+    assert wg.c_generator() is not None
+    for seed, tid, shape, name in [(1234, 3 * 16 + 8, (512, 4096), "gate_proj"), (1234, 7, (4096,), "input_layernorm"),
+                                   (99, 0xFFFF0002, (1000, 256), "lm_head"), (5, 17, (12345,), "q_proj")]:
+        a = wg.gen_tensor_bf16_bits(seed, tid, shape, name, use_c=False)
+        b = wg.gen_tensor_bf16_bits(seed, tid, shape, name)
+        assert np.array_equal(a, b), (tid, name)
+
+
 def _brute_split(n_layers, n, lc, hc):
     """All compositions of n_layers into n positive parts; (max, sum sq) optimum."""
     import itertools
@@ -178,13 +203,16 @@ def test_balanced_split_is_min_max(n_layers, n, hc):
 
 
 def test_bench_stage_split_qwen3_8b():
-    """bench.py's default stage split at the headline config prices the lm_head on the last
-    stage: its slowest stage is 5 layers at N = 8 where the even split's is 4 layers + lm_head."""
+    """bench.py's default stage split is BASELINE config 3's even split ([18,18] / [9,9,9,9] /
+    [5,5,5,5,4,4,4,4]); `balanced` prices the lm_head on the last stage: its slowest stage is 5
+    layers at N = 8 where the even split's is 4 layers + lm_head."""
     import bench
     from inferd_amd.runtime import MODELS
     d = MODELS["qwen3-8b"]
-    assert [k for _, k in bench.stage_split(d, 8, 16, 2048)] == [4, 5, 5, 5, 5, 5, 5, 2]
-    assert [k for _, k in bench.stage_split(d, 8, 16, 2048, "even")] == [5, 5, 5, 5, 4, 4, 4, 4]
+    assert [k for _, k in bench.stage_split(d, 8, 16, 2048)] == [5, 5, 5, 5, 4, 4, 4, 4]
+    assert [k for _, k in bench.stage_split(d, 2, 16, 2048)] == [18, 18]
+    assert [k for _, k in bench.stage_split(d, 4, 16, 2048)] == [9, 9, 9, 9]
+    assert [k for _, k in bench.stage_split(d, 8, 16, 2048, "balanced")] == [4, 5, 5, 5, 5, 5, 5, 2]
     assert [k for _, k in bench.stage_split(d, 1, 16, 2048)] == [36]
 
 
