@@ -17,6 +17,13 @@ backend; host-staged on gloo); the group's last rank returns the hidden rows or,
 chain's last stage, the greedy ids to rank 0, which answers with the reference's output
 schema.  Sessions (PartitionedQwen2's optional session_id) live on every rank with identical
 page accounting: rank 0 reserves and evicts first, then tells the others.
+
+Faults keep the group in lockstep.  Rank 0 validates a request (shapes, token ids) before it
+broadcasts anything, so a malformed request never reaches the other ranks.  Every hand-off
+carries a status word ahead of its rows: a rank whose compute raises (or whose predecessor
+failed) forwards zero rows with the failing rank's status and message instead of leaving its
+successor blocked; rank 0 then drops the request's sessions on every rank and raises the
+failing rank's error, and every rank keeps serving.
 Layer split inside the group: pipeline.balanced_split (the lm_head priced on the rank that
 owns it, in decode bytes) over the stage's [start_layer, end_layer].
 """
@@ -135,11 +142,34 @@ class SpanGroup(PartitionedQwen2):
         return obj[0]
 
     # ---------------------------------------------------------------- the hooks
+    def _validate(self, requests, rows, model_in):
+        """Rank 0, before anything is broadcast: the checks SpanRuntime.forward would make."""
+        if not requests or any(n <= 0 for _, n in requests):
+            raise ValueError("forward needs at least one request with n_new_tokens >= 1")
+        keys = [k for k, _ in requests if k is not None]
+        if len(set(keys)) != len(keys):
+            raise ValueError("a session may appear only once per forward call")
+        if self.stage == 0:
+            ids = torch.as_tensor(model_in).reshape(-1)
+            if ids.numel() != rows:
+                raise ValueError(f"{ids.numel()} ids for {rows} request tokens")
+            if int(ids.min()) < 0 or int(ids.max()) >= self.dims.vocab:   # nn.Embedding's IndexError
+                raise IndexError("index out of range in self (token id outside the vocabulary)")
+        elif model_in.numel() != rows * self.dims.hidden:
+            raise ValueError(f"hidden rows of {tuple(model_in.shape)} for {rows} request tokens")
+
     @torch.no_grad()
     def _run(self, requests, model_in):
         rows = sum(n for _, n in requests)
+        self._validate(requests, rows, model_in)
         self._bcast({"op": "run", "requests": requests, "rows": rows})
-        return self._step(requests, rows, model_in)
+        out, err = self._step(requests, rows, model_in)
+        if err is not None:
+            for key, _ in requests:          # their pages may be half-written on some ranks
+                if key is not None:
+                    self._release(key)
+            raise RuntimeError(f"span group: {err}")
+        return out
 
     def _release(self, key):
         self._bcast({"op": "release", "key": key})
@@ -149,31 +179,67 @@ class SpanGroup(PartitionedQwen2):
     def last_next_ids(self):
         return self._next_ids
 
+    STATUS_WORDS = 64   # status word + the failing rank's message (UTF-8, 252 bytes)
+
+    def _status(self, code, msg=""):
+        t = torch.zeros(self.STATUS_WORDS, dtype=torch.int32)
+        t[0] = code
+        raw = msg.encode("utf-8", "replace")[:4 * (self.STATUS_WORDS - 1)]
+        raw += b"\0" * (4 * (self.STATUS_WORDS - 1) - len(raw))
+        t[1:] = torch.frombuffer(bytearray(raw), dtype=torch.int32)
+        return t.to(self.device)
+
+    @staticmethod
+    def _status_msg(t):
+        t = t.cpu()
+        return int(t[0]), bytes(t[1:].numpy().tobytes()).rstrip(b"\0").decode("utf-8", "replace")
+
     @torch.no_grad()
     def _step(self, requests, rows, model_in=None):
         """This rank's share of one request: input from the previous rank (rank 0: model_in),
-        output to the next (the group's last rank: result back to rank 0)."""
+        output to the next (the group's last rank: result back to rank 0), each hand-off a
+        status word then the rows.  Never raises on a compute fault: returns (output on rank 0
+        or None, error message or None)."""
         h = self.dims.hidden
         W, r = self.world, self.rank
-        if r > 0:
-            model_in = self._recv((rows, h), torch.bfloat16, r - 1)
-        out = self.model.run(requests, model_in)
-        self.span.check_errors()
         last_stage = self.stage == self.num_stages - 1
+        code, msg = 0, ""
+        if r > 0:
+            code, msg = self._status_msg(self._recv((self.STATUS_WORDS,), torch.int32, r - 1))
+            model_in = self._recv((rows, h), torch.bfloat16, r - 1)
+        out = None
+        if code == 0:
+            try:
+                out = self.model.run(requests, model_in)
+                self.span.check_errors()
+            except Exception as e:  # noqa: BLE001 -- reported to rank 0, the group stays in lockstep
+                code, msg, out = r + 1, f"rank {r}: {type(e).__name__}: {e}", None
         if r < W - 1:
-            self._send(out.reshape(rows, h), r + 1)
+            self._send(self._status(code, msg), r + 1)
+            self._send(out.reshape(rows, h) if code == 0 else torch.zeros(rows, h, dtype=torch.bfloat16, device=self.device), r + 1)
         elif r > 0:
-            self._send(self.model.last_next_ids if last_stage else out.reshape(rows, h), 0)
-        if r == 0:
-            if W > 1:
-                if last_stage:
-                    self._next_ids = self._recv((len(requests),), torch.int32, W - 1)
-                    return None
-                return self._recv((rows, h), torch.bfloat16, W - 1)
+            self._send(self._status(code, msg), 0)
             if last_stage:
-                self._next_ids = self.model.last_next_ids
-            return out
-        return None
+                self._send(self.model.last_next_ids if code == 0 else torch.zeros(len(requests), dtype=torch.int32, device=self.device), 0)
+            else:
+                self._send(out.reshape(rows, h) if code == 0 else torch.zeros(rows, h, dtype=torch.bfloat16, device=self.device), 0)
+        if r != 0:
+            return None, (msg or None)
+        if W > 1:
+            if code == 0:     # rank 0's own failure is already known; the chain's is read back
+                code, msg = self._status_msg(self._recv((self.STATUS_WORDS,), torch.int32, W - 1))
+            else:
+                self._recv((self.STATUS_WORDS,), torch.int32, W - 1)
+            if last_stage:
+                ids = self._recv((len(requests),), torch.int32, W - 1)
+                if code == 0:
+                    self._next_ids = ids
+                return None, (msg or None) if code else None
+            res = self._recv((rows, h), torch.bfloat16, W - 1)
+            return (res if code == 0 else None), (msg or None) if code else None
+        if last_stage and code == 0:
+            self._next_ids = self.model.last_next_ids
+        return out, (msg or None) if code else None
 
     def serve_forever(self):
         """Ranks 1..: follow rank 0's requests until shutdown()."""

@@ -1,0 +1,37 @@
+"""torch.ops.inferd: the span engine's C-ABI registered as PyTorch-ROCm operators
+(inferd_amd/csrc/torch_ops.cpp -> libinferd_torch.so, built in-tree with the engine).
+
+    import inferd_amd.ops                      # registers torch.ops.inferd.*
+    span = torch.ops.inferd.span_create(cfg, eps, theta, device)
+    words, shape = torch.ops.inferd.kv_build_batch(table, seqs, n_new, device)
+    torch.ops.inferd.span_forward(span, words, shape, ids, None, None, next_ids, logits)
+
+Every op runs on torch's current HIP stream and raises RuntimeError with the library's message
+on a non-zero status.  There is no fallback: a missing library raises at import."""
+from __future__ import annotations
+
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libinferd_torch.so")
+
+if not os.path.exists(LIB_PATH):
+    raise RuntimeError(f"libinferd_torch.so not built ({LIB_PATH}); run __graft_entry__.build()")
+from . import _lib  # noqa: E402  (checks the engine library's ABI version first)
+
+_lib.load()
+torch.ops.load_library(LIB_PATH)
+ops = torch.ops.inferd
+
+OPS = ("span_create", "span_destroy", "span_init_synthetic", "span_set_weight", "span_forward", "span_lm_head",
+       "graph_capture", "graph_launch", "graph_destroy", "kv_create", "kv_destroy", "kv_reserve", "kv_advance",
+       "kv_release", "kv_query", "kv_build_batch")
+
+
+def span_config(dims, first_layer: int, n_layers: int, *, has_embed: bool, has_lm_head: bool, kv_pages: int,
+                max_tokens: int, max_seqs: int, max_positions: int) -> list:
+    """The 14 config ints of span_create (InferdSpanConfig order)."""
+    return [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
+            n_layers, int(has_embed), int(has_lm_head), max_positions, kv_pages, max_tokens, max_seqs]

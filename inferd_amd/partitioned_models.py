@@ -252,7 +252,13 @@ class PartitionedQwen2:
       * {"session_id": s, "close_session": True} releases the session along the chain.
     Sessions beyond `max_sessions` (INFERD_MAX_SESSIONS, default 64) or a full KV pool evict
     the least recently used one (the reference's session caches are never freed,
-    qwen3_server_module.py:220)."""
+    qwen3_server_module.py:220).
+    A downstream stage that no longer holds a session's rows (evicted under another pool size
+    or session cap, restarted) answers {"session_id", "session_lost": True, "generated_ids"}
+    instead of raising; later stages pass that answer through (dropping their own copy), so it
+    reaches the client as the chain's result.  The client resends the same generated_ids with
+    "restart_session": True, and stage 0 recomputes the session from position 0 (every
+    downstream stage then restarts it too: past_len 0)."""
 
     def __init__(self, model_name: str, num_stages: int, stage: int, parts_path: str):
         self.stage = stage
@@ -353,23 +359,26 @@ class PartitionedQwen2:
             self.close_session(sid)
             return {"session_id": sid, "close_session": True} if not self._last else \
                 {"session_id": sid, "closed": True}
+        if inputs.get("session_lost"):         # an upstream stage lost it: pass the answer on
+            self.close_session(sid)
+            return {"session_id": sid, "session_lost": True, "generated_ids": inputs.get("generated_ids")}
         gen_ids, model_in = self._prepare_inputs(inputs)
         key = ("sess", sid)
         past = self._cached_len(key)
         if self.stage == 0:
             seen = self._sessions.get(sid)
             ids = model_in.reshape(-1).tolist()
-            if seen is None or past != len(seen) or ids[:past] != seen or len(ids) <= past:
-                self.close_session(sid)        # not a continuation: restart from position 0
+            if inputs.get("restart_session") or seen is None or past != len(seen) or ids[:past] != seen or \
+                    len(ids) <= past:
+                self.close_session(sid)        # not a continuation (or the client asks): restart from 0
                 past = 0
             new = model_in[:, past:]
         else:
             first_pos = int(inputs.get("past_len", 0))
             if first_pos != past:
-                if first_pos != 0:
-                    raise RuntimeError(f"session {sid!r}: hidden rows start at position {first_pos} but "
-                                       f"this stage has {past} cached")
                 self.close_session(sid)
+                if first_pos != 0:             # rows past a prefix this stage no longer holds
+                    return {"session_id": sid, "session_lost": True, "generated_ids": gen_ids}
                 past = 0
             new = model_in
         n = new.shape[1]

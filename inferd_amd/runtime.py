@@ -63,6 +63,9 @@ LINEAR_SCALE, NORM_SCALE = 0.034641016151377546, 0.1
 # margins for greedy-parity runs; every layer weight is unchanged.
 EMBED_BOOST, LM_MIX = 64.0, 1.0
 PERM_MUL, PERM_ADD = 7919, 17
+# embedding factor per profile ("peaked_deep": x512 for Qwen3-8B-deep spans, whose random
+# layers otherwise drown the x64 embedding; oracle/weightgen.py PROFILE_BOOST)
+PROFILE_BOOST = {"peaked": EMBED_BOOST, "peaked_deep": 512.0}
 
 
 def gen_tensor(seed: int, tid: int, shape, norm: bool, device) -> torch.Tensor:
@@ -260,19 +263,19 @@ class SpanRuntime:
         return torch.cuda.current_stream(self.device)
 
     def init_synthetic(self, seed: int, profile: str = "random"):
-        """Counter-based weights (the offline stand-in for a checkpoint).  profile="peaked"
-        re-composes embed / lm_head as oracle/weightgen.py's peaked profile (large greedy
-        margins for token-exact parity runs)."""
-        if profile not in ("random", "peaked"):
+        """Counter-based weights (the offline stand-in for a checkpoint).  profile="peaked" /
+        "peaked_deep" re-compose embed / lm_head as oracle/weightgen.py's peaked profiles (large
+        greedy margins for token-exact parity runs)."""
+        if profile != "random" and profile not in PROFILE_BOOST:
             raise ValueError(f"unknown synthetic profile {profile!r}")
         with torch.cuda.device(self.device):
             _lib.check(self.lib.inferd_span_init_synthetic(self.handle, seed, self._stream().cuda_stream))
-            if profile == "peaked" and (self.has_embed or self.has_lm_head):
+            if profile in PROFILE_BOOST and (self.has_embed or self.has_lm_head):
                 d = self.dims
                 emb = gen_tensor(seed, GLOBAL_TENSOR_IDS["embed_tokens"], (d.vocab, d.hidden), False,
                                  self.device).float()
                 if self.has_embed:
-                    self.set_weight(-1, "embed_tokens", (emb * EMBED_BOOST).to(torch.bfloat16))
+                    self.set_weight(-1, "embed_tokens", (emb * PROFILE_BOOST[profile]).to(torch.bfloat16))
                 if self.has_lm_head:
                     lm = gen_tensor(seed, GLOBAL_TENSOR_IDS["lm_head"], (d.vocab, d.hidden), False,
                                     self.device).float()
@@ -439,6 +442,7 @@ class SpanRuntime:
                 else:
                     st = self._seq(sid)
                 states.append(st)
+            ok, advanced = False, False
             try:
                 for st, (_, n) in zip(states, requests):
                     self.kv.reserve(st.seq, n)
@@ -473,6 +477,7 @@ class SpanRuntime:
                              layers=c_lay)
                     for i, _, t in call:
                         self.kv.advance(states[i].seq, t)
+                    advanced = True
                     if not single:
                         if finals:
                             dst = torch.tensor([call[j][0] for j in finals], device=dev)
@@ -484,9 +489,13 @@ class SpanRuntime:
                         if c_lay is not None:
                             lay[:, r0:r0 + m] = c_lay
                         keep.append((c_nid, c_lg, c_lay))
+                ok = True
             finally:
                 for st in temp:
                     self.kv.release(st.seq)
+                if not ok and advanced:   # a chunked call that failed part-way leaves no
+                    for sid in sids:      # half-advanced session behind: drop its sessions
+                        self.release(sid)
         out = {}
         if hid is not None:
             out["hidden"] = hid

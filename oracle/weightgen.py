@@ -162,6 +162,10 @@ def gen_tensor_bf16_bits(seed: int, tid: int, shape, name: str, use_c: bool = Tr
 EMBED_BOOST = 64.0
 LM_MIX = 1.0
 PERM_MUL, PERM_ADD = 7919, 17
+# "peaked_deep": the same structure for deep / wide models (Qwen3-8B's 36 layers of 4096): the
+# random layers' accumulated residual (rms ~10 after 36 layers) drowns a x64 embedding, leaving
+# top-1 margins of a few hundredths of a logit, so the embedding gets x512 instead
+PROFILE_BOOST = {"peaked": EMBED_BOOST, "peaked_deep": 512.0}
 
 
 def peaked_perm(vocab: int) -> np.ndarray:

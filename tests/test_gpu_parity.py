@@ -213,6 +213,37 @@ def test_nn_forward_session_cache_matches_full_recompute(q06_peaked):
            new_row_hidden_vs_oracle_worst_rms_rel=worst_rms)
 
 
+def test_nn_forward_session_lost_downstream_restarts(q06_peaked):
+    """A downstream stage that lost a session (evicted there only) answers session_lost instead
+    of raising; the client resends with restart_session and the chain recomputes from position
+    0: the ids stay those of the stateless chain, and the session then continues cached."""
+    n0, n1, _, _ = q06_peaked
+    d = R.CONFIGS["qwen3-0.6b"]
+    prompt = torch.randint(0, d.vocab, (24,), generator=torch.Generator().manual_seed(14)).tolist()
+    ids, full = list(prompt), []
+    for _ in range(6):
+        o1 = n1.forward(n0.forward({"generated_ids": ids}))
+        full.append(o1["next_token_id"])
+        ids = o1["generated_ids"]
+    ids, got, events = list(prompt), [], []
+    for step in range(6):
+        if step == 3:
+            n1.close_session("lost")           # stage 1 alone forgets the session (an eviction there)
+        inp = {"generated_ids": ids, "session_id": "lost"}
+        o1 = n1.forward(n0.forward(inp))
+        if o1.get("session_lost"):
+            events.append(step)
+            assert o1["session_id"] == "lost" and o1["generated_ids"] == ids
+            o0 = n0.forward({**inp, "restart_session": True})
+            assert o0["past_len"] == 0 and _hidden(o0["hidden_meta"]).shape[1] == len(ids)
+            o1 = n1.forward(o0)
+        got.append(o1["next_token_id"])
+        ids = o1["generated_ids"]
+    assert events == [3] and got == full
+    n1.forward(n0.forward({"session_id": "lost", "close_session": True}))
+    record("nn_forward_session_lost_restart", lost_at=events, identical=True)
+
+
 def test_nn_forward_long_prompt_chunked(q06_peaked):
     """A 4500-token prompt (> the 4096-row engine call) through the node API, stateless and
     with a session: chunked prefill through the sequence's own pages; the greedy id and the
@@ -471,6 +502,9 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes):
 # BASELINE config 3's even splits and the bench's balanced 8-way split, ranks sharing this box's
 # GPU (hand-offs staged through gloo), B=2 sequences per microbatch (every microbatch the same
 # two 64-token prompts, on its own pages), 16 free-running decode steps as decode-graph replays.
+# Profile "peaked_deep" (embedding x512, oracle/weightgen.py): with the x64 "peaked" profile the
+# 36 random 8B layers leave top-1 margins of 0.03-0.2 logits, where two CPU oracles on different
+# host ISAs already disagree (measured: step 4 of sequence 0, margin 0.125).
 B8X, T8X, STEPS8X = 2, 64, 16
 
 
@@ -484,7 +518,7 @@ def q8b_oracle_greedy():
     the last-row logits[k] (bf16, [B, vocab]) that chose them (Qwen3Server.send semantics:
     prefill, then one cached token per step)."""
     d = R.CONFIGS["qwen3-8b"]
-    sp = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa", profile="peaked")
+    sp = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa", profile="peaked_deep")
     lg = sp.forward_cached("p", _q8b_exact_prompts())[:, -1]
     ids, logits = [], []
     for k in range(STEPS8X + 1):
@@ -509,7 +543,7 @@ def _pipe_exact_worker(rank, world, port, sizes, out_dir):
     spans = [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
     first, n = spans[rank]
     st = PipelineStage(d, rank, world, first, n, device=dev, seed=SEED, n_microbatches=world, batch=B8X,
-                       max_ctx=T8X + STEPS8X + 8, prefill_chunk=2, profile="peaked", want_logits=True)
+                       max_ctx=T8X + STEPS8X + 8, prefill_chunk=2, profile="peaked_deep", want_logits=True)
     cap = {}
     st.prefill([_q8b_exact_prompts()] * world, capture=cap)
     st.prepare_decode(STEPS8X)

@@ -33,6 +33,9 @@ def _chain(n0, n1, prompt, steps, sid=None):
     return out
 
 
+FAIL_ROWS = 7   # a request of this many rows raises on the group's last rank (fault injection)
+
+
 def _worker(rank, world, port, grouped_stage, out_path):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -43,6 +46,14 @@ def _worker(rank, world, port, grouped_stage, out_path):
     from inferd_amd.partitioned_models import PartitionedQwen2
     grp = SpanGroup("qwen3-0.6b", 2, grouped_stage, SPECS[grouped_stage])
     if rank != 0:
+        if rank == world - 1:
+            run = grp.model.run
+
+            def faulty(requests, model_in, **kw):
+                if sum(n for _, n in requests) == FAIL_ROWS:
+                    raise RuntimeError("injected fault")
+                return run(requests, model_in, **kw)
+            grp.model.run = faulty
         grp.serve_forever()
         dist.destroy_process_group()
         return
@@ -50,8 +61,23 @@ def _worker(rank, world, port, grouped_stage, out_path):
     single = PartitionedQwen2("qwen3-0.6b", 2, other, SPECS[other])
     n0, n1 = (grp, single) if grouped_stage == 0 else (single, grp)
     prompt = torch.randint(0, 151936, (32,), generator=torch.Generator().manual_seed(5)).tolist()
-    res = {"split": grp.first_rank_layers, "stateless": _chain(n0, n1, prompt, 8),
-           "session": _chain(n0, n1, prompt, 8, sid="g")}
+    res = {"split": grp.first_rank_layers}
+    # faults: a bad token id is refused on rank 0 before anything is broadcast; a compute fault
+    # on the group's last rank comes back as rank 0's RuntimeError; the group keeps serving
+    faults = []
+    bad = {"generated_ids": [1, 2, 151936]} if grouped_stage == 0 else None
+    if bad is not None:
+        try:
+            n1.forward(n0.forward(bad))
+        except IndexError:
+            faults.append("index")
+    try:
+        n1.forward(n0.forward({"generated_ids": prompt[:FAIL_ROWS]}))
+    except RuntimeError as e:
+        faults.append("injected" if "injected fault" in str(e) else str(e))
+    res["faults"] = faults
+    res["stateless"] = _chain(n0, n1, prompt, 8)
+    res["session"] = _chain(n0, n1, prompt, 8, sid="g")
     n1.forward(n0.forward({"session_id": "g", "close_session": True}))
     res["free_after_close"] = grp.span.kv.n_free == grp.span.kv.n_pages
     grp.shutdown()
@@ -80,6 +106,7 @@ def test_span_group_node_matches_single_gpu_chain(tmp_path, world, grouped_stage
     res = torch.load(out, weights_only=True)
     print(f"world {world}, stage {grouped_stage} grouped, split {res['split']}: {res['stateless']}")
     assert len(res["split"]) == world
+    assert res["faults"] == (["index", "injected"] if grouped_stage == 0 else ["injected"]), res["faults"]
     assert res["stateless"] == res["reference"]
     assert res["session"] == res["reference"]
     assert res["free_after_close"]
