@@ -91,9 +91,12 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const u16* __restrict__ x,
                                                       const int32_t* __restrict__ row_index,
                                                       int row_sub, const u16* __restrict__ w,
                                                       u16* __restrict__ y, int64_t ldy, int N,
-                                                      float eps, int pack) {
+                                                      float eps, int pack, unsigned long long* zero_slots,
+                                                      int n_slots) {
   __shared__ float red[4];
   int row = blockIdx.x;
+  // this row's words of the SSQ slots the span's decode GEMVs will fill (kernels.h DecodeNorm)
+  for (int i = threadIdx.x; i < n_slots * SSQ_SHARDS * 2; i += 256) zero_slots[(int64_t)i * 64 + row] = 0ull;
   int src_row = row_index ? row_index[row] - row_sub : row;
   const u16* xr = x + (int64_t)src_row * ldx;
   int nch = N / 8;
@@ -132,18 +135,24 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const u16* __restrict__ x,
 }
 
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
-                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out) {
+                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out,
+                    unsigned long long* zero_slots, int n_slots) {
+  if (!zero_slots || M > 64) n_slots = 0;
   const int pk = pack_out ? 1 : 0;
   int ch = (N / 8 + 255) / 256;
   dim3 g(M), b(256);
   if (ch <= 1)
-    hipLaunchKernelGGL(rmsnorm_kernel<1>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk);
+    hipLaunchKernelGGL(rmsnorm_kernel<1>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk,
+                       zero_slots, n_slots);
   else if (ch <= 2)
-    hipLaunchKernelGGL(rmsnorm_kernel<2>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk);
+    hipLaunchKernelGGL(rmsnorm_kernel<2>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk,
+                       zero_slots, n_slots);
   else if (ch <= 4)
-    hipLaunchKernelGGL(rmsnorm_kernel<4>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk);
+    hipLaunchKernelGGL(rmsnorm_kernel<4>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk,
+                       zero_slots, n_slots);
   else
-    hipLaunchKernelGGL(rmsnorm_kernel<8>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk);
+    hipLaunchKernelGGL(rmsnorm_kernel<8>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk,
+                       zero_slots, n_slots);
 }
 
 // ------------------------------------------------------------------ rope table

@@ -42,8 +42,8 @@ __device__ __forceinline__ float row16_sum(float v) {
 // RMSNorm modes of the decode GEMV (NORM template argument, kernels.h DN_*):
 //  DN_NONE  A used as is;
 //  DN_EXACT Qwen3RMSNorm at the reference rounding points (qwen3_server_module.py:19-25):
-//           A' = bf16(w * bf16(A * r)), r = 1 / sqrt(sum_p ssq_in[p][row] / K + eps) from the
-//           per-tile sums of squares the producer wrote (ssq_out below), applied to each A
+//           A' = bf16(w * bf16(A * r)), r = 1 / sqrt(ssq[row] / K + eps) from the SSQ slot
+//           the producer filled (ssq_out below; kernels.h DecodeNorm), applied to each A
 //           fragment before its MFMA.
 struct DecodeArgs {
   const u16* A;
@@ -61,43 +61,61 @@ struct DecodeArgs {
   // to part[y][row][col] (row stride ldp).
   float* part;
   int64_t ldp;
-  // DN_EXACT: producer partial sums of squares ssq_in[p * MP + row] (MP = M rounded up to a
-  // multiple of 4: one part's rows are contiguous), p < n_parts, and the
+  // DN_EXACT: the SSQ slot (kernels.h DecodeNorm) holding A's row sums of squares, and the
   // norm weight [K]
-  const float* ssq_in;
-  int n_parts;
+  const unsigned long long* ssq_in;
   const u16* norm_w;
-  // EPI_RESID producer side: ssq_out[tile * MP + row] = sum over the tile's 16 columns of
-  // the stored bf16 outputs squared (the next DN_EXACT consumer's ssq_in), or null
-  float* ssq_out;
+  // EPI_RESID producer side: the SSQ slot that receives the row sums of squares of the stored
+  // bf16 outputs (the next DN_EXACT consumer's ssq_in), or null
+  unsigned long long* ssq_out;
   // GEMM_PACK_A / GEMM_PACK_C (launch_gemm `pack`): A read / EPI_SILU output written
   // fragment-packed (packed_index); decode path only
   int pack;
 };
 
-#define DECODE_NORM_MAXK 8192  // DN_EXACT: K of one workgroup (hidden <= 8192)
-// (the timing probes of the DN_EXACT parts live in tools/decode_gemv_lab.hip's build of the
-// round-2 tree, git 6a90f3d: DN_PROBE=1..8)
 
-// DN_EXACT workgroups carry one extra "norm wave" (wave NW): it alone loads and reduces the
-// row sums of squares and stages the norm weight, so the NW streaming waves issue their whole
-// weight prologue at once and wait for the row scales on a raw barrier -- their vmcnt never
-// includes those loads (a wave that waited for its own row-scale loads had to drain its weight
-// stages behind them, since vmcnt retires in order; so does __syncthreads: +3-4 us per launch)
-template <int NORM>
-constexpr bool dn_norm_wave() {
-  return NORM == DN_EXACT;
+// Row sums of squares between a decode producer and its DN_EXACT consumer (kernels.h DecodeNorm):
+// q (>= 0, a 16-column tile's fp32 sum of squares of bf16 values) as the fixed-point pair
+// hi = floor(q * 2^8), lo = frac(q * 2^8) * 2^32, added to one shard of the slot by no-return
+// agent-scope 64-bit atomics (performed at the memory side: every XCD adds to the same words).
+// Integer adds commute, so the slot's sum is the same whatever order the 256 producer workgroups
+// arrive in.  q >= 2^47 (|x| > 3e6 in bf16 rows) or NaN saturates: the reference's fp32 sum
+// would be as meaningless.  A workgroup adds its 16 rows' hi words and lo words with ONE wave
+// instruction (lanes 0-15 hi, 16-31 lo: two contiguous 128-B runs), i.e. four 64-B atomic
+// requests; the memory side serialises requests per 64-B segment, so 32 such per segment (one
+// per shard member) instead of 8 per workgroup when each row went alone (+4 us per o GEMV).
+__device__ __forceinline__ unsigned long long ssq_fixed(float q, bool lo_half) {
+  float t = q * 256.0f;
+  t = t < 3.6028797e16f ? t : 3.6028797e16f;  // 2^55 (also maps NaN here)
+  const float ft = floorf(t);
+  return lo_half ? (unsigned long long)(unsigned)((t - ft) * 4294967296.0f) : (unsigned long long)ft;
 }
+// the sum of a row's shards (hi0, lo0: this lane's two shards, summed; the wave's four 16-lane
+// groups hold the other six) -> r = 1 / sqrt(sum / K + eps), in every lane of the row
+__device__ __forceinline__ float ssq_rscale(unsigned long long hi, unsigned long long lo, int K, float eps) {
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    hi += __shfl_xor(hi, o);
+    lo += __shfl_xor(lo, o);
+  }
+  const double tot = (double)hi * (1.0 / 256.0) + (double)lo * (1.0 / 1099511627776.0);
+  return 1.0f / sqrtf((float)tot / (float)K + eps);
+}
+
 template <int NW, int NORM>
 constexpr int decode_threads() {
-  return (NW + (dn_norm_wave<NORM>() ? 1 : 0)) * 64;
+  return NW * 64;
 }
 
-// dynamic LDS of a DN_EXACT workgroup over KT 32-column steps: the bf16 norm weight (plus its
-// fp32 image in one-stream kernels; gemm_decode_kernel's dn_lds)
-template <int NORM, int S>
+// dynamic LDS of a DN_EXACT workgroup over KT 32-column steps: per wave the staged bf16 norm
+// weight of its batches, its fp32 copy in one-stream kernels, and the staged SSQ pieces
+template <int NW, int TW>
+__host__ __device__ constexpr int dn_region_bytes(int KT) {
+  return ((KT / TW + NW - 1) / NW * TW * 4 + 63) / 64 * 1024;
+}
+template <int NORM, int S, int NW, int TW, int MT>
 constexpr unsigned dn_lds_bytes(int KT) {
-  return NORM == DN_EXACT ? (unsigned)KT * (S == 1 ? 192u : 64u) : 0u;
+  return NORM == DN_EXACT ? (unsigned)(NW * (dn_region_bytes<NW, TW>(KT) * (S == 1 ? 3 : 1) + MT * 2048)) : 0u;
 }
 
 // APK: A is read fragment-packed (common.h packed_index: the decode path's act buffer, attention
@@ -106,21 +124,18 @@ template <int MT, int S, int NW, int TW, int D, int EPI, int NORM, bool APK = fa
 __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kernel(DecodeArgs g) {
   constexpr int NV = S * MT * 64;  // f32x4 values of one workgroup result
   __shared__ f32x4 red[NW][NV];
-  __shared__ __attribute__((aligned(16))) float sm_r[NORM == DN_EXACT ? 64 : 4];
-  // DN_EXACT (dynamic LDS, dn_lds_bytes): this workgroup's K range of the norm weight as loaded
-  // (bf16, sm_wb, KT * 32) and, for one-stream kernels, as fp32 (sm_w: saves the streaming
-  // waves one unpack per element; the two-stream kernels amortise the unpack over two MFMAs
-  // and have no registers to spare for the wider reads)
+  // DN_EXACT (dynamic LDS, dn_lds_bytes): each wave stages the norm weight of its own batches
+  // only (so no wave waits for another before its ring): bf16 as loaded (nstage, 1 KiB per 64
+  // pieces), and for one-stream kernels an fp32 copy (nstage_f: saves the streaming waves one
+  // unpack per element; the two-stream kernels amortise the unpack over two MFMAs)
   extern __shared__ __attribute__((aligned(16))) float dn_lds[];
   constexpr bool W_F32 = S == 1;
-  float* const sm_w = dn_lds;
   const int M = g.M;
   const int nt = blockIdx.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // K range of this workgroup (all of K unless EPI_PARTIAL splits it over gridDim.y)
   const int kt0 = (EPI == EPI_PARTIAL) ? (int)blockIdx.y * (g.KT / (int)gridDim.y) : 0;
   const int KT = (EPI == EPI_PARTIAL) ? g.KT / (int)gridDim.y : g.KT;
-  u16* const sm_wb = (u16*)(dn_lds + (W_F32 ? KT * 32 : 0));
   // Two ring forms.  The exact-norm kernels (PADDED) load through buffer descriptors: a batch
   // index past the wave's last batch becomes an out-of-range offset (the load returns zeros),
   // every step issues unconditionally and the loop runs whole passes of straight-line code, so
@@ -167,13 +182,21 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   int b = swave;
   // this wave's batches b, b + NW, ... < nb
   const int nbw = swave < nb ? (nb - swave + NW - 1) / NW : 0;
+  // DN_EXACT staging regions: dn_region_bytes(KT) per wave (whole KiB: a DMA instruction writes
+  // 64 pieces), bf16 then (W_F32) the fp32 copy at twice the stride
+  const int rgn = dn_region_bytes<NW, TW>(KT);
+  char* const nssq = (char*)dn_lds + NW * rgn * (S == 1 ? 3 : 1) + swave * MT * 2048;  // [MT][8][2][16] u64
+  u16* const nstage = (u16*)((char*)dn_lds + swave * rgn);
+  float* const nstage_f = (float*)((char*)dn_lds + NW * rgn + swave * 2 * rgn);
   bf16x8 wv[D][S][TW], av[D][TW][MT];
   // DN_EXACT: a stage's activation fragments are issued BEFORE its weights, so the
   // normalisation of A can run as soon as A (L2) lands, while the weight bytes (HBM) are
   // still in flight (vmcnt retires in issue order)
   constexpr bool A_FIRST = NORM == DN_EXACT;
-  constexpr bool FULL_PROLOGUE = NORM == DN_EXACT;
-  constexpr bool PADDED = NORM == DN_EXACT;
+  // the lm_head GEMV (EPI_ARGMAX, 4 batches per wave) keeps the guarded ring with the exact norm
+  // too: its padded passes would issue 2 dead batches per 4 live ones
+  constexpr bool PADDED = NORM == DN_EXACT && EPI != EPI_ARGMAX;
+  constexpr bool FULL_PROLOGUE = PADDED;
   constexpr int AKS = APK ? 512 : 32;  // elements between consecutive k-tiles of one lane's A
   constexpr int AKB = 2 * AKS;         // the same in bytes (buffer-load offsets)
   auto issue = [&](auto stage, int bb) {
@@ -240,74 +263,79 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   float rr[MT];  // DN_EXACT: r of row mt*16 + (lane & 15)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) rr[mt] = 1.0f;
-  if constexpr (dn_norm_wave<NORM>()) {
-    if (wave == NW) {
-      // the norm wave: the norm weight of this workgroup's K range (to LDS as fp32), then
-      // the M rows' partial sums of squares: lane l takes row quad l / PPW
-      // (QM = ceil(M / 4) quads, PPW = the largest power of two <= 64 / QM lanes each) and
-      // parts l % PPW, l % PPW + PPW, ... (sixteen 16-B loads in flight), a butterfly over the
-      // PPW lanes (fixed order: deterministic), r = 1 / sqrt(sum / K + eps) into LDS.  Its
-      // loads go out BEFORE the streaming waves' weight prologue (first barrier): issued
-      // behind the prologue they queued behind the HBM misses in the CU's memory pipeline
-      const int QM = (M + 3) >> 2;
-      int PPW = 64;
-      while (PPW * QM > 64) PPW >>= 1;
-      const int quad = min(lane / PPW, QM - 1), p0 = lane % PPW;
-      const int MP = QM * 4;  // part stride of ssq_in (rows rounded up to a quad)
-      // the norm weight goes to LDS by LDS-DMA, the sums of squares to registers (sixteen
-      // LDS-DMA loads made hipcc's waitcnt pass drain the streaming waves' ring)
-      f32x4 v[16];
-      for (int c = lane; c < KT * 4; c += 64)
-        __builtin_amdgcn_global_load_lds((const void*)(g.norm_w + kt0 * 32 + c * 8), (void*)(sm_wb + (c - lane) * 8),
-                                         16, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        v[i] = *(const f32x4*)(g.ssq_in + min(p0 + i * PPW, g.n_parts - 1) * MP + 4 * quad);
-      raw_barrier();  // #1: the row-scale loads are out; the streaming waves may issue theirs
+  if constexpr (NORM == DN_EXACT) {
+    if (nbw > 0) {
+      // Issued before the weight prologue, so the waits for them are counted (vmcnt retires in
+      // issue order) and never drain the ring: (1) the row sums of squares, lane l reading shards
+      // 2(l/16), 2(l/16)+1 of row mt*16 + l%16; (2) the norm weight of this wave's own batches by
+      // LDS-DMA into the wave's staging region (no registers): 16-B piece p = 64i + lane is
+      // batch j = p / (4TW) of the wave, columns 8(p % (4TW)) on, so a step's fragment sits at
+      // (j TW + u) 32 + 8(lane / 16) of the region, like the global columns with b -> j
+      typedef __attribute__((address_space(3))) void* lds_ptr;
       {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (W_F32)
-        for (int c = lane; c < KT * 4; c += 64) {
-          const u16x8 nv = *(const u16x8*)(sm_wb + c * 8);
+        // (1) by LDS-DMA too (no registers held across the prologue): piece (mt, h) of lane l
+        // to the wave's ssq area at ((mt * 2 + h) * 64 + l) * 16
+        const __amdgpu_buffer_rsrc_t sr =
+            __builtin_amdgcn_make_buffer_rsrc((void*)g.ssq_in, 0, SSQ_SLOT_WORDS * 8, 0x00020000);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            // 128-B run c = (shard, hi|lo) of rows mt*16.. -> LDS [shard][hi|lo][16 rows] u64
+            const int c = (64 * k + lane) >> 3;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(sr, (lds_ptr)(nssq + mt * 2048 + k * 1024), 16,
+                                                     (c * 64 + mt * 16) * 8 + (lane & 7) * 16, 0, 0, 0);
+          }
+      }
+      {
+        const __amdgpu_buffer_rsrc_t nr =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(g.norm_w + kt0 * 32), 0, KT * 64, 0x00020000);
+        const int npieces = nbw * TW * 4;
+        for (int i = 0; i * 64 < npieces; ++i) {  // wave-uniform trip count
+          const int p = 64 * i + lane;
+          const int j = p / (4 * TW), c = p % (4 * TW);
+          const int col = ((swave + j * NW) * TW) * 32 + 8 * c;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(nr, (lds_ptr)(nstage + i * 512), 16,
+                                                   p < npieces ? col * 2 : OOB, 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // the staged row sums and norm weight have landed once every load but the prologue's has
+      // retired
+      if constexpr (PADDED) {  // prologue: all D stages
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          (issue(std::integral_constant<int, I>{}, b + I * NW), ...);
+        }(std::make_integer_sequence<int, D>{});
+        vm_wait<D * TW * (MT + S)>();
+      } else {  // stages 0..D-2, guarded
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          ((b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
+        }(std::make_integer_sequence<int, D - 1>{});
+        if (nbw >= D - 1)
+          vm_wait<(D - 1) * TW * (MT + S)>();
+        else
+          vm_wait<0>();
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        // lane l: row l % 16, shards 2(l / 16) and 2(l / 16) + 1
+        const unsigned long long* w =
+            (const unsigned long long*)(nssq + mt * 2048) + (4 * (lane >> 4)) * 16 + (lane & 15);
+        rr[mt] = ssq_rscale(w[0] + w[32], w[16] + w[48], g.KT * 32, g.eps);
+      }
+      if constexpr (W_F32) {
+        for (int p = lane; p < nbw * TW * 4; p += 64) {
+          const u16x8 nv = *(const u16x8*)(nstage + p * 8);
           f32x4 lo, hi;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             lo[j] = bf2f(nv[j]);
             hi[j] = bf2f(nv[4 + j]);
           }
-          *(f32x4*)(sm_w + c * 8) = lo;
-          *(f32x4*)(sm_w + c * 8 + 4) = hi;
+          *(f32x4*)(nstage_f + p * 8) = lo;
+          *(f32x4*)(nstage_f + p * 8 + 4) = hi;
         }
-        f32x4 s4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          if (p0 + i * PPW < g.n_parts) s4 += v[i];
-        for (int base = p0 + 16 * PPW; base < g.n_parts; base += PPW)   // M > 16 rows only
-          s4 += *(const f32x4*)(g.ssq_in + base * MP + 4 * quad);
-        for (int o = 1; o < PPW; o <<= 1) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) s4[j] += __shfl_xor(s4[j], o);
-        }
-        if (p0 == 0 && lane / PPW < QM) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) sm_r[4 * quad + j] = 1.0f / sqrtf(s4[j] / (float)(g.KT * 32) + g.eps);
-        }
-        // the norm weight and sm_r stores complete before the barrier releases the others
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
-      raw_barrier();  // #2: row scales and norm weight in LDS
-    } else {
-      raw_barrier();  // #1
-      // prologue: all D stages (the step-0 issue of stage D-1 would wait behind barrier #2;
-      // here it goes out with the rest and step 0 skips its issue)
-      [&]<int... I>(std::integer_sequence<int, I...>) {
-        (issue(std::integral_constant<int, I>{}, b + I * NW), ...);
-      }(std::make_integer_sequence<int, FULL_PROLOGUE ? D : D - 1>{});
-      // a barrier that does not drain vmcnt: __syncthreads() would first wait for every
-      // weight load just issued
-      raw_barrier();  // #2
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) rr[mt] = sm_r[mt * 16 + (lane & 15)];
     }
   } else if (nbw > 0) {
     // prologue: stages 0..D-2 (all D with FULL_PROLOGUE)
@@ -315,7 +343,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       ((PADDED || b + I * NW < nb ? issue(std::integral_constant<int, I>{}, b + I * NW) : void()), ...);
     }(std::make_integer_sequence<int, FULL_PROLOGUE ? D : D - 1>{});
   }
-  if (nbw > 0 && (!dn_norm_wave<NORM>() || wave < NW)) {
+  if (nbw > 0) {
     // one step: issue the batch D-1 steps ahead into the slot this step's predecessor freed,
     // then consume slot d.  With FULL_PROLOGUE the first step's issue went out with the
     // prologue, so that step is peeled (no issue) and the loop runs the slots rotated by one
@@ -335,17 +363,19 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       if constexpr (NORM == DN_EXACT) {
 #pragma unroll
         for (int u = 0; u < TW; ++u) {
-          const int wo = (min(b, nb - 1) * TW + u) * 32 + 8 * (lane >> 4);
+          // steps past the wave's last batch (zeros from their loads) re-read its last batch's
+          // weight: finite, so 0 * w stays 0
+          const int wo = (min((b - swave) / NW, nbw - 1) * TW + u) * 32 + 8 * (lane >> 4);
           float wf[8];
           if constexpr (W_F32) {
-            const f32x4 w_lo = *(const f32x4*)(sm_w + wo), w_hi = *(const f32x4*)(sm_w + wo + 4);
+            const f32x4 w_lo = *(const f32x4*)(nstage_f + wo), w_hi = *(const f32x4*)(nstage_f + wo + 4);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               wf[j] = w_lo[j];
               wf[4 + j] = w_hi[j];
             }
           } else {
-            const u16x8 nv = *(const u16x8*)(sm_wb + wo);
+            const u16x8 nv = *(const u16x8*)(nstage + wo);
 #pragma unroll
             for (int j = 0; j < 8; ++j) wf[j] = bf2f(nv[j]);
           }
@@ -386,7 +416,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       }
     }
   }
-  if (!dn_norm_wave<NORM>() || wave < NW) {
+  {
 #pragma unroll
     for (int s = 0; s < S; ++s)
 #pragma unroll
@@ -416,6 +446,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
     }
     return;
   }
+  float qr[4] = {0.f, 0.f, 0.f, 0.f};  // EPI_RESID: the tile's sums of squares of rows 4(ln/16)+r
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = mt * 16 + 4 * (ln >> 4) + r;
@@ -436,10 +467,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
       const bool live = row < M;
       const u16 ob = live ? f2bf(rbf(v[0][r]) + bf2f(rpre[r])) : (u16)0;
       if (live) g.C[(g.pack & GEMM_PACK_C) ? packed_index(row, col, g.ldc) : (int64_t)row * g.ldc + col] = ob;
-      if (g.ssq_out) {
-        const float q = row16_sum(bf2f(ob) * bf2f(ob));
-        if (live && (ln & 15) == 0) g.ssq_out[nt * ((M + 3) & ~3) + row] = q;
-      }
+      if (g.ssq_out) qr[r] = row16_sum(bf2f(ob) * bf2f(ob));
     } else if (row < M) {
       float o;
       if constexpr (EPI == EPI_NONE) {
@@ -450,6 +478,23 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
         o = 0.f;  // EPI_PARTIAL returns above
       }
       g.C[(g.pack & GEMM_PACK_C) ? packed_index(row, col, g.ldc) : (int64_t)row * g.ldc + col] = f2bf(o);
+    }
+  }
+  if constexpr (EPI == EPI_RESID) {
+    if (g.ssq_out) {
+      // lane i < 32 takes row i % 16 (held by lanes 16(i%16 / 4) .. as qr[i % 4]) and adds its hi
+      // (i < 16) or lo word to shard nt % SSQ_SHARDS: slot [shard][hi | lo][64 rows]
+      const int i = ln & 15;
+      float qv = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t = __shfl(qr[r], 16 * (i >> 2));
+        if ((i & 3) == r) qv = t;
+      }
+      const int row = mt * 16 + i;
+      if (ln < 32 && row < M)
+        __hip_atomic_fetch_add(g.ssq_out + (nt % SSQ_SHARDS) * 128 + (ln >> 4) * 64 + row, ssq_fixed(qv, ln >= 16),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -470,18 +515,18 @@ static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   if (a.pack & GEMM_PACK_A) {
     if (a.KT % C::TW == 0)
       hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, true>), dim3(a.n_tiles), dim3(T),
-                         (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+                         (dn_lds_bytes<NORM, S, C::NW, C::TW, MT>(a.KT)), s, a);
     else
       hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM, true>), dim3(a.n_tiles), dim3(T),
-                         (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+                         (dn_lds_bytes<NORM, S, C::NW, 1, MT>(a.KT)), s, a);
     return;
   }
   if (a.KT % C::TW == 0)
     hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM>), dim3(a.n_tiles), dim3(T),
-                       (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+                       (dn_lds_bytes<NORM, S, C::NW, C::TW, MT>(a.KT)), s, a);
   else  // odd K/32 (single-op API only; every Qwen3 projection has K % 128 == 0)
     hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, 1, 2, EPI, NORM>), dim3(a.n_tiles), dim3(T),
-                       (dn_lds_bytes<NORM, S>(a.KT)), s, a);
+                       (dn_lds_bytes<NORM, S, C::NW, 1, MT>(a.KT)), s, a);
 }
 
 template <int EPI, int NORM>
@@ -499,7 +544,7 @@ static void decode_mt(const DecodeArgs& a, hipStream_t s) {
 // q/k/v projection of a decode step with K split over `kslices` workgroup slices and the
 // reduction left to the consumer (launch_attn_decode_fused): with NW = 4 the 384 x 2
 // workgroups of Qwen3-8B sit 3 per CU, every CU streaming the same bytes.  `norm` selects
-// the RMSNorm mode: DN_EXACT (ssq_in / n_parts / norm_w) or none.
+// the RMSNorm mode: DN_EXACT (ssq slot / norm_w) or none.
 void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, int kslices,
                                 float* part, const DecodeNorm& norm, hipStream_t s, int pack) {
   DecodeArgs a = {};
@@ -512,17 +557,16 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
   a.eps = norm.eps;
   a.part = part;
   a.ldp = N;
-  a.ssq_in = norm.ssq_in;
-  a.n_parts = norm.n_parts;
+  a.ssq_in = norm.ssq;
   a.norm_w = norm.w;
   a.pack = pack;
   const dim3 grid(N / 16, kslices);
   if (norm.mode == DN_EXACT && (pack & GEMM_PACK_A))
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT, true>), grid,
-                       dim3(decode_threads<4, DN_EXACT>()), (dn_lds_bytes<DN_EXACT, 1>(a.KT / kslices)), s, a);
+                       dim3(decode_threads<4, DN_EXACT>()), (dn_lds_bytes<DN_EXACT, 1, 4, 4, 1>(a.KT / kslices)), s, a);
   else if (norm.mode == DN_EXACT)
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_EXACT>), grid,
-                       dim3(decode_threads<4, DN_EXACT>()), (dn_lds_bytes<DN_EXACT, 1>(a.KT / kslices)), s, a);
+                       dim3(decode_threads<4, DN_EXACT>()), (dn_lds_bytes<DN_EXACT, 1, 4, 4, 1>(a.KT / kslices)), s, a);
   else
     hipLaunchKernelGGL((gemm_decode_kernel<1, 1, 4, 4, 3, EPI_PARTIAL, DN_NONE>), grid, dim3(256), 0, s, a);
 }
@@ -1445,7 +1489,7 @@ bool gemm_uses_tiled(int M, int N, int K, int epi) {
 
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s, const GemmWs* ws,
-                 const DecodeNorm* dn, float* ssq_out, int pack) {
+                 const DecodeNorm* dn, unsigned long long* ssq_out, int pack) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
   const bool tiled = gemm_uses_tiled(M, N, K, epi);
@@ -1516,8 +1560,7 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     a.ssq_out = (epi == EPI_RESID) ? ssq_out : nullptr;
     a.pack = pack;
     if (mode == DN_EXACT) {
-      a.ssq_in = dn->ssq_in;
-      a.n_parts = dn->n_parts;
+      a.ssq_in = dn->ssq;
       a.norm_w = dn->w;
       switch (epi) {
         case EPI_NONE: decode_mt<EPI_NONE, DN_EXACT>(a, s); break;

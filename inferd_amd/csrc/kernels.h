@@ -35,8 +35,10 @@ struct QkvEpilogue {
 void launch_weightgen(u16* dst, int64_t n, uint64_t key, float scale, float center, hipStream_t s);
 void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s);
 void launch_unpack(const u16* src, int N, int K, u16* dst, hipStream_t s);
+// zero_slots: rows < M of n_slots SSQ slots (kernels.h DecodeNorm) are zeroed too, or null
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
-                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out = false);
+                    u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out = false,
+                    unsigned long long* zero_slots = nullptr, int n_slots = 0);
 void launch_rope_table(const float* inv_freq, int max_pos, u16* cos_t, u16* sin_t, hipStream_t s);
 void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positions,
                             const int32_t* slots, const u16* qn_w, const u16* kn_w,
@@ -55,15 +57,19 @@ bool gemm_uses_tiled(int M, int N, int K, int epi);
 // RMSNorm modes of the decode (M <= 64) GEMV
 enum { DN_NONE = 0, DN_EXACT = 2 };
 // DN_EXACT: Qwen3RMSNorm at the reference's rounding points applied to A inside the GEMV,
-// A' = bf16(w * bf16(A * r)), r = 1 / sqrt(sum_p ssq_in[p * MP + row] / K + eps) (MP = M rounded
-// up to a multiple of 4: compact parts, so a wave's loads cover whole cache lines): the row sums
-// of squares come from the kernel that produced A (launch_gemm's ssq_out on an EPI_RESID
-// GEMV, one partial per 16-column tile, n_parts = K / 16)
+// A' = bf16(w * bf16(A * r)), r = 1 / sqrt(ssq[row] / K + eps).  ssq[row] comes from the kernel
+// that produced A (launch_gemm's ssq_out on an EPI_RESID GEMV) as an exact fixed-point sum in one
+// SSQ slot: each producer workgroup adds its 16-column tile's fp32 row sums of squares, split into
+// hi = floor(q * 2^8) and lo = frac(q * 2^8) * 2^32, to shard (tile % SSQ_SHARDS) with no-return
+// 64-bit atomics; integer adds commute, so the sum is order-independent (deterministic) and exact
+// to 2^-40.  Slot layout: [SSQ_SHARDS][hi | lo][64 rows] u64; a slot must be zero before its
+// producer runs (launch_rmsnorm's `zero_slots`).
+#define SSQ_SHARDS 8
+#define SSQ_SLOT_WORDS (SSQ_SHARDS * 64 * 2)
 struct DecodeNorm {
   int mode;
   float eps;
-  const float* ssq_in;
-  int n_parts;
+  const unsigned long long* ssq;  // the slot the producer of A filled
   const u16* w;
 };
 // Per-span GEMM workspace: the prefill tail split's fp32 partials and tickets, allocated once
@@ -78,11 +84,12 @@ struct GemmWs {
 };
 int gemm_ws_alloc(GemmWs* w);  // hipError_t as int
 void gemm_ws_free(GemmWs* w);
-// ssq_out (EPI_RESID, M <= 64): per 16-column tile sums of squares of the stored outputs,
-// [N/16][64] floats -- the DecodeNorm input of the next normed GEMV.
+// ssq_out (EPI_RESID, M <= 64): the SSQ slot (above) that receives the row sums of squares of
+// the stored outputs -- the DecodeNorm input of the next normed GEMV.
 void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
-                 const GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr, float* ssq_out = nullptr, int pack = 0);
+                 const GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr, unsigned long long* ssq_out = nullptr,
+                 int pack = 0);
 // launch_gemm `pack` bits (decode path, M <= 64 only; common.h packed_index): A is read
 // fragment-packed / the EPI_SILU or EPI_RESID output C is written so / the EPI_RESID residual
 // R is read so

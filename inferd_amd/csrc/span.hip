@@ -126,12 +126,12 @@ struct InferdSpan {
   size_t attn_ws_bytes = 0;
   Knobs knobs;
   // RMSNorms at the reference's rounding points (qwen3_server_module.py:19-25).  On the decode
-  // GEMV path (<= 64 rows) the o and down GEMVs write per-tile row sums of squares of their
-  // outputs (ssq_post / ssq_in, [hidden/16][MP], MP = rows rounded up to 4, <= 64), and the
-  // gate/up and next layer's q/k/v GEMVs normalise their A fragments from them; otherwise (a
+  // GEMV path (<= 64 rows) the o and down GEMVs add the row sums of squares of their outputs
+  // into SSQ slots (kernels.h DecodeNorm; slot 2l: layer l's o -> its gate/up, slot 2l+1: layer
+  // l's down -> layer l+1's q/k/v), and those GEMVs normalise their A fragments from them; the
+  // layer-0 rmsnorm_kernel zeroes the slots at the start of each such forward.  Otherwise (a
   // span's first layer, prefill) rmsnorm_kernel writes the normed rows to xn.
-  float* ssq_in = nullptr;
-  float* ssq_post = nullptr;
+  unsigned long long* ssq = nullptr;
   GemmWs gws;                 // prefill tail-split workspace (per span: spans never share tickets)
   float* qkv_part = nullptr;  // decode split-K q/k/v partials [QKV_KSL_MAX][16][qkv_rows]
   unsigned long long* argmax_partial = nullptr;
@@ -258,8 +258,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
-  SALLOC(s->ssq_in, (size_t)(h / 16) * 64 * 4);
-  SALLOC(s->ssq_post, (size_t)(h / 16) * 64 * 4);
+  SALLOC(s->ssq, (size_t)(2 * c.n_layers + 1) * SSQ_SLOT_WORDS * 8);
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
   SALLOC(s->qkv_part, (size_t)QKV_KSL_MAX * 16 * s->qkv_rows() * 4);
   // the prefill tail split's workspace, once (a forward never allocates): only spans whose
@@ -445,12 +444,18 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   // projection of this call is a decode GEMV (<= 64 rows), so the o / down GEMVs can hand the
   // next norm its row sums of squares.
   const bool gemv = M <= 64;
-  const int n_parts = h / 16;
+  auto slot = [&](int i) { return s->ssq + (size_t)i * SSQ_SLOT_WORDS; };
   // decode: the residual stream between layers (and h1 inside a layer) fragment-packed
   // (common.h packed_index) for the GEMVs that read it; the input and the last layer's
   // output stay row-major, and so does every layer's output when layer_out asks for them
   const bool pkx = gemv && kn.pack_act && !layer_out && h % 128 == 0 && I % 128 == 0;
   bool x_packed = false;  // x (this layer's input) is fragment-packed
+  // decode on the last span without x_out: the last layer's down GEMV hands the final norm its row
+  // sums of squares (SSQ slot 2 n_layers - 1) and the lm_head GEMV normalises exactly like the
+  // q/k/v and gate/up GEMVs (one row per sequence, so the rows are the last rows); the last
+  // layer's output then stays fragment-packed for it
+  const bool fold_final = gemv && b->decode && c.has_lm_head && c.n_layers > 0 && !x_out && !layer_out &&
+                          (next_ids || logits) && B <= 64;
   long pe = -1;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
@@ -462,12 +467,13 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     if ((h / 32) % (4 * ksl)) ksl = 1;
     // ---- input_layernorm -> q/k/v projection
     const u16* a_in = x;
-    DecodeNorm dn = {DN_NONE, c.rms_eps, nullptr, 0, nullptr};
+    DecodeNorm dn = {DN_NONE, c.rms_eps, nullptr, nullptr};
     if (gemv && l > 0) {
-      dn = {DN_EXACT, c.rms_eps, s->ssq_in, n_parts, W.in_ln};
+      dn = {DN_EXACT, c.rms_eps, slot(2 * l - 1), W.in_ln};
     } else {
       pe = s->prof_begin(PROF_NORM, st);
-      launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st);
+      launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st, false, gemv ? s->ssq : nullptr,
+                     2 * c.n_layers);
       s->prof_end(pe, st);
       a_in = s->xn;
     }
@@ -520,18 +526,18 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // span's embedding output) or is to receive this layer's row-major output (the last layer
     // without x_out).
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
-    const bool out_packed = pkx && l < c.n_layers - 1;
+    const bool out_packed = pkx && (l < c.n_layers - 1 || fold_final);
     u16* h1 = (pkx && ((x == s->h && !x_packed) || (out == s->h && !out_packed))) ? s->xn : s->h;
     pe = s->prof_begin(PROF_O, st);
     launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
-                gemv ? s->ssq_post : nullptr,
+                gemv ? slot(2 * l) : nullptr,
                 (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (pkx ? GEMM_PACK_C : 0));
     s->prof_end(pe, st);
     // ---- post_attention_layernorm -> gate/up (+SwiGLU)
     const u16* m_in = h1;
-    DecodeNorm dm = {DN_NONE, c.rms_eps, nullptr, 0, nullptr};
+    DecodeNorm dm = {DN_NONE, c.rms_eps, nullptr, nullptr};
     if (gemv) {
-      dm = {DN_EXACT, c.rms_eps, s->ssq_post, n_parts, W.post_ln};
+      dm = {DN_EXACT, c.rms_eps, slot(2 * l), W.post_ln};
     } else {
       pe = s->prof_begin(PROF_NORM, st);
       launch_rmsnorm(h1, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st);
@@ -548,7 +554,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // ---- x = h1 + down(act)
     pe = s->prof_begin(PROF_DOWN, st);
     launch_gemm(s->act, I, W.down, M, h, I, out, h, h1, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
-                gemv ? s->ssq_in : nullptr,
+                (gemv && (l + 1 < c.n_layers || fold_final)) ? slot(2 * l + 1) : nullptr,
                 (pk ? GEMM_PACK_A : 0) | (pkx ? GEMM_PACK_R : 0) | (out_packed ? GEMM_PACK_C : 0));
     s->prof_end(pe, st);
     x = out;
@@ -564,10 +570,16 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pe = s->prof_begin(PROF_LMHEAD, st);
     // the normed last rows go to the lm_head GEMV fragment-packed (its A operand only; the
     // logits it may also store stay row-major)
-    const bool pk_last = kn.pack_act && h % 32 == 0;
-    launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st, pk_last);
-    launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
-                s->argmax_partial, st, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0);
+    if (fold_final) {
+      const DecodeNorm dl = {DN_EXACT, c.rms_eps, slot(2 * c.n_layers - 1), s->final_norm};
+      launch_gemm(x, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX, s->argmax_partial,
+                  st, nullptr, &dl, nullptr, x_packed ? GEMM_PACK_A : 0);
+    } else {
+      const bool pk_last = kn.pack_act && h % 32 == 0;
+      launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st, pk_last);
+      launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
+                  s->argmax_partial, st, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0);
+    }
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
     s->prof_end(pe, st);
   }

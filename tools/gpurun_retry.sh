@@ -1,0 +1,17 @@
+#!/bin/bash
+# Submit one gpurun call; resubmit ONLY while the pool reports no free slot/box (nothing ran,
+# nothing charged: exit code 3 or a "busy ... nothing was charged" message).  A call that ran
+# (any outcome, including a failed or timed-out GPU step) is never resubmitted.
+# usage: tools/gpurun_retry.sh <log> <timeout_s> '<command>'
+log=$1; to=$2; cmd=$3
+for i in $(seq 1 20); do
+  /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
+  rc=$?
+  if [ $rc -eq 3 ] || { grep -q "nothing was charged" "$log" && grep -q -i "busy\|no box\|no free" "$log"; }; then
+    echo "[retry $i] no slot (rc=$rc), waiting" >> "$log.retries"
+    sleep 150
+    continue
+  fi
+  exit $rc
+done
+exit 3
