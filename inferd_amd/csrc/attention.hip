@@ -837,6 +837,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
 
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
                          hipStream_t s) {
+  if (b.pfk == 1 && launch_attn_prefill_w64(q, kv_layer, b, H, KV, scale, out, s)) return;
   const int n = (b.max_q_len + 127) / 128 * H;
   const int order = b.order >= 0 ? b.order : (n % 8 == 0 ? 1 : 0);  // the span's INFERD_ATTN_ORDER
   hipLaunchKernelGGL(attn_prefill_kernel, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out,

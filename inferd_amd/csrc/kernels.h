@@ -121,6 +121,8 @@ struct AttnBatch {
   // decode waves per workgroup / chunks per (sequence, kv head), per-lane q loads instead of
   // the staged q image, prefill block order (-1 default, 0 head-major, 1 XCD-grouped)
   int nw = 0, nc = 0, qlanes = 0, order = -1;
+  // prefill kernel: 1 = the one-wave-per-SIMD body (attn_prefill.hip), 0 = attn_prefill_kernel
+  int pfk = 0;
 };
 // q [M][H][128] bf16 -> out [M][H*128] bf16.  kv_layer: this layer's pool base.
 void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
@@ -138,6 +140,9 @@ void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, co
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx);
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
                          float scale, u16* out, hipStream_t s);
+// attn_prefill.hip; false (nothing launched) if the kernel cannot get its 128 KiB of LDS
+bool launch_attn_prefill_w64(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale,
+                             u16* out, hipStream_t s);
 
 // sets the thread-local message of inferd_last_error() and returns `code` (span.hip)
 int inferd_fail(int code, const std::string& msg);

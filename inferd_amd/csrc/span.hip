@@ -85,6 +85,7 @@ struct Knobs {
   int attn_nw = 0, attn_nc = 0;  // INFERD_ATTN_NW / _NC: decode attention shape (0: default)
   int attn_qlanes = 0;           // INFERD_ATTN_QLANES=1: per-lane q loads in the fused decode attention
   int attn_order = -1;           // INFERD_ATTN_ORDER: prefill block order (-1: default)
+  int attn_prefill = 0;          // INFERD_ATTN_PREFILL: 1 = one-wave-per-SIMD prefill attention
 };
 
 int env_int(const char* name, int dflt) {
@@ -104,6 +105,7 @@ Knobs knobs_from_env() {
   k.attn_nc = env_int("INFERD_ATTN_NC", 0);
   k.attn_qlanes = env_int("INFERD_ATTN_QLANES", 0);
   k.attn_order = env_int("INFERD_ATTN_ORDER", -1);
+  k.attn_prefill = env_int("INFERD_ATTN_PREFILL", 0);
   return k;
 }
 
@@ -403,6 +405,7 @@ static AttnBatch to_attn(const InferdBatch* b, const Knobs& kn = Knobs{}) {
   a.nc = kn.attn_nc;
   a.qlanes = kn.attn_qlanes;
   a.order = kn.attn_order;
+  a.pfk = kn.attn_prefill;
   a.seq_start = b->seq_start;
   a.positions = b->positions;
   a.ctx_lens = b->ctx_lens;
@@ -796,7 +799,7 @@ extern "C" int64_t inferd_attention_workspace_bytes(int32_t n_seqs, int32_t head
 extern "C" int inferd_attention(const void* q, const void* kv_layer, const InferdBatch* b, int32_t H,
                                 int32_t KV, void* out, void* ws, int64_t ws_bytes, void* stream) {
   if (!q || !kv_layer || !b || !out || KV <= 0 || H % KV || H / KV > 16) return fail(INFERD_ERR_ARG, "bad attention args");
-  const AttnBatch ab = to_attn(b);
+  const AttnBatch ab = to_attn(b, knobs_from_env());  // single-op API (tests, labs): env read per call
   const float scale = 1.0f / sqrtf((float)HEAD_DIM);
   if (b->decode) {
     if (!ws || ws_bytes < (int64_t)attn_decode_ws_bytes(b->n_seqs, H, b->max_ctx_len))

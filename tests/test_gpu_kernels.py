@@ -280,11 +280,15 @@ def test_attention_decode(lib, H, KV):
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
 
 
+@pytest.mark.parametrize("pfk", [0, 1])
 @pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2), (64, 8)])
-def test_attention_prefill(lib, H, KV):
-    """The 4-wave prefill kernel on ragged prompts, with and without cached prefixes,
-    including a 700-token prompt (several 128-row blocks, > 4 pages)."""
-    err, ref = _attn_case(lib, H, KV, [1, 17, 64, 130, 700], [0, 5, 0, 200, 61], seed=H + 1)
+def test_attention_prefill(lib, monkeypatch, H, KV, pfk):
+    """Both prefill kernels (INFERD_ATTN_PREFILL=0: 4-wave attn_prefill_kernel, 1: the
+    one-wave-per-SIMD attn_prefill.hip) on ragged prompts, with and without cached prefixes:
+    a 700-token prompt (several 128-row blocks, > 4 pages) and a 1000-token prompt behind 300
+    cached tokens (several 256-row blocks, masks on pages that start mid-block)."""
+    monkeypatch.setenv("INFERD_ATTN_PREFILL", str(pfk))
+    err, ref = _attn_case(lib, H, KV, [1, 17, 64, 130, 700, 1000], [0, 5, 0, 200, 61, 300], seed=H + 1)
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
 
 
