@@ -66,9 +66,7 @@ constexpr int frag_c(int f) { return AP_SORD ? (f >> 1) : (f & 7); }
 constexpr int NA = 42;        // softmax values (of a lane's 64 per page) finished in phase A
 constexpr float THR = 8.0f;   // lazy rescale threshold, log2 units (attention.hip RESCALE_THR)
 constexpr int PAGE_BYTES = 32768;
-constexpr int NBUF = 4;  // page j in buffer j % 4, issued 3 pages ahead
-constexpr int BT_OFF = NBUF * PAGE_BYTES;  // the workgroup's block-table row in LDS (<= BT_MAX pages)
-constexpr int BT_MAX = 4096;
+constexpr int NBUF = 5;  // page j in buffer j % 5: DMA issued 4 pages (2 iterations of slack) ahead
 
 // ---- fixed schedule (global slot g: 0..31 phase A, 32..63 phase B) --------------------------
 // softmax value v of a lane: tile tb = v >> 5, query block nq = (v >> 4) & 1, register v & 15
@@ -80,35 +78,27 @@ constexpr int fslot(int v) { return v < NA ? v * 32 / NA : 32 + (v - NA) / 2; }
 // page i+1 (f >= 3) at phase-A slot 2f - 6, three slots of MFMAs ahead of its first use (slot 2f);
 // V(kk, db) of page i ahead of its P.V slice; K fragments 0..2 of page i+2 at the end of phase B
 // (the next phase A starts on them).  K lives in a KR-fragment AGPR ring (fragment f in kr[f % KR]).
-constexpr int kslot(int f) { return f >= 3 ? 2 * f - 6 : f - 3; }  // f < 3: the previous iteration's 61..63
+constexpr int kslot(int f) { return f >= 3 ? 2 * f - 6 : 49 + 2 * f; }  // f < 3: page i+2, early enough to land before phase B ends
 // V(kk, db) four slots ahead of its first P.V MFMA (slot 32 + 8kk + 2db): three fragments live
 constexpr int vslot(int kk, int db) { return 28 + 8 * kk + 2 * db; }
 constexpr int KR = 6;  // K ring: fragment f in kr[f % KR], read 6 slots before use, its predecessor
                        // f - KR last used 5 slots before that read
-// Iteration boundary inside phase A (no drain, no idle MFMA pipe between pages): slot 1 reads the
-// block-table entry of page i+3 from LDS, slot 8 waits for this wave's DMA of page i+2 and meets
-// the other waves at the page barrier (their reads of page i-1's buffer are complete: every read
-// up to slot 0 has been waited for), slots 9 and 11 issue the DMA of page i+3 into that buffer.
-constexpr int BT_SLOT = 1, BAR_SLOT = 8, DMA_SLOT0 = 9, DMA_SLOT1 = 11;
-constexpr int reads_in(int g) {  // slots -3 .. 63 (-3..-1: the previous iteration's 61..63)
+constexpr int reads_in(int g) {
   int n = 0;
   for (int kk = 0; kk < 4; ++kk)
     for (int db = 0; db < 4; ++db) n += vslot(kk, db) == g;
   for (int f = 0; f < 16; ++f) n += kslot(f) == g;
-  for (int f = 0; f < 3; ++f) n += 61 + f == g;
-  n += g == BT_SLOT;
   return n;
 }
 constexpr int reads_before(int g) {
   int n = 0;
-  for (int x = -3; x < g; ++x) n += reads_in(x);
+  for (int x = 0; x < g; ++x) n += reads_in(x);
   return n;
 }
 // lgkmcnt before the MFMA of slot g that first consumes the read issued in slot rs: the reads
 // issued after it (a slot's read follows its MFMA)
 constexpr int rd_wait(int g, int rs) { return reads_before(g) - reads_before(rs) - 1; }
-static_assert(reads_in(0) == 1 && reads_in(1) == 1 && reads_in(28) == 1 && reads_in(61) == 1 && reads_in(-1) == 1,
-              "one read per slot");
+static_assert(reads_in(0) == 1 && reads_in(28) == 1 && reads_in(49) == 1 && reads_in(48) == 1, "one read per slot");
 // byte offsets of the reads from the lane's base in a page buffer
 constexpr int koff(int tb, int c) { return tb * 8192 + (c >> 1) * 1024 + (c & 1) * 512; }
 constexpr int voff(int kk, int db) { return 16384 + (kk >> 1) * 8192 + db * 2048 + (kk & 1) * 512; }
@@ -120,7 +110,7 @@ __device__ __forceinline__ void mfma_s(f32x16& d, const bf16x8& a, const bf16x8&
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "a"(a), "a"(b));
 }
 __device__ __forceinline__ void mfma_o(f32x16& d, const bf16x8& a, const u32x4v& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(d) : "a"(a), "v"(b));
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
 }
 template <int OFF>
 __device__ __forceinline__ void rd_a(bf16x8& d, unsigned addr) {
@@ -273,13 +263,29 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
     stage_half(page, phys, 0);
     stage_half(page, phys, 1);
   };
-  // this wave's DMA of page i+2 (issued an iteration ago) has landed; the page barrier
-  auto page_barrier = [&](int i) AI {
-    if constexpr (AP_PROBE != 2) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  // The page boundary of iteration i, inside phase A (MFMAs keep the matrix pipe busy around it):
+  // part 0 (slot 8): page i+2 landed (this wave's pieces, issued two iterations ago) and every wave
+  // is done with page i-1's buffer (its reads were all waited for by slot 0); parts 1, 2 (slots 9,
+  // 11): refill that buffer with page i+4, then prefetch the next block-table entry (after the
+  // use of the previous one: SMEM returns out of order, so waiting for the old entry would wait for
+  // the new load too).  Block-table entries alternate between two variables, one per half of the
+  // two-iteration loop body (no register rotation: hipcc waits for a load only where it is used).
+  int physv[2] = {0, 0};
+  // (branch-free inside the phase -- a branch there split the slots and hipcc spilled: past the
+  // last page the entry is clamped and the DMA re-stages the last page into page i-1's free buffer,
+  // so DMA(i+3) is always in flight and vmcnt(8) always leaves exactly it)
+  auto page_barrier_dma = [&](int i, int part) AI {
+    if (part == 0) {
+      if constexpr (AP_PROBE != 2) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      return;
+    }
+    if constexpr (AP_NODMA) return;
+    const int cur = i & 1;
+    stage_half(i + 4, physv[cur], part - 1);
+    if (part == 2) physv[cur ^ 1] = bt[min(i + 5, n_pages - 1)];
   };
   // per-lane read bases (LDS byte addresses) within a page buffer
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_ptr)lds;
-  const unsigned bt_lds = lds0 + BT_OFF;  // block-table row (ds_read_b32 per page)
   const int tk = tau(r);
   const unsigned lane_k = (tk >> 4) * 4096 + ((tk & 15) + 16 * hh) * 16;
   const unsigned lane_v = (r >> 4) * 1024 + ((r & 15) + 16 * hh) * 16;
@@ -374,7 +380,6 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
   // ---- phase A_i: S_{i+1} MFMAs || softmax of page i || K_{i+1} and V_i slice-0 reads
   auto phase_a = [&]<int CUR, bool NEXT>(int page, u32x4v (&pf)[2][4]) AI {
     constexpr int NXT = CUR ^ 1;
-    int bt_e = 0;
     mneg[0] = -m[0];
     mneg[1] = -m[1];
     const unsigned va = vbase(page), ka = kbase(page + 1);
@@ -383,7 +388,7 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
           [&]() AI {
             constexpr int f = G >> 1, tb = frag_tb(f), c = frag_c(f), nq = G & 1;
             if constexpr (NEXT) {
-              if constexpr ((G & 1) == 0) lgkm_wait_a<rd_wait(G, kslot(f))>(kr[f % KR]);
+              if constexpr (f >= 3 && (G & 1) == 0) lgkm_wait_a<rd_wait(G, kslot(f))>(kr[f % KR]);
               if constexpr (c == 0)
                 mfma_s0(s[NXT][nq][tb], kr[f % KR], qf[nq][c]);
               else
@@ -394,17 +399,10 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
               constexpr int fr = G / 2 + 3;
               rd_a<koff(frag_tb(fr), frag_c(fr))>(kr[fr % KR], ka);
             }
-            if constexpr (AP_PROBE != 3 && G >= 28 && (G & 1) == 0) rd_a<voff(0, (G - 28) / 2)>(vf[0][(G - 28) / 2], va);
-            // (branch-free: past the last page the entry is clamped and the DMA re-stages the last
-            // page into page i-1's free buffer; a branch here split the slots and hipcc spilled)
-            if constexpr (G == BT_SLOT) rd_b32(bt_e, bt_lds + min(page + 3, n_pages - 1) * 4);
-            if constexpr (G == BAR_SLOT) page_barrier(page);
-            if constexpr (G == DMA_SLOT0) {
-              lgkm_wait_i<rd_wait(DMA_SLOT0, BT_SLOT)>(bt_e);
-              if constexpr (!AP_NODMA) stage_half(page + 3, __builtin_amdgcn_readfirstlane(bt_e), 0);
-            }
-            if constexpr (G == DMA_SLOT1)
-              if constexpr (!AP_NODMA) stage_half(page + 3, __builtin_amdgcn_readfirstlane(bt_e), 1);
+            if constexpr (AP_PROBE != 3 && G >= 28 && (G & 1) == 0) rd_v<voff(0, (G - 28) / 2)>(vf[0][(G - 28) / 2], va);
+            if constexpr (G == 8) page_barrier_dma(page, 0);
+            if constexpr (G == 9) page_barrier_dma(page, 1);
+            if constexpr (G == 11) page_barrier_dma(page, 2);
             SLOT_END();
           }(),
           ...);
@@ -420,7 +418,7 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
           [&]() AI {
             constexpr int G = 32 + K;
             constexpr int kk = K >> 3, db = (K >> 1) & 3, nq = K & 1;
-            if constexpr ((K & 1) == 0) lgkm_wait_a<rd_wait(G, vslot(kk, db))>(vf[kk][db]);
+            if constexpr ((K & 1) == 0) lgkm_wait<rd_wait(G, vslot(kk, db))>(vf[kk][db]);
             mfma_o(o[db][nq], vf[kk][db], pf[nq][kk]);
             soft.template operator()<G, CUR>(pf);
             // row max of S_{i+1}: chains (nq, tb), 8 max3 steps each, slots 44..59
@@ -456,15 +454,18 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
               (
                   [&]() AI {
                     constexpr int rk = R >> 2, rd = R & 3;
-                    if constexpr (AP_PROBE != 3 && vslot(rk, rd) == G) rd_a<voff(rk, rd)>(vf[rk][rd], va);
+                    if constexpr (AP_PROBE != 3 && vslot(rk, rd) == G) rd_v<voff(rk, rd)>(vf[rk][rd], va);
                   }(),
                   ...);
             }(std::make_integer_sequence<int, 16>{});
-            if constexpr (AP_PROBE != 3 && NEXT && G >= 61) rd_a<koff(frag_tb(G - 61), frag_c(G - 61))>(kr[G - 61], ka);
+            [&]<int... F>(std::integer_sequence<int, F...>) AI {
+              ((AP_PROBE != 3 && NEXT && kslot(F) == G ? rd_a<koff(frag_tb(F), frag_c(F))>(kr[F], ka) : void()), ...);
+            }(std::make_integer_sequence<int, 3>{});
             SLOT_END();
           }(),
           ...);
     }(std::make_integer_sequence<int, 32>{});
+    lgkm_drain();
   };
   // S of one page, plain (prologue): K fragments through the ring in quarters, 32 MFMAs
   auto s_quarter = [&]<int SET, int QF>(unsigned ka) AI {
@@ -498,15 +499,21 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
     lgkm_drain();
   };
 
-  // ---- prologue: the block-table row to LDS, pages 0..2 in flight, S_0, its max, K_1
-  for (int pi = threadIdx.x; pi < n_pages; pi += 256) *(int*)(lds + BT_OFF + pi * 4) = b.block_table[(int64_t)bseq * b.max_pages + pi];
+  // ---- prologue: pages 0..3 in flight, S_0, its max, K_1.  Iteration i issues DMA(i+4) (8 pieces
+  // per wave), so at the top of iteration i+1, vmcnt(8) leaves only that one in flight: DMA(i+3),
+  // needed from phase B_{i+1} on, has landed.  Block-table entries by scalar loads one iteration
+  // ahead, alternating between two variables (one per half of the two-iteration loop body: no
+  // register rotation, so hipcc waits for the load only where the next iteration uses it; a single
+  // rotated variable made it wait in front of the DMA)
   stage(0, bt[0]);
   if (n_pages > 1) stage(1, bt[1]);
   if (n_pages > 2) stage(2, bt[2]);
-  if (n_pages > 2)
-    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");  // pages 0 and 1 landed (this wave's pieces)
+  if (n_pages > 3) stage(3, bt[3]);
+  physv[0] = bt[min(4, n_pages - 1)];
+  if (n_pages > 3)
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // pages 0 and 1 landed (this wave's pieces)
   else
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   asm volatile("s_barrier" ::: "memory");
   if (wave_last_page >= 0) {
     s_page.template operator()<0>(0);
@@ -531,13 +538,10 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
   };
   auto iter = [&]<int CUR>(int i) AI {
     stamp(i, 0);
-    if (i > wave_last_page) {  // this wave is done: only the page boundary (barrier, DMA share)
-      int e = 0;
-      lgkm_drain();
-      rd_b32(e, bt_lds + min(i + 3, n_pages - 1) * 4);
-      lgkm_wait_i<0>(e);
-      page_barrier(i);
-      if (!AP_NODMA) stage(i + 3, __builtin_amdgcn_readfirstlane(e));
+    if (i > wave_last_page) {  // this wave is done with its pages: only the page boundary
+      page_barrier_dma(i, 0);
+      page_barrier_dma(i, 1);
+      page_barrier_dma(i, 2);
       return;
     }
     rescale();
@@ -595,16 +599,16 @@ static bool w64_lds_ok() {
   static int ok = -1;
   if (ok < 0)
     ok = hipFuncSetAttribute((const void*)attn_prefill_w64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             BT_OFF + BT_MAX * 4) == hipSuccess;
+                             NBUF * PAGE_BYTES) == hipSuccess;
   return ok == 1;
 }
 
 bool launch_attn_prefill_w64(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale,
                              u16* out, hipStream_t s) {
-  if (!w64_lds_ok() || b.max_pages > BT_MAX) return false;
+  if (!w64_lds_ok()) return false;
   const int n = (b.max_q_len + 255) / 256 * H;
   const int order = b.order >= 0 ? b.order : (n % 8 == 0 ? 1 : 0);
-  hipLaunchKernelGGL(attn_prefill_w64_kernel, dim3(n, b.B), dim3(256), BT_OFF + BT_MAX * 4, s, q, kv_layer, b, H, KV,
+  hipLaunchKernelGGL(attn_prefill_w64_kernel, dim3(n, b.B), dim3(256), NBUF * PAGE_BYTES, s, q, kv_layer, b, H, KV,
                      scale * 1.4426950408889634f, out, (order == 1 && n % 8 == 0) ? 1 : 0);
   return true;
 }
