@@ -5,7 +5,7 @@ written bytes = WRITE_SIZE * 1024; MI355X_MICROARCH.md §HBM).  Alongside each c
 algorithmic bytes of one launch (operands read once, output written once), so the ratio
 shows how much of the L2/MALL tile re-reading reaches HBM.
 
-  tools/pmc_prefill.sh   (on the GPU box) -> profiles/traffic_prefill_r01.json
+  tools/pmc_prefill.sh   (on the GPU box) -> profiles/traffic_prefill_rNN.json
 """
 import json
 import os
