@@ -736,7 +736,10 @@ __device__ __forceinline__ void tile_order_v(const SplitTail& st, int grid_m, in
       sidx = x * (st.tiles_per_xcd - st.full_per_xcd) + j / st.split;
     }
   }
-  constexpr int GM = 8;
+#ifndef W4_GM
+#define W4_GM 8
+#endif
+  constexpr int GM = W4_GM;  // lab builds vary it (tools/build_probes.sh)
   const int group = tile / (GM * grid_n);
   const int first_m = group * GM;
   const int gsz = min(grid_m - first_m, GM);

@@ -260,7 +260,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   s->attn_ws_bytes = attn_decode_ws_bytes(c.max_seqs, H, c.max_positions);
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
-  SALLOC(s->ssq, (size_t)(2 * c.n_layers + 1) * SSQ_SLOT_WORDS * 8);
+  SALLOC(s->ssq, (size_t)(2 * c.n_layers) * SSQ_SLOT_WORDS * 8);
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
   SALLOC(s->qkv_part, (size_t)QKV_KSL_MAX * 16 * s->qkv_rows() * 4);
   // the prefill tail split's workspace, once (a forward never allocates): only spans whose
@@ -453,12 +453,6 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   // output stay row-major, and so does every layer's output when layer_out asks for them
   const bool pkx = gemv && kn.pack_act && !layer_out && h % 128 == 0 && I % 128 == 0;
   bool x_packed = false;  // x (this layer's input) is fragment-packed
-  // decode on the last span without x_out: the last layer's down GEMV hands the final norm its row
-  // sums of squares (SSQ slot 2 n_layers - 1) and the lm_head GEMV normalises exactly like the
-  // q/k/v and gate/up GEMVs (one row per sequence, so the rows are the last rows); the last
-  // layer's output then stays fragment-packed for it
-  const bool fold_final = gemv && b->decode && c.has_lm_head && c.n_layers > 0 && !x_out && !layer_out &&
-                          (next_ids || logits) && B <= 64;
   long pe = -1;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
@@ -529,7 +523,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // span's embedding output) or is to receive this layer's row-major output (the last layer
     // without x_out).
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
-    const bool out_packed = pkx && (l < c.n_layers - 1 || fold_final);
+    const bool out_packed = pkx && l < c.n_layers - 1;
     u16* h1 = (pkx && ((x == s->h && !x_packed) || (out == s->h && !out_packed))) ? s->xn : s->h;
     pe = s->prof_begin(PROF_O, st);
     launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
@@ -557,7 +551,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // ---- x = h1 + down(act)
     pe = s->prof_begin(PROF_DOWN, st);
     launch_gemm(s->act, I, W.down, M, h, I, out, h, h1, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
-                (gemv && (l + 1 < c.n_layers || fold_final)) ? slot(2 * l + 1) : nullptr,
+                (gemv && l + 1 < c.n_layers) ? slot(2 * l + 1) : nullptr,
                 (pk ? GEMM_PACK_A : 0) | (pkx ? GEMM_PACK_R : 0) | (out_packed ? GEMM_PACK_C : 0));
     s->prof_end(pe, st);
     x = out;
@@ -571,18 +565,13 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     if (B > 64) return fail(INFERD_ERR_ARG, "lm_head argmax supports <= 64 sequences per call");
     // last row of each sequence: seq_start[b+1] - 1
     pe = s->prof_begin(PROF_LMHEAD, st);
-    // the normed last rows go to the lm_head GEMV fragment-packed (its A operand only; the
-    // logits it may also store stay row-major)
-    if (fold_final) {
-      const DecodeNorm dl = {DN_EXACT, c.rms_eps, slot(2 * c.n_layers - 1), s->final_norm};
-      launch_gemm(x, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX, s->argmax_partial,
-                  st, nullptr, &dl, nullptr, x_packed ? GEMM_PACK_A : 0);
-    } else {
-      const bool pk_last = kn.pack_act && h % 32 == 0;
-      launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st, pk_last);
-      launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
-                  s->argmax_partial, st, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0);
-    }
+    // the final norm writes the last rows fragment-packed for the lm_head GEMV (its A operand
+    // only; the logits it may also store stay row-major).  Folding this norm into the GEMV's A
+    // path (DN_EXACT, as q/k/v) measured 213.8 us in the graph against 195 + 5 us (round 3).
+    const bool pk_last = kn.pack_act && h % 32 == 0;
+    launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st, pk_last);
+    launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
+                s->argmax_partial, st, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0);
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
     s->prof_end(pe, st);
   }
