@@ -536,20 +536,43 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
   // workgroup's ticket add, and every load of one here is an sc1 load, so no acquire fence
   // is needed (MI355X_MICROARCH.md, visibility "Valid forms", row 1: one workgroup per CU,
   // unsharded counter, last adder told by the returned value).  One pass per (head, dim),
-  // chunks merged in fixed order (deterministic).
+  // chunks merged in fixed order (deterministic).  The chunks' (m, l, o) are loaded MB at a
+  // time from clamped addresses, all issued before the first use: one memory round trip per
+  // MB chunks (a loop of dependent loads cost two round trips per chunk: nc = 16 took 118 us).
+  constexpr int MB = 8;
+  auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   for (int idx = threadIdx.x; idx < n_rep * HEAD_DIM; idx += NW * 64) {
     const int n = idx / HEAD_DIM, d = idx % HEAD_DIM;
     const float* pn = base + n * PART_STRIDE;
+    float mc[MB], lc[MB], oc[MB];
+    auto load_block = [&](int c0) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j) {
+        const float* pc = pn + (int64_t)min(c0 + j, nc - 1) * stride;
+        mc[j] = ld(pc + HEAD_DIM);
+        lc[j] = ld(pc + HEAD_DIM + 1);
+        oc[j] = ld(pc + d);
+      }
+    };
+    load_block(0);
     float M = -INFINITY;
-    for (int c = 0; c < nc; ++c)
-      M = fmaxf(M, __hip_atomic_load(pn + (int64_t)c * stride + HEAD_DIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int c0 = 0; c0 < nc; c0 += MB) {
+      if (c0) load_block(c0);
+#pragma unroll
+      for (int j = 0; j < MB; ++j)
+        if (c0 + j < nc) M = fmaxf(M, mc[j]);
+    }
+    if (nc > MB) load_block(0);
     float acc = 0.f, L = 0.f;
-    for (int c = 0; c < nc; ++c) {
-      const float* pc = pn + (int64_t)c * stride;
-      const float f =
-          exp2f(__hip_atomic_load(pc + HEAD_DIM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - M);
-      L += __hip_atomic_load(pc + HEAD_DIM + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
-      acc += __hip_atomic_load(pc + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * f;
+    for (int c0 = 0; c0 < nc; c0 += MB) {
+      if (c0) load_block(c0);
+#pragma unroll
+      for (int j = 0; j < MB; ++j)
+        if (c0 + j < nc) {
+          const float f = exp2f(mc[j] - M);
+          L += lc[j] * f;
+          acc += oc[j] * f;
+        }
     }
     const u16 ov = f2bf(acc / L);
     if (fz.pack_ld) out[packed_index(tok, (g * n_rep + n) * HEAD_DIM + d, fz.pack_ld)] = ov;

@@ -82,6 +82,26 @@ void launch_unpack(const u16* src, int N, int K, u16* dst, hipStream_t s) {
   hipLaunchKernelGGL(unpack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, N, K, dst);
 }
 
+// ------------------------------------------------------------------ decode-step advance
+// Device-side scheduler step for a captured decode graph: the new token of sequence b sits
+// at position ctx_lens[b] (the cached length), writes its K/V to the slot the block table
+// gives for that position, and the cached length grows by one.  Runs in the graph's first
+// node (decode_advance_kernel, or the first RMSNorm launch: NormPrologue), so a replay needs
+// no host work.  A sequence whose block table is full gets slot -1 (no cache write) and sets
+// err bit 2.
+__device__ __forceinline__ void decode_advance_one(int32_t* positions, int32_t* slots, int32_t* ctx_lens,
+                                                   const int32_t* block_table, int max_pages, int b, int32_t* err) {
+  int p = ctx_lens[b];
+  positions[b] = p;
+  if (p / KV_PAGE < max_pages) {
+    slots[b] = block_table[(int64_t)b * max_pages + p / KV_PAGE] * KV_PAGE + p % KV_PAGE;
+    ctx_lens[b] = p + 1;
+  } else {
+    slots[b] = -1;
+    atomicOr(err, 2);
+  }
+}
+
 // ------------------------------------------------------------------ RMSNorm
 // y = w * bf16(x * 1/sqrt(mean(x^2) + eps))     (qwen3_server_module.py:19-25)
 // One 256-thread block per row; each thread keeps <= CH 8-element chunks in registers.
@@ -92,13 +112,24 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const u16* __restrict__ x,
                                                       int row_sub, const u16* __restrict__ w,
                                                       u16* __restrict__ y, int64_t ldy, int N,
                                                       float eps, int pack, unsigned long long* zero_slots,
-                                                      int n_slots) {
+                                                      int n_slots, NormPrologue pro) {
   __shared__ float red[4];
   int row = blockIdx.x;
+  if (pro.positions && row == 0)
+    for (int b = threadIdx.x; b < pro.B; b += 256) decode_advance_one(pro.positions, pro.slots, pro.ctx_lens,
+                                                                       pro.block_table, pro.max_pages, b, pro.err);
   // this row's words of the SSQ slots the span's decode GEMVs will fill (kernels.h DecodeNorm)
   for (int i = threadIdx.x; i < n_slots * SSQ_SHARDS * 2; i += 256) zero_slots[(int64_t)i * 64 + row] = 0ull;
   int src_row = row_index ? row_index[row] - row_sub : row;
   const u16* xr = x + (int64_t)src_row * ldx;
+  if (pro.ids) {  // embedding gather (embed_kernel's checks)
+    int id = pro.ids[row];
+    if (id < 0 || id >= pro.vocab) {
+      if (threadIdx.x == 0) atomicOr(pro.err, 1);
+      id = 0;
+    }
+    xr = pro.table + (int64_t)id * N;
+  }
   int nch = N / 8;
   float v[CH][8];
   float ss = 0.f;
@@ -107,6 +138,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const u16* __restrict__ x,
     int ci = threadIdx.x + c * 256;
     if (ci < nch) {
       u16x8 p = *(const u16x8*)(xr + ci * 8);
+      if (pro.x_out) *(u16x8*)(pro.x_out + (int64_t)row * N + ci * 8) = p;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         v[c][j] = bf2f(p[j]);
@@ -136,23 +168,24 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const u16* __restrict__ x,
 
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
                     u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out,
-                    unsigned long long* zero_slots, int n_slots) {
+                    unsigned long long* zero_slots, int n_slots, const NormPrologue* pro_in) {
   if (!zero_slots || M > 64) n_slots = 0;
+  const NormPrologue pro = pro_in ? *pro_in : NormPrologue{};
   const int pk = pack_out ? 1 : 0;
   int ch = (N / 8 + 255) / 256;
   dim3 g(M), b(256);
   if (ch <= 1)
     hipLaunchKernelGGL(rmsnorm_kernel<1>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk,
-                       zero_slots, n_slots);
+                       zero_slots, n_slots, pro);
   else if (ch <= 2)
     hipLaunchKernelGGL(rmsnorm_kernel<2>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk,
-                       zero_slots, n_slots);
+                       zero_slots, n_slots, pro);
   else if (ch <= 4)
     hipLaunchKernelGGL(rmsnorm_kernel<4>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk,
-                       zero_slots, n_slots);
+                       zero_slots, n_slots, pro);
   else
     hipLaunchKernelGGL(rmsnorm_kernel<8>, g, b, 0, s, x, ldx, row_index, row_sub, w, y, ldy, N, eps, pk,
-                       zero_slots, n_slots);
+                       zero_slots, n_slots, pro);
 }
 
 // ------------------------------------------------------------------ rope table
@@ -274,26 +307,12 @@ void launch_embed(const int32_t* ids, const u16* table, int M, int N, int vocab,
   hipLaunchKernelGGL(embed_kernel, dim3(M), dim3(256), 0, s, ids, table, N, vocab, out, err);
 }
 
-// ------------------------------------------------------------------ decode-step advance
-// Device-side scheduler step for a captured decode graph: the new token of sequence b sits
-// at position ctx_lens[b] (the cached length), writes its K/V to the slot the block table
-// gives for that position, and the cached length grows by one.  Runs as the first node of
-// the graph, so a replay needs no host work.  A sequence whose block table is full gets
-// slot -1 (no cache write) and sets err bit 2.
+// ------------------------------------------------------------------ decode-step advance (own launch)
 __global__ void decode_advance_kernel(int32_t* __restrict__ positions, int32_t* __restrict__ slots,
                                       int32_t* __restrict__ ctx_lens, const int32_t* __restrict__ block_table,
                                       int max_pages, int B, int32_t* __restrict__ err) {
   int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  int p = ctx_lens[b];
-  positions[b] = p;
-  if (p / KV_PAGE < max_pages) {
-    slots[b] = block_table[(int64_t)b * max_pages + p / KV_PAGE] * KV_PAGE + p % KV_PAGE;
-    ctx_lens[b] = p + 1;
-  } else {
-    slots[b] = -1;
-    atomicOr(err, 2);
-  }
+  if (b < B) decode_advance_one(positions, slots, ctx_lens, block_table, max_pages, b, err);
 }
 
 void launch_decode_advance(int32_t* positions, int32_t* slots, int32_t* ctx_lens, const int32_t* block_table,

@@ -35,10 +35,27 @@ struct QkvEpilogue {
 void launch_weightgen(u16* dst, int64_t n, uint64_t key, float scale, float center, hipStream_t s);
 void launch_pack(const u16* src, int64_t ld, int N, int K, u16* dst, hipStream_t s);
 void launch_unpack(const u16* src, int N, int K, u16* dst, hipStream_t s);
+// Work a decode step's first RMSNorm launch can take over from two launches of its own (each
+// a ~4.5 us node of the decode graph): the embedding gather (ids != null: row r of x is
+// table[ids[r]], also written to x_out, ldx = N; bad ids set err bit 0 like embed_kernel) and
+// the graph's scheduler step (positions != null: decode_advance_kernel's update by workgroup
+// 0 -- nothing in the norm reads them).
+struct NormPrologue {
+  const int32_t* ids = nullptr;
+  const u16* table = nullptr;
+  int vocab = 0;
+  int32_t* err = nullptr;
+  u16* x_out = nullptr;
+  int32_t* positions = nullptr;
+  int32_t* slots = nullptr;
+  int32_t* ctx_lens = nullptr;
+  const int32_t* block_table = nullptr;
+  int max_pages = 0, B = 0;
+};
 // zero_slots: rows < M of n_slots SSQ slots (kernels.h DecodeNorm) are zeroed too, or null
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
                     u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out = false,
-                    unsigned long long* zero_slots = nullptr, int n_slots = 0);
+                    unsigned long long* zero_slots = nullptr, int n_slots = 0, const NormPrologue* pro = nullptr);
 void launch_rope_table(const float* inv_freq, int max_pos, u16* cos_t, u16* sin_t, hipStream_t s);
 void launch_qk_norm_rope_kv(const u16* qkv, int64_t ldqkv, const int32_t* positions,
                             const int32_t* slots, const u16* qn_w, const u16* kn_w,

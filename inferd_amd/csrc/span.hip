@@ -138,6 +138,10 @@ struct InferdSpan {
   float* qkv_part = nullptr;  // decode split-K q/k/v partials [QKV_KSL_MAX][16][qkv_rows]
   unsigned long long* argmax_partial = nullptr;
   int32_t* err = nullptr;
+  // set by inferd_span_graph_capture(advance): the scheduler step the next forward's first
+  // RMSNorm launch runs (NormPrologue) instead of a decode_advance_kernel node of its own
+  NormPrologue adv;
+  bool adv_pending = false;
   std::vector<void*> allocs;
   // optional per-kernel-class timing with HIP events on the launch stream
   bool prof_on = false;
@@ -432,9 +436,24 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   const int qkvN = s->qkv_rows();
   const float scale = 1.0f / sqrtf((float)HEAD_DIM);
   const u16* x;
+  // the first RMSNorm launch (layer 0's input norm) also runs the embedding gather and a
+  // pending graph scheduler step (kernels.h NormPrologue): two graph nodes fewer per step
+  NormPrologue pro;
+  if (s->adv_pending) {
+    pro = s->adv;
+    s->adv_pending = false;
+  }
   if (c.has_embed) {
     if (!ids) return fail(INFERD_ERR_ARG, "first span needs token ids");
-    launch_embed(ids, s->embed, M, h, c.vocab, s->h, s->err, st);
+    if (c.n_layers > 0) {
+      pro.ids = ids;
+      pro.table = s->embed;
+      pro.vocab = c.vocab;
+      pro.err = s->err;
+      pro.x_out = s->h;
+    } else {
+      launch_embed(ids, s->embed, M, h, c.vocab, s->h, s->err, st);
+    }
     x = s->h;
   } else {
     if (!x_in) return fail(INFERD_ERR_ARG, "span needs x_in hidden states");
@@ -470,7 +489,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     } else {
       pe = s->prof_begin(PROF_NORM, st);
       launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st, false, gemv ? s->ssq : nullptr,
-                     2 * c.n_layers);
+                     2 * c.n_layers, l == 0 ? &pro : nullptr);
       s->prof_end(pe, st);
       a_in = s->xn;
     }
@@ -614,10 +633,22 @@ extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, in
   s->prof_on = false;  // event pairs are timed eagerly only (HIP cannot time captured events)
   HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
   int rc = INFERD_OK;
-  if (advance)
+  if (advance && s->cfg.n_layers > 0) {  // run by layer 0's input norm (NormPrologue)
+    s->adv = NormPrologue{};
+    s->adv.positions = (int32_t*)b->positions;
+    s->adv.slots = (int32_t*)b->slots;
+    s->adv.ctx_lens = (int32_t*)b->ctx_lens;
+    s->adv.block_table = b->block_table;
+    s->adv.max_pages = b->max_pages;
+    s->adv.B = b->n_seqs;
+    s->adv.err = s->err;
+    s->adv_pending = true;
+  } else if (advance) {
     launch_decode_advance((int32_t*)b->positions, (int32_t*)b->slots, (int32_t*)b->ctx_lens, b->block_table,
                           b->max_pages, b->n_seqs, s->err, st);
+  }
   rc = inferd_span_forward(s, b, ids, x_in, x_out, next_ids, logits, nullptr, stream);
+  s->adv_pending = false;
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(st, &g);
   if (rc) {

@@ -5,6 +5,7 @@
 // Standalone; not part of the engine.  Build + run on the GPU box:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++20 -I inferd_amd/csrc tools/attn_lab.hip -o /tmp/attn_lab && /tmp/attn_lab
 #include "../inferd_amd/csrc/attention.hip"
+#include "../inferd_amd/csrc/attn_prefill.hip"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -270,6 +271,15 @@ int main(int argc, char** argv) {
   });
   control("stream nw4 nc4 depth4", [&](u16* kvp) {
     hipLaunchKernelGGL((stream_kv_kernel<4, 4>), dim3(4, KV, B), dim3(256), 0, 0, kvp, ab, KV, 4, sink);
+  });
+  control("stream nw8 nc1 depth2", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_kv_kernel<8, 2>), dim3(1, KV, B), dim3(512), 0, 0, kvp, ab, KV, 1, sink);
+  });
+  control("stream nw8 nc1 depth4", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_kv_kernel<8, 4>), dim3(1, KV, B), dim3(512), 0, 0, kvp, ab, KV, 1, sink);
+  });
+  control("stream nw16 nc1 depth4", [&](u16* kvp) {
+    hipLaunchKernelGGL((stream_kv_kernel<16, 4>), dim3(1, KV, B), dim3(1024), 0, 0, kvp, ab, KV, 1, sink);
   });
   control("stream nw16 nc1 depth2", [&](u16* kvp) {
     hipLaunchKernelGGL((stream_kv_kernel<16, 2>), dim3(1, KV, B), dim3(1024), 0, 0, kvp, ab, KV, 1, sink);
