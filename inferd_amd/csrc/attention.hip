@@ -679,11 +679,11 @@ void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, co
 //  * l is kept per lane (each lane's share of its query's row sum) and reduced across the 4
 //    lanes of a query once, at the end;
 //  * row max reductions use v_permlane{32,16}_swap instead of ds_bpermute.
-template <bool MASK>
-__device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, const bf16x8 (&qf)[2][4],
-                                                 int page_tok0, const int (&lim)[2], float c,
-                                                 float (&m_i)[2], float (&l_i)[2], f32x4 (&o)[2][8], int lane) {
-  f32x4 sc[2][4];
+template <bool MASK, int NB>
+__device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, const bf16x8 (&qf)[NB][4],
+                                                 int page_tok0, const int (&lim)[NB], float c,
+                                                 float (&m_i)[NB], float (&l_i)[NB], f32x4 (&o)[NB][8], int lane) {
+  f32x4 sc[NB][4];
   // k-slice outermost: eight accumulation chains in flight (tb outermost left two, with
   // s_nops between dependent MFMAs)
 #pragma unroll
@@ -692,12 +692,12 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
     for (int tb = 0; tb < 4; ++tb) {
       const bf16x8 kf = *(const bf16x8*)(lds + (tb * 4 + ks) * 1024 + lane * 16);
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
+      for (int nb = 0; nb < NB; ++nb)
         sc[nb][tb] = mfma16(kf, qf[nb][ks], ks ? sc[nb][tb] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
-  bf16x8 pf[2][2];
+  bf16x8 pf[NB][2];
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
+  for (int nb = 0; nb < NB; ++nb) {
     if constexpr (MASK) {
 #pragma unroll
       for (int tb = 0; tb < 4; ++tb)
@@ -743,7 +743,7 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
     for (int db = 0; db < 8; ++db) {
       const bf16x8 vf = *(const bf16x8*)(lds + 16384 + (kt * 8 + db) * 1024 + lane * 16);
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) o[nb][db] = mfma16(vf, pf[nb][kt], o[nb][db]);
+      for (int nb = 0; nb < NB; ++nb) o[nb][db] = mfma16(vf, pf[nb][kt], o[nb][db]);
     }
 }
 
@@ -752,16 +752,21 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
 // head) with the n_rep heads of a group fastest, so the heads that read the same K/V pages
 // run together on one XCD (one L2); query blocks heaviest first, so light blocks fill the
 // tail.  Mode 0: head-major, heaviest query block first.
+// NB: 16-row MFMA column blocks per wave (each staged K/V fragment feeds NB MFMAs): 2 = 128 rows
+// per workgroup; 3 = 192 rows (a third fewer LDS fragment reads per MFMA)
+template <int NB>
 __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restrict__ q,
                                                            const u16* __restrict__ kv,
                                                            AttnBatch b, int H, int KV,
                                                            float scale_log2,
                                                            u16* __restrict__ out, int order) {
+  constexpr int QB = 64 * NB;  // query rows per workgroup
+  constexpr int RW = 16 * NB;  // per wave
   __shared__ __attribute__((aligned(16))) char lds[2 * 32768];
   const int bseq = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_rep = H / KV;
-  const int mqb = (b.max_q_len + 127) / 128;  // query blocks per head in the grid
+  const int mqb = (b.max_q_len + QB - 1) / QB;  // query blocks per head in the grid
   int h, qbi;
   if (order == 1) {
     const int n = gridDim.x, x = blockIdx.x;  // n % 8 == 0 (launcher)
@@ -776,17 +781,17 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   const int g = h / n_rep;
   const int t0 = b.seq_start[bseq];
   const int T = b.seq_start[bseq + 1] - t0;
-  const int nqb = (T + 127) / 128;
+  const int nqb = (T + QB - 1) / QB;
   // heaviest (latest) query blocks first
   const int qb = mqb - 1 - qbi;
   if (qb >= nqb) return;  // uniform over the workgroup
-  const int qb0 = qb * 128;
-  bf16x8 qf[2][4];
-  int lim[2], tokrow[2];
-  bool valid[2];
+  const int qb0 = qb * QB;
+  bf16x8 qf[NB][4];
+  int lim[NB], tokrow[NB];
+  bool valid[NB];
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
-    const int row = qb0 + wave * 32 + nb * 16 + (lane & 15);
+  for (int nb = 0; nb < NB; ++nb) {
+    const int row = qb0 + wave * RW + nb * 16 + (lane & 15);
     valid[nb] = row < T;
     tokrow[nb] = t0 + (valid[nb] ? row : T - 1);
     lim[nb] = b.positions[tokrow[nb]];
@@ -796,10 +801,12 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   }
   // pages: up to the workgroup's last row; a wave computes up to its own last row and
   // masks only pages that reach past its smallest row limit
-  const int wg_last = b.positions[t0 + min(qb0 + 127, T - 1)];
-  const int wave_first_row = qb0 + wave * 32;
-  const int wave_last = wave_first_row < T ? b.positions[t0 + min(wave_first_row + 31, T - 1)] : -1;
-  int wave_min_lim = min(lim[0], lim[1]);
+  const int wg_last = b.positions[t0 + min(qb0 + QB - 1, T - 1)];
+  const int wave_first_row = qb0 + wave * RW;
+  const int wave_last = wave_first_row < T ? b.positions[t0 + min(wave_first_row + RW - 1, T - 1)] : -1;
+  int wave_min_lim = lim[0];
+#pragma unroll
+  for (int nb = 1; nb < NB; ++nb) wave_min_lim = min(wave_min_lim, lim[nb]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wave_min_lim = min(wave_min_lim, __shfl_xor(wave_min_lim, o));
   const int n_pages = wg_last / KV_PAGE + 1;
@@ -825,10 +832,15 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
                                                0);
     }
   };
-  float m_i[2] = {-INFINITY, -INFINITY}, l_i[2] = {0.f, 0.f};
-  f32x4 o[2][8];
+  float m_i[NB], l_i[NB];
+  f32x4 o[NB][8];
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
+  for (int nb = 0; nb < NB; ++nb) {
+    m_i[nb] = -INFINITY;
+    l_i[nb] = 0.f;
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int db = 0; db < 8; ++db) o[nb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
   stage(0, 0);
@@ -838,13 +850,13 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
     if (pi + 1 < n_pages) stage(cur ^ 1, pi + 1);
     const int tok0 = pi * KV_PAGE;
     if (tok0 + KV_PAGE - 1 <= wave_min_lim)
-      prefill_page_lds<false>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, o, lane);
+      prefill_page_lds<false, NB>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, o, lane);
     else if (tok0 <= wave_last)
-      prefill_page_lds<true>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, o, lane);
+      prefill_page_lds<true, NB>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, o, lane);
     __syncthreads();  // next page landed (vmcnt(0)) and everyone is done with this buffer
   }
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
+  for (int nb = 0; nb < NB; ++nb) {
     const float inv = 1.0f / sum_q4(l_i[nb]);
     if (!valid[nb]) continue;
     u16* op = out + (int64_t)tokrow[nb] * H * HEAD_DIM + h * HEAD_DIM;
@@ -861,8 +873,15 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
                          hipStream_t s) {
   if (b.pfk == 1 && launch_attn_prefill_w64(q, kv_layer, b, H, KV, scale, out, s)) return;
+  if (b.pfk == 3) {  // 48 query rows per wave (INFERD_ATTN_PREFILL=3)
+    const int n = (b.max_q_len + 191) / 192 * H;
+    const int order = b.order >= 0 ? b.order : (n % 8 == 0 ? 1 : 0);
+    hipLaunchKernelGGL(attn_prefill_kernel<3>, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E,
+                       out, (order == 1 && n % 8 == 0) ? 1 : 0);
+    return;
+  }
   const int n = (b.max_q_len + 127) / 128 * H;
   const int order = b.order >= 0 ? b.order : (n % 8 == 0 ? 1 : 0);  // the span's INFERD_ATTN_ORDER
-  hipLaunchKernelGGL(attn_prefill_kernel, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out,
+  hipLaunchKernelGGL(attn_prefill_kernel<2>, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out,
                      (order == 1 && n % 8 == 0) ? 1 : 0);
 }

@@ -111,6 +111,36 @@ __global__ __launch_bounds__(NW * 64) void phase_a_kernel(const u32x4* w, long l
   if (x == 0x9e3779b9u) sink[0] = x;
 }
 
+// cache-policy variants of the A + W stream (buffer loads, aux bits: 1 sc0, 2 nt, 16 sc1)
+template <int NW, int D, int AW, int AA>
+__global__ __launch_bounds__(NW * 64) void phase_pol_kernel(const u32x4* w, long long slice, const u32x4* a,
+                                                            long long a_tiles, unsigned* sink) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long ntiles = slice / 1024;
+  const long long nper = (ntiles - wave + NW - 1) / NW;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(w + (long long)blockIdx.x * slice / 16), 0, (int)slice, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a, 0, (int)(a_tiles * 1024), 0x00020000);
+  auto wo = [&](long long j) { return (int)((wave + (j < nper ? j : nper - 1) * NW) * 1024 + lane * 16); };
+  auto ao = [&](long long j) { return (int)(((wave + (j < nper ? j : nper - 1) * NW) % a_tiles) * 1024 + lane * 16); };
+  u32x4 r[D], ra[D];
+  unsigned x = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    ra[d] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, ao(d), 0, AA));
+    r[d] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, wo(d), 0, AW));
+  }
+  for (long long j = 0; j < nper; j += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      x ^= r[d][0] ^ r[d][1] ^ r[d][2] ^ r[d][3] ^ ra[d][0] ^ ra[d][3];
+      ra[d] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(ar, ao(j + d + D), 0, AA));
+      r[d] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, wo(j + d + D), 0, AW));
+    }
+  }
+  if (x == 0x9e3779b9u) sink[0] = x;
+}
+
 __device__ __forceinline__ int xcc_id() {
   int v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 3)" : "=s"(v));
@@ -244,6 +274,22 @@ int main() {
     hipLaunchKernelGGL((phase_a_kernel<8, 4>), dim3(256), dim3(512), 0, 0, sets[2][i % ROT], bytes[2] / 256, abuf, 384ll,
                        sink);
   });
+  auto pol = [&](const char* name, auto kern, int ph, long long at) {
+    timeit(name, [&](int i) {
+      hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, sets[ph][i % ROT], bytes[ph] / 256, abuf, at, sink);
+    });
+  };
+  pol("o-like pol W nt, A plain", phase_pol_kernel<8, 3, 2, 0>, 0, 128ll);
+  pol("o-like pol W nt, A nt", phase_pol_kernel<8, 3, 2, 2>, 0, 128ll);
+  pol("o-like pol W nt, A sc1", phase_pol_kernel<8, 3, 2, 16>, 0, 128ll);
+  pol("o-like pol W plain, A plain", phase_pol_kernel<8, 3, 0, 0>, 0, 128ll);
+  pol("o-like pol W sc1, A plain", phase_pol_kernel<8, 3, 16, 0>, 0, 128ll);
+  pol("o-like pol W nt, A plain, D 5", phase_pol_kernel<8, 5, 2, 0>, 0, 128ll);
+  pol("down-like pol W nt, A plain", phase_pol_kernel<8, 3, 2, 0>, 2, 384ll);
+  pol("down-like pol W nt, A nt", phase_pol_kernel<8, 3, 2, 2>, 2, 384ll);
+  pol("down-like pol W nt, A sc1", phase_pol_kernel<8, 3, 2, 16>, 2, 384ll);
+  pol("down-like pol W plain, A plain", phase_pol_kernel<8, 3, 0, 0>, 2, 384ll);
+  pol("down-like pol W nt, A plain, D 5", phase_pol_kernel<8, 5, 2, 0>, 2, 384ll);
   timeit("o-like + A, W first", [&](int i) {
     hipLaunchKernelGGL((phase_a_kernel<8, 3, 0, 1>), dim3(256), dim3(512), 0, 0, sets[0][i % ROT], bytes[0] / 256, abuf,
                        128ll, sink);
