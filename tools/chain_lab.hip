@@ -141,6 +141,40 @@ __global__ __launch_bounds__(NW * 64) void phase_pol_kernel(const u32x4* w, long
   if (x == 0x9e3779b9u) sink[0] = x;
 }
 
+// A staged into LDS by LDS-DMA (the whole 128 KiB, 16 pieces per wave) right behind the weight
+// ring's prologue, then read with ds_read_b128: no vector-memory instruction for A in the loop
+template <int NW, int D>
+__global__ __launch_bounds__(NW * 64) void phase_alds_kernel(const u32x4* w, long long slice, const u32x4* a,
+                                                             long long a_tiles, unsigned* sink) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 alds[];
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long ntiles = slice / 1024;
+  const long long nper = (ntiles - wave + NW - 1) / NW;
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(w + (long long)blockIdx.x * slice / 16), 0, (int)slice, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a, 0, (int)(a_tiles * 1024), 0x00020000);
+  auto wo = [&](long long j) { return (int)((wave + (j < nper ? j : nper - 1) * NW) * 1024 + lane * 16); };
+  auto ai = [&](long long j) { return (int)(((wave + (j < nper ? j : nper - 1) * NW) % a_tiles) * 64 + lane); };
+  u32x4 r[D];
+  unsigned x = 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) r[d] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, wo(d), 0, 2));
+  for (int t = wave; t < a_tiles; t += NW)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ar, (lds_ptr)(alds + t * 64), 16, lane * 16, t * 1024, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (long long j = 0; j < nper; j += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const u32x4 av = alds[ai(j + d)];
+      x ^= r[d][0] ^ r[d][1] ^ r[d][2] ^ r[d][3] ^ av[0] ^ av[3];
+      r[d] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, wo(j + d + D), 0, 2));
+    }
+  }
+  if (x == 0x9e3779b9u) sink[0] = x;
+}
+
 __device__ __forceinline__ int xcc_id() {
   int v;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 3)" : "=s"(v));
@@ -279,6 +313,22 @@ int main() {
       hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, sets[ph][i % ROT], bytes[ph] / 256, abuf, at, sink);
     });
   };
+  CHECK(hipFuncSetAttribute((const void*)phase_alds_kernel<8, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+  CHECK(hipFuncSetAttribute((const void*)phase_alds_kernel<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072));
+  timeit("o-like, A by LDS-DMA + ds_read (D 3)", [&](int i) {
+    hipLaunchKernelGGL((phase_alds_kernel<8, 3>), dim3(256), dim3(512), 131072, 0, sets[0][i % ROT], bytes[0] / 256, abuf,
+                       128ll, sink);
+  });
+  timeit("o-like, A by LDS-DMA + ds_read (D 4)", [&](int i) {
+    hipLaunchKernelGGL((phase_alds_kernel<8, 4>), dim3(256), dim3(512), 131072, 0, sets[0][i % ROT], bytes[0] / 256, abuf,
+                       128ll, sink);
+  });
+  timeit("o alone D 4", [&](int i) {
+    hipLaunchKernelGGL((phase_kernel<8, 4>), dim3(256), dim3(512), 0, 0, sets[0][i % ROT], bytes[0] / 256, sink);
+  });
+  pol("o-like pol W nt, A plain, A = 1 KiB (L1 hits)", phase_pol_kernel<8, 3, 2, 0>, 0, 1ll);
+  pol("down-like pol W nt, A plain, A = 1 KiB (L1 hits)", phase_pol_kernel<8, 3, 2, 0>, 2, 1ll);
+  pol("o-like pol W nt, A plain, A = 16 KiB", phase_pol_kernel<8, 3, 2, 0>, 0, 16ll);
   pol("o-like pol W nt, A plain", phase_pol_kernel<8, 3, 2, 0>, 0, 128ll);
   pol("o-like pol W nt, A nt", phase_pol_kernel<8, 3, 2, 2>, 0, 128ll);
   pol("o-like pol W nt, A sc1", phase_pol_kernel<8, 3, 2, 16>, 0, 128ll);
