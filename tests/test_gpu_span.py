@@ -177,6 +177,47 @@ def test_decode_graph_matches_eager():
     assert torch.equal(runs[0], runs[1]), (runs[0], runs[1])
 
 
+@pytest.mark.parametrize("first", [True, False])
+def test_decode_graph_hidden_bit_exact(first):
+    """The decode graph's first launch carries the scheduler step and (first span) the
+    embedding gather inside layer 0's input norm (span.hip NormPrologue); an eager cached
+    decode call launches the same kernels without the step.  Both give bit-identical hidden
+    states over 4 steps, for a first span (ids in) and an inner span (x in)."""
+    from inferd_amd.runtime import DecodeGraph
+    d = R.CONFIGS["tiny"]
+    gen = torch.Generator().manual_seed(21)
+    prompts = torch.randint(0, d.vocab, (3, 40), generator=gen)
+    steps_ids = torch.randint(0, d.vocab, (4, 3), generator=gen)
+    x_pre = (torch.randn(3 * 40, d.hidden, generator=gen) * 0.5).to(torch.bfloat16)
+    x_steps = (torch.randn(4, 3, d.hidden, generator=gen) * 0.5).to(torch.bfloat16)
+    runs = []
+    for use_graph in (False, True):
+        s = span("tiny", 0 if first else 1, 2, first, False)
+        sess = [f"h{b}" for b in range(3)]
+        if first:
+            s.forward([(sid, 40) for sid in sess], ids=prompts.reshape(-1), want_hidden=False)
+        else:
+            s.forward([(sid, 40) for sid in sess], x=x_pre, want_hidden=False)
+        ids = torch.zeros(3, dtype=torch.int32, device=DEV)
+        xin = torch.zeros(3, d.hidden, dtype=torch.bfloat16, device=DEV)
+        hout = torch.zeros(3, d.hidden, dtype=torch.bfloat16, device=DEV)
+        g = None
+        if use_graph:
+            g = DecodeGraph(s, sess, 4, ids=ids if first else None, x=None if first else xin, hidden_out=hout)
+        seq = []
+        for k in range(4):
+            ids.copy_(steps_ids[k])
+            xin.copy_(x_steps[k])
+            if use_graph:
+                g.launch()
+                seq.append(hout.cpu().clone())
+            else:
+                kw = {"ids": ids} if first else {"x": xin}
+                seq.append(s.forward([(sid, 1) for sid in sess], **kw)["hidden"].cpu().clone())
+        runs.append(torch.stack(seq))
+    assert torch.equal(runs[0], runs[1]), (runs[0] - runs[1]).abs().max()
+
+
 def test_q06_full_model_greedy_cached():
     """Config 2: Qwen3-0.6B single full span (peaked profile), prefill 32 + 12 cached greedy
     decode steps teacher-forced on the oracle's ids: every id identical, every oracle margin
