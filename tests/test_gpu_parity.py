@@ -563,8 +563,9 @@ def _pipe_exact_worker(rank, world, port, sizes, out_dir):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("sizes", [[18, 18], [5, 5, 5, 5, 4, 4, 4, 4], [4, 5, 5, 5, 5, 5, 5, 2]],
-                         ids=["config3_even2", "config3_even8", "balanced8"])
+@pytest.mark.parametrize("sizes", [[18, 18], [9, 9, 9, 9], [5, 5, 5, 5, 4, 4, 4, 4], [4, 5, 5, 5, 5, 5, 5, 2],
+                                   [5, 27, 4]],
+                         ids=["config3_even2", "config3_even4", "config3_even8", "balanced8", "config4_uneven3"])
 def test_q8b_pipeline_token_exact_vs_oracle(tmp_path, sizes, q8b_oracle_greedy):
     """Qwen3-8B through the span pipeline, token-exact with the CPU oracle: every greedy id fed
     to stage 0 (STEPS8X steps x every microbatch) and every id the last stage chose (prefill +
