@@ -679,10 +679,12 @@ void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, co
 //  * l is kept per lane (each lane's share of its query's row sum) and reduced across the 4
 //    lanes of a query once, at the end;
 //  * row max reductions use v_permlane{32,16}_swap instead of ds_bpermute.
+// S^T of a page (K at kl) + its online softmax -> P (bf16, the B operand of P.V) in pf
 template <bool MASK, int NB>
-__device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, const bf16x8 (&qf)[NB][4],
-                                                 int page_tok0, const int (&lim)[NB], float c,
-                                                 float (&m_i)[NB], float (&l_i)[NB], f32x4 (&o)[NB][8], int lane) {
+__device__ __forceinline__ void prefill_page_s(const char* __restrict__ kl, const bf16x8 (&qf)[NB][4], int page_tok0,
+                                               const int (&lim)[NB], float c, float (&m_i)[NB], float (&l_i)[NB],
+                                               f32x4 (&o)[NB][8], int lane, bf16x8 (&pf)[NB][2]) {
+  const char* lds = kl;
   f32x4 sc[NB][4];
   // k-slice outermost: eight accumulation chains in flight (tb outermost left two, with
   // s_nops between dependent MFMAs)
@@ -695,7 +697,6 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
       for (int nb = 0; nb < NB; ++nb)
         sc[nb][tb] = mfma16(kf, qf[nb][ks], ks ? sc[nb][tb] : f32x4{0.f, 0.f, 0.f, 0.f});
     }
-  bf16x8 pf[NB][2];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     if constexpr (MASK) {
@@ -737,14 +738,27 @@ __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, c
         pf[nb][kt][4 + j] = (__bf16)sc[nb][2 * kt + 1][j];
       }
   }
+}
+// O^T += V^T P^T of a page (V at vl)
+template <int NB>
+__device__ __forceinline__ void prefill_page_pv(const char* __restrict__ vl, const bf16x8 (&pf)[NB][2],
+                                                f32x4 (&o)[NB][8], int lane) {
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
     for (int db = 0; db < 8; ++db) {
-      const bf16x8 vf = *(const bf16x8*)(lds + 16384 + (kt * 8 + db) * 1024 + lane * 16);
+      const bf16x8 vf = *(const bf16x8*)(vl + (kt * 8 + db) * 1024 + lane * 16);
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) o[nb][db] = mfma16(vf, pf[nb][kt], o[nb][db]);
     }
+}
+template <bool MASK, int NB>
+__device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, const bf16x8 (&qf)[NB][4],
+                                                 int page_tok0, const int (&lim)[NB], float c,
+                                                 float (&m_i)[NB], float (&l_i)[NB], f32x4 (&o)[NB][8], int lane) {
+  bf16x8 pf[NB][2];
+  prefill_page_s<MASK, NB>(lds, qf, page_tok0, lim, c, m_i, l_i, o, lane, pf);
+  prefill_page_pv<NB>(lds + 16384, pf, o, lane);
 }
 
 // Block order (grid x = max_q_blocks * H per sequence, y = sequence): mode 1 (used when
@@ -871,9 +885,153 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   }
 }
 
+// Three workgroups per CU (3 waves per SIMD): the same 4-wave workgroup with 32 rows per wave
+// (157 VGPRs under these launch bounds) and a 48 KiB LDS ring of three 16 KiB half-page slots
+// (K or V of one page; half-page u = 2 page + {0: K, 1: V} lives in slot u % 3).  Per page two
+// barriers: after S + softmax (K(i) consumed: its slot takes V(i+1)) and after P.V (V(i)
+// consumed: its slot takes K(i+2)); each barrier first waits for this wave's pieces of the half
+// the next phase reads (vmcnt leaves the one half issued after it in flight).
+template <int NB>
+__global__ __launch_bounds__(256, 3) void attn_prefill_r3_kernel(const u16* __restrict__ q,
+                                                              const u16* __restrict__ kv, AttnBatch b, int H,
+                                                              int KV, float scale_log2, u16* __restrict__ out,
+                                                              int order) {
+  constexpr int QB = 64 * NB, RW = 16 * NB;
+  __shared__ __attribute__((aligned(16))) char lds[3 * 16384];
+  const int bseq = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n_rep = H / KV;
+  const int mqb = (b.max_q_len + QB - 1) / QB;
+  int h, qbi;
+  if (order == 1) {
+    const int n = gridDim.x, x = blockIdx.x;
+    const int wg = (x & 7) * (n >> 3) + (x >> 3);
+    const int r = wg % n_rep, t = wg / n_rep;
+    qbi = t % mqb;
+    h = (t / mqb) * n_rep + r;
+  } else {
+    h = blockIdx.x / mqb;
+    qbi = blockIdx.x % mqb;
+  }
+  const int g = h / n_rep;
+  const int t0 = b.seq_start[bseq];
+  const int T = b.seq_start[bseq + 1] - t0;
+  const int nqb = (T + QB - 1) / QB;
+  const int qb = mqb - 1 - qbi;
+  if (qb >= nqb) return;
+  const int qb0 = qb * QB;
+  bf16x8 qf[NB][4];
+  int lim[NB], tokrow[NB];
+  bool valid[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int row = qb0 + wave * RW + nb * 16 + (lane & 15);
+    valid[nb] = row < T;
+    tokrow[nb] = t0 + (valid[nb] ? row : T - 1);
+    lim[nb] = b.positions[tokrow[nb]];
+    const u16* qp = q + ((int64_t)tokrow[nb] * H + h) * HEAD_DIM + 8 * (lane >> 4);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
+  }
+  const int wg_last = b.positions[t0 + min(qb0 + QB - 1, T - 1)];
+  const int wave_first_row = qb0 + wave * RW;
+  const int wave_last = wave_first_row < T ? b.positions[t0 + min(wave_first_row + RW - 1, T - 1)] : -1;
+  int wave_min_lim = lim[0];
+#pragma unroll
+  for (int nb = 1; nb < NB; ++nb) wave_min_lim = min(wave_min_lim, lim[nb]);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) wave_min_lim = min(wave_min_lim, __shfl_xor(wave_min_lim, off));
+  const int n_pages = wg_last / KV_PAGE + 1;
+  const int n_half = 2 * n_pages;
+  typedef const __attribute__((address_space(4))) int* cptr;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  const cptr bt = (cptr)(b.block_table + (int64_t)bseq * b.max_pages);
+  const int swave = __builtin_amdgcn_readfirstlane(wave);
+  // half-page u -> slot u % 3: this wave's 4 of its 16 pieces
+  auto stage = [&](int u) {
+    const int pi = u >> 1, kind = u & 1;
+    const __amdgpu_buffer_rsrc_t pg_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(kv + kv_block(bt[pi], 0, g, KV)), 0, 2 * KV_BLOCK_ELEMS * 2, 0x00020000);
+    char* base = lds + (u % 3) * 16384;
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc) {
+      const int piece = swave * 4 + pc;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(pg_rsrc, (lds_ptr)(base + piece * 1024), 16, lane * 16,
+                                               (kind * 16 + piece) * 1024, 0, 0);
+    }
+  };
+  float m_i[NB], l_i[NB];
+  f32x4 o[NB][8];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    m_i[nb] = -INFINITY;
+    l_i[nb] = 0.f;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) o[nb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // prologue: K0, V0, K1 in flight; K0 must land before S(0): vmcnt leaves V0 and K1
+  stage(0);
+  stage(1);
+  if (n_half > 2) {
+    stage(2);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  }
+  raw_barrier();  // (__syncthreads() would drain the half-pages left in flight)
+  bf16x8 pf[NB][2];
+  for (int pi = 0; pi < n_pages; ++pi) {
+    const int tok0 = pi * KV_PAGE;
+    const char* kl = lds + ((2 * pi) % 3) * 16384;
+    const char* vl = lds + ((2 * pi + 1) % 3) * 16384;
+    const bool live = tok0 <= wave_last;
+    if (tok0 + KV_PAGE - 1 <= wave_min_lim)
+      prefill_page_s<false, NB>(kl, qf, tok0, lim, scale_log2, m_i, l_i, o, lane, pf);
+    else if (live)
+      prefill_page_s<true, NB>(kl, qf, tok0, lim, scale_log2, m_i, l_i, o, lane, pf);
+    // B1: V(i) landed (in flight after it: K(i+1) if issued); K(i)'s slot takes V(i+1)
+    if (2 * pi + 2 < n_half)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (2 * pi + 3 < n_half) stage(2 * pi + 3);
+    if (live) prefill_page_pv<NB>(vl, pf, o, lane);
+    // B2: K(i+1) landed (in flight after it: V(i+1) if issued); V(i)'s slot takes K(i+2)
+    if (2 * pi + 3 < n_half)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    if (2 * pi + 4 < n_half) stage(2 * pi + 4);
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const float inv = 1.0f / sum_q4(l_i[nb]);
+    if (!valid[nb]) continue;
+    u16* op = out + (int64_t)tokrow[nb] * H * HEAD_DIM + h * HEAD_DIM;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[nb][db][r] * inv);
+      *(u16x4*)(op + db * 16 + 4 * (lane >> 4)) = v;
+    }
+  }
+}
+
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
                          hipStream_t s) {
   if (b.pfk == 1 && launch_attn_prefill_w64(q, kv_layer, b, H, KV, scale, out, s)) return;
+  if (b.pfk == 6) {  // three workgroups per CU, 48 KiB half-page ring (INFERD_ATTN_PREFILL=6)
+    const int n = (b.max_q_len + 127) / 128 * H;
+    const int order = b.order >= 0 ? b.order : (n % 8 == 0 ? 1 : 0);
+    hipLaunchKernelGGL(attn_prefill_r3_kernel<2>, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV,
+                       scale * LOG2E, out, (order == 1 && n % 8 == 0) ? 1 : 0);
+    return;
+  }
   if (b.pfk == 2) {  // 32 query rows per wave (INFERD_ATTN_PREFILL=2; the default until round 3)
     const int n = (b.max_q_len + 127) / 128 * H;
     const int order = b.order >= 0 ? b.order : (n % 8 == 0 ? 1 : 0);  // the span's INFERD_ATTN_ORDER

@@ -139,7 +139,8 @@ struct AttnBatch {
   // the staged q image, prefill block order (-1 default, 0 head-major, 1 XCD-grouped)
   int nw = 0, nc = 0, qlanes = 0, order = -1;
   // prefill kernel: 1 = the one-wave-per-SIMD body (attn_prefill.hip), 0 = attn_prefill_kernel<3>
-  // (48 rows per wave), 2 = attn_prefill_kernel<2> (32 rows per wave)
+  // (48 rows per wave), 2 = attn_prefill_kernel<2> (32 rows per wave), 6 = attn_prefill_r3_kernel
+  // (32 rows per wave, three workgroups per CU)
   int pfk = 0;
 };
 // q [M][H][128] bf16 -> out [M][H*128] bf16.  kv_layer: this layer's pool base.

@@ -85,7 +85,7 @@ struct Knobs {
   int attn_nw = 0, attn_nc = 0;  // INFERD_ATTN_NW / _NC: decode attention shape (0: default)
   int attn_qlanes = 0;           // INFERD_ATTN_QLANES=1: per-lane q loads in the fused decode attention
   int attn_order = -1;           // INFERD_ATTN_ORDER: prefill block order (-1: default)
-  int attn_prefill = 0;          // INFERD_ATTN_PREFILL: 1 = one-wave-per-SIMD prefill attention, 2 = 32 rows per wave
+  int attn_prefill = 0;          // INFERD_ATTN_PREFILL: 1 = one-wave-per-SIMD prefill attention, 2 = 32 rows per wave, 6 = three WGs/CU
 };
 
 int env_int(const char* name, int dflt) {

@@ -280,7 +280,7 @@ def test_attention_decode(lib, H, KV):
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
 
 
-@pytest.mark.parametrize("pfk", [0, 1, 2])
+@pytest.mark.parametrize("pfk", [0, 1, 2, 6])
 @pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2), (64, 8)])
 def test_attention_prefill(lib, monkeypatch, H, KV, pfk):
     """Every prefill kernel (INFERD_ATTN_PREFILL=0: the 4-wave attn_prefill_kernel with 48 rows per
