@@ -280,11 +280,21 @@ def test_attention_decode(lib, H, KV):
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
 
 
+@pytest.mark.parametrize("q_lens,past", [([1], [5999]), ([1, 1], [5999, 3000])], ids=["b1_ctx6000", "b2_ctx6000_3001"])
+def test_attention_decode_many_chunks(lib, q_lens, past):
+    """Few sequences at long context split into many chunks per (sequence, kv head): 23 chunks for
+    one sequence at 6000 tokens, 16 for two -- the last-arriving chunk merges them 8 at a time
+    (attention.hip), so these exercise several merge blocks and a partial last block."""
+    err, ref = _attn_case(lib, 32, 8, q_lens, past, seed=7)
+    assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
+
+
 @pytest.mark.parametrize("pfk", [0, 1, 2, 6])
 @pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2), (64, 8)])
 def test_attention_prefill(lib, monkeypatch, H, KV, pfk):
     """Every prefill kernel (INFERD_ATTN_PREFILL=0: the 4-wave attn_prefill_kernel with 48 rows per
-    wave, 2: the same with 32 rows per wave, 1: the one-wave-per-SIMD attn_prefill.hip) on ragged prompts, with and without cached prefixes:
+    wave, 2: the same with 32 rows per wave, 6: 32 rows per wave at three workgroups per CU, 1: the
+    one-wave-per-SIMD attn_prefill.hip) on ragged prompts, with and without cached prefixes:
     a 700-token prompt (several 128-row blocks, > 4 pages) and a 1000-token prompt behind 300
     cached tokens (several 256-row blocks, masks on pages that start mid-block)."""
     monkeypatch.setenv("INFERD_ATTN_PREFILL", str(pfk))
