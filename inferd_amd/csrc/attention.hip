@@ -660,13 +660,13 @@ void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, co
 }
 
 // ------------------------------------------------------------------ prefill (causal)
-// grid (ceil(max_q_len/128), H, B), 4 waves.  The workgroup owns 128 query rows of one head;
-// wave w owns rows [32w, 32w+32) as two 16-row MFMA column blocks.  Every K/V page (K 16 KiB
+// grid (ceil(max_q_len/(64 NB)), H, B), 4 waves.  The workgroup owns 64 NB query rows of one head
+// (NB = 3 by default: 192); wave w owns 16 NB rows as NB 16-row MFMA column blocks.  Every K/V page (K 16 KiB
 // + V 16 KiB of this kv head) is staged ONCE per workgroup into double-buffered LDS with
 // global_load_lds_dwordx4 (32 x 1 KiB pieces, 8 per wave) while the previous page is being
 // consumed; the page layout is already fragment-ordered, so every fragment read is
 // lds[tile * 1 KiB + lane * 16] (contiguous, bank-conflict free), and each K/V fragment feeds
-// the MFMAs of both column blocks.  Waves whose rows all precede a page skip its compute but
+// the MFMAs of all NB column blocks.  Waves whose rows all precede a page skip its compute but
 // keep the barriers.
 //
 // Softmax VALU per page is the kernel's pole (64 MFMAs vs ~550 VALU ops before), so:
