@@ -340,10 +340,13 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # a wedged hand-off fails within 2 minutes with the process group's error instead of
+        # sitting until the driver's limit
+        from datetime import timedelta
         if backend == "gloo":
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timedelta(seconds=120))
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=timedelta(seconds=120))
 
     ranks = [{"rank": rank, "local_rank": local_rank, "device": f"cuda:{dev_index}",
               "name": torch.cuda.get_device_name(dev_index)}]
@@ -368,6 +371,10 @@ def main():
     else:
         spans = stage_split(d, world, B, ctx, args.split)
     first, n_layers = spans[rank]
+    if world > 1:
+        print(f"bench.py: rank {rank} on cuda:{dev_index}: layers {first}..{first + n_layers - 1} of {d.layers}"
+              f"{' + embed' if rank == 0 else ''}{' + norm/lm_head' if rank == world - 1 else ''}",
+              file=sys.stderr, flush=True)
     n_mb = world                                   # microbatches in flight
     st = P.PipelineStage(d, rank, world, first, n_layers, device=dev, seed=args.seed,
                          n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + args.profile_steps + 64,

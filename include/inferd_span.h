@@ -97,6 +97,8 @@ int inferd_abi_version(void);
  *      qwen3_server_module.py:209-235) ---------------------------------------------- */
 int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out);
 void inferd_span_destroy(InferdSpan* span);
+/* the configuration the span was created with (hosts size their buffers from it) */
+int inferd_span_get_config(const InferdSpan* span, InferdSpanConfig* out);
 
 /* Fill every weight of the span from the counter-based generator (oracle/weightgen.py
  * defines the same values) -- the offline stand-in for the HF checkpoint. */
@@ -140,8 +142,9 @@ int inferd_span_lm_head(InferdSpan* span, const void* x, int32_t rows, void* log
  * device-side scheduler step: for every sequence b the new token goes to position
  * ctx_lens[b], its slot comes from the block table, and ctx_lens[b] grows by one -- the
  * batch arrays are mutated in place, so repeated launches walk the sequences forward one
- * token per launch with no host work (the caller reserves the pages beforehand and sets
- * max_ctx_len to the capacity; sequences running out of pages set error flag bit 2).
+ * token per launch with no host work (build the batch with inferd_kv_build_decode_batch, which
+ * reserves the pages and sets ctx_lens / max_ctx_len as this step expects; sequences running out
+ * of pages set error flag bit 1).
  * `ids` and `next_ids` may be the same buffer (the step reads ids first).  Replaces the
  * per-token client loop over the chain (client.py:244-266, send_message.py:46-60). */
 typedef struct InferdGraph InferdGraph;
@@ -205,6 +208,16 @@ int64_t inferd_kv_batch_words(const InferdKvTable* table, const uint64_t* seqs, 
 int inferd_kv_build_batch(const InferdKvTable* table, const uint64_t* seqs, const int32_t* n_new,
                           int32_t n, int32_t* host, int64_t words, const void* device_base,
                           InferdBatch* out);
+/* The descriptor a decode graph (inferd_span_graph_capture, advance = 1) is captured on: pages
+ * for n_steps more tokens of every sequence are reserved (all or nothing), positions and slots
+ * start at 0 (the graph's scheduler step writes them), ctx_lens = the cached lengths and
+ * max_ctx_len = the capacity (max length + n_steps).  decode_batch_words() is its int32 count
+ * (-1 on a bad request).  The caller advances the table by one token per replay
+ * (inferd_kv_advance_many), as the device does. */
+int64_t inferd_kv_decode_batch_words(const InferdKvTable* table, const uint64_t* seqs, int32_t n,
+                                     int32_t n_steps);
+int inferd_kv_build_decode_batch(InferdKvTable* table, const uint64_t* seqs, int32_t n, int32_t n_steps,
+                                 int32_t* host, int64_t words, const void* device_base, InferdBatch* out);
 
 /* Device base pointer of one layer's KV pool: bf16
  * [pages / 16][kv_heads][pages % 16][K|V][64*128] (super-pages of 16 pages; a pool spans

@@ -42,6 +42,7 @@ SIGNATURES = {
     "inferd_abi_version": (C.c_int, []),
     "inferd_span_create": (C.c_int, [C.POINTER(SpanConfig), C.POINTER(c_p)]),
     "inferd_span_destroy": (None, [c_p]),
+    "inferd_span_get_config": (C.c_int, [c_p, C.POINTER(SpanConfig)]),
     "inferd_span_init_synthetic": (C.c_int, [c_p, c_u64, c_p]),
     "inferd_span_set_weight": (C.c_int, [c_p, c_i32, C.c_char_p, c_p, c_i64, c_i64, c_p]),
     "inferd_span_forward": (C.c_int, [c_p, C.POINTER(Batch), c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
@@ -76,6 +77,9 @@ SIGNATURES = {
     "inferd_kv_batch_words": (c_i64, [c_p, C.POINTER(c_u64), C.POINTER(c_i32), c_i32]),
     "inferd_kv_build_batch": (C.c_int, [c_p, C.POINTER(c_u64), C.POINTER(c_i32), c_i32, C.POINTER(c_i32), c_i64, c_p,
                                         C.POINTER(Batch)]),
+    "inferd_kv_decode_batch_words": (c_i64, [c_p, C.POINTER(c_u64), c_i32, c_i32]),
+    "inferd_kv_build_decode_batch": (C.c_int, [c_p, C.POINTER(c_u64), c_i32, c_i32, C.POINTER(c_i32), c_i64, c_p,
+                                               C.POINTER(Batch)]),
     "inferd_probe_hbm_read": (C.c_int, [c_p, c_i64, c_p, c_i32, c_p]),
     "inferd_probe_mfma": (C.c_int, [c_i32, c_i32, c_p, c_p, C.POINTER(C.c_double)]),
 }
@@ -116,6 +120,19 @@ def ptr(t) -> int | None:
     if t is None:
         return None
     return t.data_ptr()
+
+
+def batch_struct(words, shape) -> Batch:
+    """The InferdBatch of a descriptor (int32 words tensor + shape [n_seqs, n_tokens, max_q_len,
+    max_ctx_len, max_pages, decode], e.g. runtime.KvTable.build_batch's), for the single-op
+    entry points called through this binding.  The words must outlive every use."""
+    n, m, mq, mc, mp, dec = (int(v) for v in shape)
+    assert words.numel() >= n + 1 + 2 * m + n + n * mp
+    base = words.data_ptr()
+    o = [0, n + 1, n + 1 + m, n + 1 + 2 * m, n + 1 + 2 * m + n]
+    return Batch(n_seqs=n, n_tokens=m, max_q_len=mq, max_ctx_len=mc, max_pages=mp, decode=dec,
+                 seq_start=base + 4 * o[0], positions=base + 4 * o[1], slots=base + 4 * o[2],
+                 ctx_lens=base + 4 * o[3], block_table=base + 4 * o[4])
 
 
 def stream_ptr(stream=None) -> int | None:

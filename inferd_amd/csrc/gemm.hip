@@ -1490,7 +1490,7 @@ bool gemm_uses_tiled(int M, int N, int K, int epi) {
          epi != EPI_ARGMAX;
 }
 
-void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
+bool launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s, const GemmWs* ws,
                  const DecodeNorm* dn, unsigned long long* ssq_out, int pack) {
   const int KT = K / 32;
@@ -1520,10 +1520,10 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
                              M, gm, gn, st, grid, QkvEpilogue{});
           break;
       }
-      return;
+      return true;
     }
     w4_launch(epi, grid, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M, gm, gn, st);  // tail split
-    return;
+    return true;
   }
   if (tiled) {
     const int ncols = (epi == EPI_SILU) ? 64 : 128;
@@ -1540,12 +1540,14 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
         hipLaunchKernelGGL(gemm_tiled_kernel<EPI_SILU>, g, dim3(256), 0, s, A, lda, Wp, KT, ntw, C, ldc, R, ldr, M);
         break;
     }
-    return;
+    return true;
   }
-  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail; the
-  // DN_EXACT norm and the ssq_out partials are defined for M <= 64 only)
+  // decode path, 64-row slabs (M > 64 only when the tiled shape constraints fail).  The
+  // DN_EXACT norm and the ssq_out partials are defined for M <= 64 only: refused (nothing
+  // launched, false), so a consumer never reads a slot no producer filled
   const int mode = dn ? dn->mode : DN_NONE;
-  if ((mode == DN_EXACT || ssq_out) && M > 64) return;
+  if ((mode == DN_EXACT || ssq_out) && M > 64) return false;
+  if (mode == DN_EXACT && epi == EPI_RESID) return false;  // no such body
   for (int m0 = 0; m0 < M; m0 += 64) {
     DecodeArgs a = {};
     a.M = (M - m0) < 64 ? (M - m0) : 64;
@@ -1580,6 +1582,7 @@ void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     }
     if (epi == EPI_ARGMAX) break;  // argmax requires M <= 64 (checked by the caller)
   }
+  return true;
 }
 
 // Greedy id per row from the lm_head GEMV's per-tile keys (layout [M][n_tiles], so a

@@ -102,8 +102,10 @@ struct GemmWs {
 int gemm_ws_alloc(GemmWs* w);  // hipError_t as int
 void gemm_ws_free(GemmWs* w);
 // ssq_out (EPI_RESID, M <= 64): the SSQ slot (above) that receives the row sums of squares of
-// the stored outputs -- the DecodeNorm input of the next normed GEMV.
-void launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
+// the stored outputs -- the DecodeNorm input of the next normed GEMV.  Returns false, launching
+// nothing, for a combination no body implements (DN_EXACT or ssq_out with M > 64, DN_EXACT with
+// EPI_RESID): the caller must fail rather than let a consumer read an unfilled SSQ slot.
+bool launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
                  const GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr, unsigned long long* ssq_out = nullptr,
                  int pack = 0);
@@ -134,14 +136,6 @@ struct AttnBatch {
   int M;
   int max_q_len;
   int max_ctx;
-  // launch shape knobs (the span's, read once at inferd_span_create; 0 = the measured default):
-  // decode waves per workgroup / chunks per (sequence, kv head), per-lane q loads instead of
-  // the staged q image, prefill block order (-1 default, 0 head-major, 1 XCD-grouped)
-  int nw = 0, nc = 0, qlanes = 0, order = -1;
-  // prefill kernel: 1 = the one-wave-per-SIMD body (attn_prefill.hip), 0 = attn_prefill_kernel<3>
-  // (48 rows per wave), 2 = attn_prefill_kernel<2> (32 rows per wave), 6 = attn_prefill_r3_kernel
-  // (32 rows per wave, three workgroups per CU)
-  int pfk = 0;
 };
 // q [M][H][128] bf16 -> out [M][H*128] bf16.  kv_layer: this layer's pool base.
 void launch_attn_decode(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
@@ -159,9 +153,6 @@ void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, co
 size_t attn_decode_ws_bytes(int B, int H, int max_ctx);
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV,
                          float scale, u16* out, hipStream_t s);
-// attn_prefill.hip; false (nothing launched) if the kernel cannot get its 128 KiB of LDS
-bool launch_attn_prefill_w64(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale,
-                             u16* out, hipStream_t s);
 
 // sets the thread-local message of inferd_last_error() and returns `code` (span.hip)
 int inferd_fail(int code, const std::string& msg);

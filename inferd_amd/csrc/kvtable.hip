@@ -193,3 +193,67 @@ extern "C" int inferd_kv_build_batch(const InferdKvTable* t, const uint64_t* seq
                      base + (n + 1 + 2 * m), base + (n + 1 + 2 * m + n)};
   return INFERD_OK;
 }
+
+// The decode-graph descriptor (inferd_span_graph_capture with advance = 1): every sequence gets
+// pages for n_steps more tokens (all or nothing), positions and slots start at 0 (the graph's
+// device-side scheduler step writes them before each replay), ctx_lens = the cached lengths
+// and max_ctx_len = the capacity, max(length) + n_steps.
+namespace {
+int decode_shape(const InferdKvTable* t, const uint64_t* seqs, int32_t n, int32_t n_steps, int32_t* max_pages,
+                 int32_t* need_pages) {
+  if (!t || n <= 0 || !seqs || n_steps <= 0) return inferd_fail(INFERD_ERR_ARG, "kv decode batch: bad argument");
+  int32_t mp = 1, need = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    auto it = t->seqs.find(seqs[i]);
+    if (it == t->seqs.end()) return inferd_fail(INFERD_ERR_ARG, "kv decode batch: sequence not reserved");
+    for (int32_t j = 0; j < i; ++j)
+      if (seqs[j] == seqs[i]) return inferd_fail(INFERD_ERR_ARG, "kv decode batch: a sequence may appear only once");
+    const int32_t pg = pages_for((int64_t)it->second.length + n_steps);
+    need += std::max(0, pg - (int32_t)it->second.pages.size());
+    mp = std::max(mp, std::max(pg, (int32_t)it->second.pages.size()));
+  }
+  *max_pages = mp;
+  *need_pages = need;
+  return INFERD_OK;
+}
+}  // namespace
+
+extern "C" int64_t inferd_kv_decode_batch_words(const InferdKvTable* t, const uint64_t* seqs, int32_t n,
+                                                int32_t n_steps) {
+  int32_t mp, need;
+  if (decode_shape(t, seqs, n, n_steps, &mp, &need) != INFERD_OK) return -1;
+  return (int64_t)n + 1 + 2 * (int64_t)n + n + (int64_t)n * mp;
+}
+
+extern "C" int inferd_kv_build_decode_batch(InferdKvTable* t, const uint64_t* seqs, int32_t n, int32_t n_steps,
+                                            int32_t* host, int64_t words, const void* device_base, InferdBatch* out) {
+  int32_t mp, need;
+  if (int rc = decode_shape(t, seqs, n, n_steps, &mp, &need); rc != INFERD_OK) return rc;
+  const int64_t want = (int64_t)n + 1 + 2 * (int64_t)n + n + (int64_t)n * mp;
+  if (!host || !out || words < want) return inferd_fail(INFERD_ERR_ARG, "kv_build_decode_batch: host buffer too small");
+  if (need > (int32_t)t->free.size())
+    return inferd_fail(INFERD_ERR_NOMEM, "KV pool exhausted: need " + std::to_string(need) + " pages, " +
+                                             std::to_string(t->free.size()) + " free of " + std::to_string(t->n_pages));
+  for (int32_t i = 0; i < n; ++i)
+    if (int rc = inferd_kv_reserve(t, seqs[i], n_steps); rc != INFERD_OK) return rc;  // cannot fail: checked above
+  // [seq_start n+1 | positions n | slots n | ctx_lens n | block_table n x mp]
+  int32_t* seq_start = host;
+  int32_t* pos = seq_start + n + 1;
+  int32_t* slots = pos + n;
+  int32_t* ctx = slots + n;
+  int32_t* table = ctx + n;
+  std::fill(host, host + want, 0);
+  int32_t max_len = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    const auto& s = t->seqs.at(seqs[i]);
+    seq_start[i] = i;
+    ctx[i] = s.length;
+    max_len = std::max(max_len, s.length);
+    std::copy(s.pages.begin(), s.pages.end(), table + (int64_t)i * mp);
+  }
+  seq_start[n] = n;
+  const int32_t* base = (const int32_t*)device_base;
+  *out = InferdBatch{n, n, 1, max_len + n_steps, mp, 1, base, base + (n + 1), base + (2 * n + 1), base + (3 * n + 1),
+                     base + (4 * n + 1)};
+  return INFERD_OK;
+}

@@ -36,6 +36,11 @@ int inferd_fail(int code, const std::string& msg) { return fail(code, msg); }
       return fail(INFERD_ERR_HIP, std::string(#expr " failed: ") + hipGetErrorString(_e)); \
   } while (0)
 
+#define GEMM_TRY(call)                                                                      \
+  do {                                                                                      \
+    if (!(call)) return fail(INFERD_ERR_ARG, "internal: GEMM combination without a body"); \
+  } while (0)
+
 #define LAUNCH_CHECK()                                                                            \
   do {                                                                                            \
     hipError_t _e = hipGetLastError();                                                            \
@@ -65,8 +70,6 @@ const uint32_t T_EMBED = 0xFFFF0000u, T_NORM = 0xFFFF0001u, T_LM = 0xFFFF0002u;
 const float LINEAR_SCALE = 0.034641016151377546f;  // float32(0.02 * sqrt(3))
 const float NORM_SCALE = 0.1f;
 
-#define QKV_KSL_MAX 4  // decode q/k/v K-slices (qkv_split)
-
 // kernel classes timed by inferd_span_profile_* (order = INFERD_PROF_* in the header)
 enum { PROF_NORM = 0, PROF_QKV, PROF_ROPE, PROF_ATTN, PROF_O, PROF_GATEUP, PROF_DOWN, PROF_LMHEAD, PROF_NCLS };
 
@@ -74,40 +77,10 @@ uint64_t tensor_key(uint64_t seed, uint32_t tid) {
   return splitmix64(((seed & 0xFFFFFFFFull) << 32) | (uint64_t)tid);
 }
 
-// A/B and lab settings, read from the environment once, at inferd_span_create (never on the
-// forward path).  Defaults are the measured optimum.
-struct Knobs {
-  bool fuse_decode_rope = true;  // INFERD_FUSE_DECODE_ROPE=0: separate qk_norm_rope_kv launch on decode
-  bool pack_act = true;          // INFERD_PACK_ACT=0: row-major decode activations
-  int qkv_split = 2;             // INFERD_QKV_SPLIT: decode q/k/v K-slices (reduced by the attention)
-  bool fuse_qkv_epi = true;      // INFERD_FUSE_QKV_EPI=0: prefill q/k norm + RoPE + cache write as a launch
-  int gemm_split = 1;            // INFERD_GEMM_SPLIT=0: no prefill tail split
-  int attn_nw = 0, attn_nc = 0;  // INFERD_ATTN_NW / _NC: decode attention shape (0: default)
-  int attn_qlanes = 0;           // INFERD_ATTN_QLANES=1: per-lane q loads in the fused decode attention
-  int attn_order = -1;           // INFERD_ATTN_ORDER: prefill block order (-1: default)
-  int attn_prefill = 0;          // INFERD_ATTN_PREFILL: 1 = one-wave-per-SIMD prefill attention, 2 = 32 rows per wave, 6 = three WGs/CU
-};
-
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
-
-Knobs knobs_from_env() {
-  Knobs k;
-  k.fuse_decode_rope = env_int("INFERD_FUSE_DECODE_ROPE", 1) != 0;
-  k.pack_act = env_int("INFERD_PACK_ACT", 1) != 0;
-  k.qkv_split = env_int("INFERD_QKV_SPLIT", 2);
-  if (k.qkv_split < 1 || k.qkv_split > QKV_KSL_MAX) k.qkv_split = 1;
-  k.fuse_qkv_epi = env_int("INFERD_FUSE_QKV_EPI", 1) != 0;
-  k.gemm_split = env_int("INFERD_GEMM_SPLIT", 1) != 0;
-  k.attn_nw = env_int("INFERD_ATTN_NW", 0);
-  k.attn_nc = env_int("INFERD_ATTN_NC", 0);
-  k.attn_qlanes = env_int("INFERD_ATTN_QLANES", 0);
-  k.attn_order = env_int("INFERD_ATTN_ORDER", -1);
-  k.attn_prefill = env_int("INFERD_ATTN_PREFILL", 0);
-  return k;
-}
+// Decode q/k/v K-slices (reduced by the fused decode attention): the measured optimum
+// (other slice counts, like every other A/B variant, live in tools/ lab
+// builds -- the product library has one path per op and reads no environment).
+#define QKV_KSL 2
 
 }  // namespace
 
@@ -126,7 +99,6 @@ struct InferdSpan {
       *last = nullptr;
   float* attn_ws = nullptr;
   size_t attn_ws_bytes = 0;
-  Knobs knobs;
   // RMSNorms at the reference's rounding points (qwen3_server_module.py:19-25).  On the decode
   // GEMV path (<= 64 rows) the o and down GEMVs add the row sums of squares of their outputs
   // into SSQ slots (kernels.h DecodeNorm; slot 2l: layer l's o -> its gate/up, slot 2l+1: layer
@@ -135,7 +107,7 @@ struct InferdSpan {
   // span's first layer, prefill) rmsnorm_kernel writes the normed rows to xn.
   unsigned long long* ssq = nullptr;
   GemmWs gws;                 // prefill tail-split workspace (per span: spans never share tickets)
-  float* qkv_part = nullptr;  // decode split-K q/k/v partials [QKV_KSL_MAX][16][qkv_rows]
+  float* qkv_part = nullptr;  // decode split-K q/k/v partials [QKV_KSL][16][qkv_rows]
   unsigned long long* argmax_partial = nullptr;
   int32_t* err = nullptr;
   // set by inferd_span_graph_capture(advance): the scheduler step the next forward's first
@@ -200,7 +172,6 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   if (c.kv_pages > (1 << 24)) return fail(INFERD_ERR_ARG, "kv_pages must be <= 2^24");
   InferdSpan* s = new InferdSpan();
   s->cfg = c;
-  s->knobs = knobs_from_env();
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
   s->layers.resize(c.n_layers);
   int rc = 0;
@@ -266,10 +237,10 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   SALLOC(s->ssq, (size_t)(2 * c.n_layers) * SSQ_SLOT_WORDS * 8);
   if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
-  SALLOC(s->qkv_part, (size_t)QKV_KSL_MAX * 16 * s->qkv_rows() * 4);
+  SALLOC(s->qkv_part, (size_t)QKV_KSL * 16 * s->qkv_rows() * 4);
   // the prefill tail split's workspace, once (a forward never allocates): only spans whose
   // calls can reach the 256x256 GEMMs (>= 512 rows) need it
-  s->gws.split = s->knobs.gemm_split && c.max_tokens >= 512;
+  s->gws.split = c.max_tokens >= 512;
   if (gemm_ws_alloc(&s->gws) != (int)hipSuccess) return bail(fail(INFERD_ERR_HIP, "tail-split workspace allocation failed"));
   SALLOC(s->err, 256);
   if (hipMemset(s->err, 0, 4) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
@@ -280,6 +251,12 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
 }
 
 extern "C" void inferd_span_destroy(InferdSpan* span) { delete span; }
+
+extern "C" int inferd_span_get_config(const InferdSpan* span, InferdSpanConfig* out) {
+  if (!span || !out) return fail(INFERD_ERR_ARG, "null argument");
+  *out = span->cfg;
+  return INFERD_OK;
+}
 
 // ------------------------------------------------------------------ weights
 namespace {
@@ -402,14 +379,9 @@ static int check_batch(const InferdSpan* s, const InferdBatch* b) {
   return INFERD_OK;
 }
 
-// the attention's view of a batch; `kn` (a span's knobs) sets its launch-shape overrides
-static AttnBatch to_attn(const InferdBatch* b, const Knobs& kn = Knobs{}) {
+// the attention's view of a batch
+static AttnBatch to_attn(const InferdBatch* b) {
   AttnBatch a;
-  a.nw = kn.attn_nw;
-  a.nc = kn.attn_nc;
-  a.qlanes = kn.attn_qlanes;
-  a.order = kn.attn_order;
-  a.pfk = kn.attn_prefill;
   a.seq_start = b->seq_start;
   a.positions = b->positions;
   a.ctx_lens = b->ctx_lens;
@@ -429,7 +401,6 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   int rc = check_batch(s, b);
   if (rc) return rc;
   const InferdSpanConfig& c = s->cfg;
-  const Knobs& kn = s->knobs;
   hipStream_t st = (hipStream_t)stream;
   const int M = b->n_tokens, B = b->n_seqs;
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
@@ -461,7 +432,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   }
   if (c.n_layers == 0 && x_out && x != x_out)
     HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
-  const AttnBatch ab = to_attn(b, kn);
+  const AttnBatch ab = to_attn(b);
   // RMSNorms (qwen3_server_module.py:19-25, :173-176): see InferdSpan::ssq_in.  gemv: every
   // projection of this call is a decode GEMV (<= 64 rows), so the o / down GEMVs can hand the
   // next norm its row sums of squares.
@@ -470,16 +441,17 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   // decode: the residual stream between layers (and h1 inside a layer) fragment-packed
   // (common.h packed_index) for the GEMVs that read it; the input and the last layer's
   // output stay row-major, and so does every layer's output when layer_out asks for them
-  const bool pkx = gemv && kn.pack_act && !layer_out && h % 128 == 0 && I % 128 == 0;
+  const bool pkx = gemv && !layer_out && h % 128 == 0 && I % 128 == 0;
   bool x_packed = false;  // x (this layer's input) is fragment-packed
   long pe = -1;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
     u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
-    const bool fused = b->decode && kn.fuse_decode_rope;
+    // decode: QK-norm + RoPE + the cache write run inside the attention
+    const bool fused = b->decode;
     // decode q/k/v K-slices (reduced inside the fused attention): M <= 16 and K/32 divisible
     // by 4 * slices
-    int ksl = (fused && M <= 16) ? kn.qkv_split : 1;
+    int ksl = (fused && M <= 16) ? QKV_KSL : 1;
     if ((h / 32) % (4 * ksl)) ksl = 1;
     // ---- input_layernorm -> q/k/v projection
     const u16* a_in = x;
@@ -501,18 +473,18 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       launch_gemm_decode_partial(a_in, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, dn, st,
                                  (x_packed && a_in == x) ? GEMM_PACK_A : 0);
     } else {
-      if (!b->decode && kn.fuse_qkv_epi) {
+      if (!b->decode) {
         const QkvEpilogue qe = {b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t, s->sin_t, s->q, kv_l,
                                 H, KV, c.rms_eps};
         qkv_done = launch_gemm_qkv_fused(a_in, h, W.qkv, M, qkvN, h, qe, st);
       }
       if (!qkv_done)
-        launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &s->gws, &dn,
-                    nullptr, (x_packed && a_in == x) ? GEMM_PACK_A : 0);
+        GEMM_TRY(launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &s->gws, &dn,
+                    nullptr, (x_packed && a_in == x) ? GEMM_PACK_A : 0));
     }
     s->prof_end(pe, st);
     // decode: the attention output goes to the o projection's GEMV fragment-packed
-    const bool pk_o = fused && gemv && kn.pack_act && !gemm_uses_tiled(M, h, H * HEAD_DIM, EPI_RESID);
+    const bool pk_o = fused && gemv && !gemm_uses_tiled(M, h, H * HEAD_DIM, EPI_RESID);
     if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
       if (ksl > 1)
@@ -530,10 +502,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
         s->prof_end(pe, st);
       }
       pe = s->prof_begin(PROF_ATTN, st);
-      if (b->decode)
-        launch_attn_decode(s->q, kv_l, ab, H, KV, scale, s->attn, s->attn_ws, st);
-      else
-        launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
+      launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
       s->prof_end(pe, st);
     }
     // ---- h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
@@ -545,9 +514,9 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     const bool out_packed = pkx && l < c.n_layers - 1;
     u16* h1 = (pkx && ((x == s->h && !x_packed) || (out == s->h && !out_packed))) ? s->xn : s->h;
     pe = s->prof_begin(PROF_O, st);
-    launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
+    GEMM_TRY(launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
                 gemv ? slot(2 * l) : nullptr,
-                (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (pkx ? GEMM_PACK_C : 0));
+                (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (pkx ? GEMM_PACK_C : 0)));
     s->prof_end(pe, st);
     // ---- post_attention_layernorm -> gate/up (+SwiGLU)
     const u16* m_in = h1;
@@ -563,15 +532,15 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pe = s->prof_begin(PROF_GATEUP, st);
     // decode (the GEMV path): act goes between gate/up and down fragment-packed
     const int pk =
-        (gemv && kn.pack_act && !gemm_uses_tiled(M, I, h, EPI_SILU) && !gemm_uses_tiled(M, h, I, EPI_RESID)) ? 1 : 0;
-    launch_gemm(m_in, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, &s->gws, &dm, nullptr,
-                (pk ? GEMM_PACK_C : 0) | ((pkx && m_in == h1) ? GEMM_PACK_A : 0));
+        (gemv && !gemm_uses_tiled(M, I, h, EPI_SILU) && !gemm_uses_tiled(M, h, I, EPI_RESID)) ? 1 : 0;
+    GEMM_TRY(launch_gemm(m_in, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, &s->gws, &dm, nullptr,
+                (pk ? GEMM_PACK_C : 0) | ((pkx && m_in == h1) ? GEMM_PACK_A : 0)));
     s->prof_end(pe, st);
     // ---- x = h1 + down(act)
     pe = s->prof_begin(PROF_DOWN, st);
-    launch_gemm(s->act, I, W.down, M, h, I, out, h, h1, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
+    GEMM_TRY(launch_gemm(s->act, I, W.down, M, h, I, out, h, h1, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
                 (gemv && l + 1 < c.n_layers) ? slot(2 * l + 1) : nullptr,
-                (pk ? GEMM_PACK_A : 0) | (pkx ? GEMM_PACK_R : 0) | (out_packed ? GEMM_PACK_C : 0));
+                (pk ? GEMM_PACK_A : 0) | (pkx ? GEMM_PACK_R : 0) | (out_packed ? GEMM_PACK_C : 0)));
     s->prof_end(pe, st);
     x = out;
     x_packed = out_packed;
@@ -587,10 +556,10 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // the final norm writes the last rows fragment-packed for the lm_head GEMV (its A operand
     // only; the logits it may also store stay row-major).  Folding this norm into the GEMV's A
     // path (DN_EXACT, as q/k/v) measured 213.8 us in the graph against 195 + 5 us (round 3).
-    const bool pk_last = kn.pack_act && h % 32 == 0;
+    const bool pk_last = h % 32 == 0;
     launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, s->last, h, B, h, c.rms_eps, st, pk_last);
-    launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
-                s->argmax_partial, st, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0);
+    GEMM_TRY(launch_gemm(s->last, h, s->lm_head, B, c.vocab, h, (u16*)logits, c.vocab, nullptr, 0, EPI_ARGMAX,
+                s->argmax_partial, st, nullptr, nullptr, nullptr, pk_last ? GEMM_PACK_A : 0));
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
     s->prof_end(pe, st);
   }
@@ -607,8 +576,8 @@ extern "C" int inferd_span_lm_head(InferdSpan* s, const void* x, int32_t rows, v
   if (rows > c.max_tokens) return fail(INFERD_ERR_ARG, "rows > max_tokens");
   hipStream_t st = (hipStream_t)stream;
   launch_rmsnorm((const u16*)x, c.hidden, nullptr, 0, s->final_norm, s->xn, c.hidden, rows, c.hidden, c.rms_eps, st);
-  launch_gemm(s->xn, c.hidden, s->lm_head, rows, c.vocab, c.hidden, (u16*)logits, c.vocab, nullptr, 0, EPI_NONE,
-              nullptr, st, &s->gws);
+  GEMM_TRY(launch_gemm(s->xn, c.hidden, s->lm_head, rows, c.vocab, c.hidden, (u16*)logits, c.vocab, nullptr, 0, EPI_NONE,
+              nullptr, st, &s->gws));
   LAUNCH_CHECK();
   return INFERD_OK;
 }
@@ -767,17 +736,19 @@ extern "C" int inferd_gemm(const void* a, const void* w, void* c, const void* r,
   if (!a || !w || !c || m <= 0 || n % 16 || k % 32) return fail(INFERD_ERR_ARG, "gemm needs n%16==0, k%32==0");
   if (epi < 0 || epi > 2) return fail(INFERD_ERR_ARG, "bad epilogue");
   if (epi == INFERD_EPI_RESID && !r) return fail(INFERD_ERR_ARG, "resid epilogue needs R");
-  // the op API's own tail-split workspace (per host thread, allocated on its first use;
-  // spans keep theirs); INFERD_GEMM_SPLIT=0 runs this call without the split (tests)
-  static thread_local GemmWs op_ws;
-  if (!op_ws.ws) {
-    op_ws.split = 1;
-    if (gemm_ws_alloc(&op_ws) != (int)hipSuccess) return fail(INFERD_ERR_HIP, "tail-split workspace allocation failed");
+  // the op API's own tail-split workspace: one per host thread, allocated on its first use and
+  // freed when the thread exits (spans keep theirs)
+  struct OpWs {
+    GemmWs w;
+    ~OpWs() { gemm_ws_free(&w); }
+  };
+  static thread_local OpWs op_ws;
+  if (!op_ws.w.ws) {
+    op_ws.w.split = 1;
+    if (gemm_ws_alloc(&op_ws.w) != (int)hipSuccess) return fail(INFERD_ERR_HIP, "tail-split workspace allocation failed");
   }
-  GemmWs call_ws = op_ws;
-  call_ws.split = env_int("INFERD_GEMM_SPLIT", 1) != 0;
-  launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr,
-              (hipStream_t)stream, &call_ws);
+  GEMM_TRY(launch_gemm((const u16*)a, k, (const u16*)w, m, n, k, (u16*)c, n, (const u16*)r, n, epi, nullptr,
+              (hipStream_t)stream, &op_ws.w));
   LAUNCH_CHECK();
   return INFERD_OK;
 }
@@ -819,7 +790,7 @@ extern "C" int64_t inferd_attention_workspace_bytes(int32_t n_seqs, int32_t head
 extern "C" int inferd_attention(const void* q, const void* kv_layer, const InferdBatch* b, int32_t H,
                                 int32_t KV, void* out, void* ws, int64_t ws_bytes, void* stream) {
   if (!q || !kv_layer || !b || !out || KV <= 0 || H % KV || H / KV > 16) return fail(INFERD_ERR_ARG, "bad attention args");
-  const AttnBatch ab = to_attn(b, knobs_from_env());  // single-op API (tests, labs): env read per call
+  const AttnBatch ab = to_attn(b);
   const float scale = 1.0f / sqrtf((float)HEAD_DIM);
   if (b->decode) {
     if (!ws || ws_bytes < (int64_t)attn_decode_ws_bytes(b->n_seqs, H, b->max_ctx_len))

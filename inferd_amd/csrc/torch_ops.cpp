@@ -1,14 +1,18 @@
 // PyTorch-ROCm operator registration of the span engine's C-ABI (include/inferd_span.h):
-// torch.ops.inferd.* for torch hosts (BASELINE north_star: "a thin C-ABI layer exposed as a
-// PyTorch-ROCm extension").  Every op is a direct call of one
-// extern "C" entry point of libinferd_span.so on torch's current HIP stream of the tensors'
-// device; an INFERD_ERR_* status becomes a RuntimeError carrying inferd_last_error() (the
-// reference's exceptions reach aiohttp the same way, partitioned_models.py:137 / task.py:54).
-// Handles (InferdSpan*, InferdKvTable*, InferdGraph*) cross as int64.  Non-torch hosts bind the
-// same C-ABI directly (ctypes: inferd_amd/_lib.py; C: tests/c_abi/kv_host.c).
+// torch.ops.inferd.* and torch.classes.inferd.DecodeGraph, the binding the node-facing host
+// (inferd_amd/runtime.py) drives the engine through (BASELINE north_star: "a thin C-ABI layer
+// exposed as a PyTorch-ROCm extension").  Every op is a direct
+// call of extern "C" entry points of libinferd_span.so on torch's current HIP stream of the
+// tensors' device; an INFERD_ERR_* status becomes a RuntimeError carrying inferd_last_error()
+// (the reference's exceptions reach aiohttp the same way, partitioned_models.py:137 /
+// task.py:54).  Span and page-table handles cross as int64.  Every tensor argument is checked
+// against the batch shape and the span's configuration before a kernel can touch it.
+// Non-torch hosts bind the same C-ABI directly (ctypes: inferd_amd/_lib.py; C:
+// tests/c_abi/kv_host.c).
 #include <ATen/ATen.h>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
+#include <torch/custom_class.h>
 #include <torch/library.h>
 
 #include <string>
@@ -28,15 +32,24 @@ T* handle(int64_t h, const char* what) {
   return reinterpret_cast<T*>(h);
 }
 
-void* stream_of(const at::Tensor& t) { return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+void* stream_of(at::Device d) { return (void*)c10::hip::getCurrentHIPStream(d.index()).stream(); }
 
 const void* opt_ptr(const std::optional<at::Tensor>& t) { return t ? t->data_ptr() : nullptr; }
 
-void check_dev(const std::optional<at::Tensor>& t, const at::Tensor& ref, at::ScalarType dt, const char* name) {
+InferdSpanConfig config_of(InferdSpan* s) {
+  InferdSpanConfig c;
+  ok(inferd_span_get_config(s, &c), "span_get_config");
+  return c;
+}
+
+// device, dtype, contiguity and the minimum element count of an optional tensor argument
+void check_arg(const std::optional<at::Tensor>& t, at::Device dev, at::ScalarType dt, int64_t min_numel,
+               const char* name) {
   if (!t) return;
-  TORCH_CHECK(t->device() == ref.device(), name, " must be on ", ref.device());
-  TORCH_CHECK(t->scalar_type() == dt, name, " has the wrong dtype");
+  TORCH_CHECK(t->device() == dev, name, " must be on ", dev, " (is on ", t->device(), ")");
+  TORCH_CHECK(t->scalar_type() == dt, name, " must be ", dt, " (is ", t->scalar_type(), ")");
   TORCH_CHECK(t->is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t->numel() >= min_numel, name, " has ", t->numel(), " elements, the call needs ", min_numel);
 }
 
 // the InferdBatch view of a device int32 descriptor [seq_start | positions | slots | ctx_lens |
@@ -47,10 +60,29 @@ InferdBatch batch_of(const at::Tensor& words, at::IntArrayRef shape) {
   TORCH_CHECK(words.scalar_type() == at::kInt && words.is_contiguous() && words.is_cuda(),
               "batch words: a contiguous int32 device tensor");
   const int64_t n = shape[0], m = shape[1], mp = shape[4];
+  TORCH_CHECK(n > 0 && m > 0 && mp > 0, "batch shape: empty batch");
   TORCH_CHECK(words.numel() >= n + 1 + 2 * m + n + n * mp, "batch words: too few for the shape");
   const int32_t* w = words.data_ptr<int32_t>();
   return InferdBatch{(int32_t)n, (int32_t)m, (int32_t)shape[2], (int32_t)shape[3], (int32_t)mp, (int32_t)shape[5],
                      w, w + n + 1, w + n + 1 + m, w + n + 1 + 2 * m, w + n + 1 + 2 * m + n};
+}
+
+// every buffer of one span forward over `b` against the span's sizes
+void check_forward_args(const InferdSpanConfig& c, const at::Tensor& words, const InferdBatch& b,
+                        const std::optional<at::Tensor>& ids, const std::optional<at::Tensor>& x,
+                        const std::optional<at::Tensor>& x_out, const std::optional<at::Tensor>& next_ids,
+                        const std::optional<at::Tensor>& logits, const std::optional<at::Tensor>& layers) {
+  const at::Device dev = words.device();
+  const int64_t M = b.n_tokens, B = b.n_seqs, h = c.hidden;
+  TORCH_CHECK(!c.has_embed || ids, "a first span needs ids");
+  TORCH_CHECK(c.has_embed || x, "a span without the embedding needs x");
+  TORCH_CHECK(c.has_lm_head || (!next_ids && !logits), "next_ids / logits need a span with lm_head");
+  check_arg(ids, dev, at::kInt, M, "ids");
+  check_arg(x, dev, at::kBFloat16, M * h, "x");
+  check_arg(x_out, dev, at::kBFloat16, M * h, "x_out");
+  check_arg(next_ids, dev, at::kInt, B, "next_ids");
+  check_arg(logits, dev, at::kBFloat16, B * (int64_t)c.vocab, "logits");
+  check_arg(layers, dev, at::kBFloat16, (int64_t)c.n_layers * M * h, "layers");
 }
 
 // ---- span lifetime ------------------------------------------------------------------------
@@ -71,80 +103,88 @@ int64_t span_create(at::IntArrayRef cfg, double rms_eps, double rope_theta, at::
 
 void span_destroy(int64_t span) { inferd_span_destroy(handle<InferdSpan>(span, "span_destroy")); }
 
+std::vector<int64_t> span_config(int64_t span) {
+  const InferdSpanConfig c = config_of(handle<InferdSpan>(span, "span_config"));
+  return {c.hidden, c.intermediate, c.heads, c.kv_heads, c.head_dim, c.vocab, c.first_layer, c.n_layers,
+          c.has_embed, c.has_lm_head, c.max_positions, c.kv_pages, c.max_tokens, c.max_seqs};
+}
+
 void span_init_synthetic(int64_t span, int64_t seed, at::Device device) {
+  TORCH_CHECK(device.is_cuda(), "span_init_synthetic: a GPU device");
   c10::hip::HIPGuard g(device.index());
-  ok(inferd_span_init_synthetic(handle<InferdSpan>(span, "span_init_synthetic"), (uint64_t)seed,
-                                (void*)c10::hip::getCurrentHIPStream(device.index()).stream()),
+  ok(inferd_span_init_synthetic(handle<InferdSpan>(span, "span_init_synthetic"), (uint64_t)seed, stream_of(device)),
      "span_init_synthetic");
 }
 
 void span_set_weight(int64_t span, int64_t layer, std::string name, const at::Tensor& w) {
   TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.is_contiguous(), "set_weight: contiguous bf16 GPU tensor");
+  TORCH_CHECK(w.dim() == 1 || w.dim() == 2, "set_weight: a 1-D or 2-D tensor");
   c10::hip::HIPGuard g(w.device().index());
   const int64_t rows = w.dim() == 1 ? 1 : w.size(0), cols = w.dim() == 1 ? w.size(0) : w.size(1);
+  // the library checks (rows, cols) against the named weight's shape
   ok(inferd_span_set_weight(handle<InferdSpan>(span, "span_set_weight"), (int32_t)layer, name.c_str(), w.data_ptr(),
-                            rows, cols, stream_of(w)),
+                            rows, cols, stream_of(w.device())),
      "span_set_weight");
+}
+
+// sticky device error flags, read and cleared (synchronises the device)
+int64_t span_error_flags(int64_t span, at::Device device) {
+  TORCH_CHECK(device.is_cuda(), "span_error_flags: a GPU device");
+  c10::hip::HIPGuard g(device.index());
+  int32_t f = 0;
+  ok(inferd_span_error_flags(handle<InferdSpan>(span, "span_error_flags"), &f), "span_error_flags");
+  return f;
+}
+
+void span_profile_start(int64_t span, int64_t max_pairs) {
+  ok(inferd_span_profile_start(handle<InferdSpan>(span, "span_profile_start"), (int32_t)max_pairs), "span_profile_start");
+}
+
+// per kernel class (INFERD_PROF_* order): total ms and launch counts since profile_start
+std::tuple<std::vector<double>, std::vector<int64_t>> span_profile_stop(int64_t span, int64_t n_classes) {
+  std::vector<double> ms(n_classes, 0.0);
+  std::vector<int32_t> cnt(n_classes, 0);
+  ok(inferd_span_profile_stop(handle<InferdSpan>(span, "span_profile_stop"), ms.data(), cnt.data(), (int32_t)n_classes),
+     "span_profile_stop");
+  return {ms, std::vector<int64_t>(cnt.begin(), cnt.end())};
 }
 
 // ---- forward -------------------------------------------------------------------------------
 void span_forward(int64_t span, const at::Tensor& words, at::IntArrayRef shape, const std::optional<at::Tensor>& ids,
                   const std::optional<at::Tensor>& x, const std::optional<at::Tensor>& x_out,
-                  const std::optional<at::Tensor>& next_ids, const std::optional<at::Tensor>& logits) {
-  check_dev(ids, words, at::kInt, "ids");
-  check_dev(x, words, at::kBFloat16, "x");
-  check_dev(x_out, words, at::kBFloat16, "x_out");
-  check_dev(next_ids, words, at::kInt, "next_ids");
-  check_dev(logits, words, at::kBFloat16, "logits");
-  c10::hip::HIPGuard g(words.device().index());
+                  const std::optional<at::Tensor>& next_ids, const std::optional<at::Tensor>& logits,
+                  const std::optional<at::Tensor>& layers) {
+  InferdSpan* s = handle<InferdSpan>(span, "span_forward");
   const InferdBatch b = batch_of(words, shape);
-  ok(inferd_span_forward(handle<InferdSpan>(span, "span_forward"), &b, (const int32_t*)opt_ptr(ids), opt_ptr(x),
-                         (void*)opt_ptr(x_out), (int32_t*)opt_ptr(next_ids), (void*)opt_ptr(logits), nullptr,
-                         stream_of(words)),
+  check_forward_args(config_of(s), words, b, ids, x, x_out, next_ids, logits, layers);
+  c10::hip::HIPGuard g(words.device().index());
+  ok(inferd_span_forward(s, &b, (const int32_t*)opt_ptr(ids), opt_ptr(x), (void*)opt_ptr(x_out),
+                         (int32_t*)opt_ptr(next_ids), (void*)opt_ptr(logits), (void*)opt_ptr(layers),
+                         stream_of(words.device())),
      "span_forward");
 }
 
+// final norm + lm_head over every row of x [rows, hidden] -> logits [rows, vocab]
 void span_lm_head(int64_t span, const at::Tensor& x, const at::Tensor& logits) {
-  check_dev(logits, x, at::kBFloat16, "logits");
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(), "x: contiguous bf16");
+  InferdSpan* s = handle<InferdSpan>(span, "span_lm_head");
+  const InferdSpanConfig c = config_of(s);
+  TORCH_CHECK(x.is_cuda(), "span_lm_head: x must be on a GPU");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) == c.hidden, "span_lm_head: x must be [rows, ", c.hidden, "]");
+  check_arg(x, x.device(), at::kBFloat16, 0, "x");
+  check_arg(logits, x.device(), at::kBFloat16, x.size(0) * (int64_t)c.vocab, "logits");
   c10::hip::HIPGuard g(x.device().index());
-  ok(inferd_span_lm_head(handle<InferdSpan>(span, "span_lm_head"), x.data_ptr(), (int32_t)x.size(0), logits.data_ptr(),
-                         stream_of(x)),
-     "span_lm_head");
+  ok(inferd_span_lm_head(s, x.data_ptr(), (int32_t)x.size(0), logits.data_ptr(), stream_of(x.device())), "span_lm_head");
 }
 
-// decode graphs: capture with the device-side scheduler step (advance = 1), replay, destroy
-int64_t graph_capture(int64_t span, const at::Tensor& words, at::IntArrayRef shape, const std::optional<at::Tensor>& ids,
-                      const std::optional<at::Tensor>& x, const std::optional<at::Tensor>& x_out,
-                      const std::optional<at::Tensor>& next_ids, const std::optional<at::Tensor>& logits) {
-  c10::hip::HIPGuard g(words.device().index());
-  const InferdBatch b = batch_of(words, shape);
-  // capture on a side stream (the legacy default stream cannot capture)
-  c10::hip::HIPStream cs = c10::hip::getStreamFromPool(false, words.device().index());
-  hipStream_t cur = c10::hip::getCurrentHIPStream(words.device().index()).stream();
-  hipEvent_t ev;
-  TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "graph_capture: event");
-  (void)hipEventRecord(ev, cur);
-  (void)hipStreamWaitEvent(cs.stream(), ev, 0);
-  InferdGraph* gr = nullptr;
-  const int rc = inferd_span_graph_capture(handle<InferdSpan>(span, "graph_capture"), &b, 1,
-                                           (const int32_t*)opt_ptr(ids), opt_ptr(x), (void*)opt_ptr(x_out),
-                                           (int32_t*)opt_ptr(next_ids), (void*)opt_ptr(logits), (void*)cs.stream(), &gr);
-  (void)hipEventRecord(ev, cs.stream());
-  (void)hipStreamWaitEvent(cur, ev, 0);
-  (void)hipEventDestroy(ev);
-  ok(rc, "graph_capture");
-  return reinterpret_cast<int64_t>(gr);
+// one synthetic weight tensor (the counter-based generator; oracle/weightgen.py defines the same values)
+void weightgen(const at::Tensor& dst, int64_t seed, int64_t tensor_id, double scale, double center) {
+  TORCH_CHECK(dst.is_cuda() && dst.scalar_type() == at::kBFloat16 && dst.is_contiguous(),
+              "weightgen: contiguous bf16 GPU tensor");
+  c10::hip::HIPGuard g(dst.device().index());
+  ok(inferd_weightgen(dst.data_ptr(), dst.numel(), (uint64_t)seed, (uint32_t)tensor_id, (float)scale, (float)center,
+                      stream_of(dst.device())),
+     "weightgen");
 }
-
-void graph_launch(int64_t graph, at::Device device) {
-  c10::hip::HIPGuard g(device.index());
-  ok(inferd_graph_launch(handle<InferdGraph>(graph, "graph_launch"),
-                         (void*)c10::hip::getCurrentHIPStream(device.index()).stream()),
-     "graph_launch");
-}
-
-void graph_destroy(int64_t graph) { inferd_graph_destroy(handle<InferdGraph>(graph, "graph_destroy")); }
 
 // ---- KV page table (host only) -------------------------------------------------------------
 int64_t kv_create(int64_t n_pages) {
@@ -175,6 +215,21 @@ std::tuple<int64_t, int64_t> kv_query(int64_t table, int64_t seq) {
   return {len, np};
 }
 
+std::vector<int64_t> kv_pages(int64_t table, int64_t seq) {
+  auto* t = handle<InferdKvTable>(table, "kv_pages");
+  int32_t len = 0, np = 0;
+  ok(inferd_kv_query(t, (uint64_t)seq, &len, &np), "kv_pages");
+  std::vector<int32_t> p(np > 0 ? np : 1);
+  ok(inferd_kv_pages(t, (uint64_t)seq, p.data(), np), "kv_pages");
+  return std::vector<int64_t>(p.begin(), p.begin() + np);
+}
+
+int64_t kv_free_pages(int64_t table) {
+  int32_t f = 0;
+  ok(inferd_kv_free_pages(handle<InferdKvTable>(table, "kv_free_pages"), &f), "kv_free_pages");
+  return f;
+}
+
 // the batch of `seqs` (n_new new tokens each) as (device int32 words, shape) for span_forward
 std::tuple<at::Tensor, std::vector<int64_t>> kv_build_batch(int64_t table, at::IntArrayRef seqs, at::IntArrayRef n_new,
                                                             at::Device device) {
@@ -193,27 +248,107 @@ std::tuple<at::Tensor, std::vector<int64_t>> kv_build_batch(int64_t table, at::I
   return {dev, {b.n_seqs, b.n_tokens, b.max_q_len, b.max_ctx_len, b.max_pages, b.decode}};
 }
 
+// ---- decode graphs -------------------------------------------------------------------------
+// One decode step of a fixed set of sequences captured as a HIP graph (inferd_span_graph_capture
+// with advance = 1; the per-token client loop of client.py:244-266 / send_message.py:46-60 as one
+// replay).  The constructor reserves pages for n_steps tokens of every sequence and builds the
+// descriptor natively (inferd_kv_build_decode_batch: ctx_lens = the cached lengths, max_ctx_len =
+// the capacity), then captures on a side stream.  The object owns every buffer the graph's
+// pointers refer to -- the descriptor and the caller's ids / x / x_out / next_ids / logits -- so
+// none can be freed and reused while the graph exists.  launch() replays on the current stream
+// and advances the host page table by one token (all or nothing); more than n_steps launches
+// raise.  `ids` and `next_ids` may be one tensor (greedy feedback).
+struct DecodeGraph : torch::CustomClassHolder {
+  int64_t span = 0, table = 0, n_steps = 0, launched = 0;
+  std::vector<uint64_t> seqs;
+  at::Tensor words;
+  std::vector<at::Tensor> keep;
+  at::Device device;
+  InferdGraph* graph = nullptr;
+
+  DecodeGraph(int64_t span_, int64_t table_, std::vector<int64_t> seqs_, int64_t n_steps_,
+              std::optional<at::Tensor> ids, std::optional<at::Tensor> x, std::optional<at::Tensor> x_out,
+              std::optional<at::Tensor> next_ids, std::optional<at::Tensor> logits, at::Device device_)
+      : span(span_), table(table_), n_steps(n_steps_), device(device_) {
+    TORCH_CHECK(device.is_cuda(), "DecodeGraph: a GPU device");
+    TORCH_CHECK(!seqs_.empty() && n_steps > 0, "DecodeGraph: sequences and n_steps >= 1");
+    InferdSpan* s = handle<InferdSpan>(span, "DecodeGraph");
+    auto* t = handle<InferdKvTable>(table, "DecodeGraph");
+    seqs.assign(seqs_.begin(), seqs_.end());
+    const int32_t n = (int32_t)seqs.size();
+    const int64_t nw = inferd_kv_decode_batch_words(t, seqs.data(), n, (int32_t)n_steps);
+    TORCH_CHECK(nw > 0, "DecodeGraph: ", inferd_last_error());
+    at::Tensor host = at::empty({nw}, at::TensorOptions().dtype(at::kInt));
+    words = at::empty({nw}, at::TensorOptions().dtype(at::kInt).device(device));
+    InferdBatch b;
+    ok(inferd_kv_build_decode_batch(t, seqs.data(), n, (int32_t)n_steps, host.data_ptr<int32_t>(), nw, words.data_ptr(),
+                                    &b),
+       "DecodeGraph: kv_build_decode_batch");
+    c10::hip::HIPGuard g(device.index());
+    words.copy_(host);
+    check_forward_args(config_of(s), words, b, ids, x, x_out, next_ids, logits, std::nullopt);
+    for (const auto* o : {&ids, &x, &x_out, &next_ids, &logits})
+      if (*o) keep.push_back(**o);
+    // capture on a side stream (the legacy default stream cannot capture), ordered after the
+    // current stream's work and before its later work
+    c10::hip::HIPStream cs = c10::hip::getStreamFromPool(false, device.index());
+    hipStream_t cur = c10::hip::getCurrentHIPStream(device.index()).stream();
+    hipEvent_t ev;
+    TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "DecodeGraph: event");
+    (void)hipEventRecord(ev, cur);
+    (void)hipStreamWaitEvent(cs.stream(), ev, 0);
+    const int rc = inferd_span_graph_capture(s, &b, 1, (const int32_t*)opt_ptr(ids), opt_ptr(x), (void*)opt_ptr(x_out),
+                                             (int32_t*)opt_ptr(next_ids), (void*)opt_ptr(logits), (void*)cs.stream(),
+                                             &graph);
+    (void)hipEventRecord(ev, cs.stream());
+    (void)hipStreamWaitEvent(cur, ev, 0);
+    (void)hipEventDestroy(ev);
+    ok(rc, "DecodeGraph: graph_capture");
+  }
+  ~DecodeGraph() override {
+    if (graph) inferd_graph_destroy(graph);
+  }
+  void launch() {
+    TORCH_CHECK(launched < n_steps, "decode graph ran out of reserved steps (", n_steps, ")");
+    c10::hip::HIPGuard g(device.index());
+    ok(inferd_graph_launch(graph, stream_of(device)), "DecodeGraph.launch");
+    ++launched;
+    // the host page table follows the device-side advance: one native call per replay
+    ok(inferd_kv_advance_many(handle<InferdKvTable>(table, "DecodeGraph"), seqs.data(), (int32_t)seqs.size(), 1),
+       "DecodeGraph.launch: kv_advance");
+  }
+  int64_t steps_left() const { return n_steps - launched; }
+};
+
 }  // namespace
 
 TORCH_LIBRARY(inferd, m) {
   m.def("span_create(int[] cfg, float rms_eps, float rope_theta, Device device) -> int", &span_create);
   m.def("span_destroy(int span) -> ()", &span_destroy);
+  m.def("span_config(int span) -> int[]", &span_config);
   m.def("span_init_synthetic(int span, int seed, Device device) -> ()", &span_init_synthetic);
   m.def("span_set_weight(int span, int layer, str name, Tensor w) -> ()", &span_set_weight);
+  m.def("span_error_flags(int span, Device device) -> int", &span_error_flags);
+  m.def("span_profile_start(int span, int max_pairs) -> ()", &span_profile_start);
+  m.def("span_profile_stop(int span, int n_classes) -> (float[], int[])", &span_profile_stop);
   m.def("span_forward(int span, Tensor words, int[] shape, Tensor? ids, Tensor? x, Tensor(a!)? x_out, "
-        "Tensor(b!)? next_ids, Tensor(c!)? logits) -> ()",
+        "Tensor(b!)? next_ids, Tensor(c!)? logits, Tensor(d!)? layers=None) -> ()",
         &span_forward);
   m.def("span_lm_head(int span, Tensor x, Tensor(a!) logits) -> ()", &span_lm_head);
-  m.def("graph_capture(int span, Tensor words, int[] shape, Tensor? ids, Tensor? x, Tensor(a!)? x_out, "
-        "Tensor(b!)? next_ids, Tensor(c!)? logits) -> int",
-        &graph_capture);
-  m.def("graph_launch(int graph, Device device) -> ()", &graph_launch);
-  m.def("graph_destroy(int graph) -> ()", &graph_destroy);
+  m.def("weightgen(Tensor(a!) dst, int seed, int tensor_id, float scale, float center) -> ()", &weightgen);
   m.def("kv_create(int n_pages) -> int", &kv_create);
   m.def("kv_destroy(int table) -> ()", &kv_destroy);
   m.def("kv_reserve(int table, int seq, int n_new) -> ()", &kv_reserve);
   m.def("kv_advance(int table, int[] seqs, int n) -> ()", &kv_advance);
   m.def("kv_release(int table, int seq) -> ()", &kv_release);
   m.def("kv_query(int table, int seq) -> (int, int)", &kv_query);
+  m.def("kv_pages(int table, int seq) -> int[]", &kv_pages);
+  m.def("kv_free_pages(int table) -> int", &kv_free_pages);
   m.def("kv_build_batch(int table, int[] seqs, int[] n_new, Device device) -> (Tensor, int[])", &kv_build_batch);
+  m.class_<DecodeGraph>("DecodeGraph")
+      .def(torch::init<int64_t, int64_t, std::vector<int64_t>, int64_t, std::optional<at::Tensor>,
+                       std::optional<at::Tensor>, std::optional<at::Tensor>, std::optional<at::Tensor>,
+                       std::optional<at::Tensor>, at::Device>())
+      .def("launch", &DecodeGraph::launch)
+      .def("steps_left", &DecodeGraph::steps_left);
 }

@@ -1,13 +1,17 @@
 """torch.ops.inferd: the span engine's C-ABI registered as PyTorch-ROCm operators
-(inferd_amd/csrc/torch_ops.cpp -> libinferd_torch.so, built in-tree with the engine).
+(inferd_amd/csrc/torch_ops.cpp -> libinferd_torch.so, built in-tree with the engine) -- the
+binding the node-facing host (runtime.py) drives the engine through.
 
-    import inferd_amd.ops                      # registers torch.ops.inferd.*
+    import inferd_amd.ops                      # registers torch.ops.inferd.* / torch.classes.inferd.*
     span = torch.ops.inferd.span_create(cfg, eps, theta, device)
     words, shape = torch.ops.inferd.kv_build_batch(table, seqs, n_new, device)
     torch.ops.inferd.span_forward(span, words, shape, ids, None, None, next_ids, logits)
+    g = torch.classes.inferd.DecodeGraph(span, table, seqs, n_steps, ids, None, None, ids, None, device)
+    g.launch()
 
-Every op runs on torch's current HIP stream and raises RuntimeError with the library's message
-on a non-zero status.  There is no fallback: a missing library raises at import."""
+Every op runs on torch's current HIP stream, checks its tensors against the batch shape and the
+span's sizes, and raises RuntimeError with the library's message on a non-zero status.  There is
+no fallback: a missing library raises at import."""
 from __future__ import annotations
 
 import os
@@ -25,9 +29,13 @@ _lib.load()
 torch.ops.load_library(LIB_PATH)
 ops = torch.ops.inferd
 
-OPS = ("span_create", "span_destroy", "span_init_synthetic", "span_set_weight", "span_forward", "span_lm_head",
-       "graph_capture", "graph_launch", "graph_destroy", "kv_create", "kv_destroy", "kv_reserve", "kv_advance",
-       "kv_release", "kv_query", "kv_build_batch")
+OPS = ("span_create", "span_destroy", "span_config", "span_init_synthetic", "span_set_weight", "span_error_flags",
+       "span_profile_start", "span_profile_stop", "span_forward", "span_lm_head", "weightgen", "kv_create",
+       "kv_destroy", "kv_reserve", "kv_advance", "kv_release", "kv_query", "kv_pages", "kv_free_pages",
+       "kv_build_batch")
+CLASSES = ("DecodeGraph",)
+KV_PAGE = _lib.KV_PAGE              # tokens per KV page (INFERD_KV_PAGE_TOKENS)
+PROF_CLASSES = _lib.PROF_CLASSES    # span_profile_stop's kernel classes (INFERD_PROF_* order)
 
 
 def span_config(dims, first_layer: int, n_layers: int, *, has_embed: bool, has_lm_head: bool, kv_pages: int,

@@ -26,6 +26,7 @@ executor.
 """
 from __future__ import annotations
 
+import sys
 import time
 
 import torch
@@ -111,13 +112,12 @@ class SpanExecutor:
         for _ in range(n_steps):
             for m, sessions in enumerate(microbatches):
                 states = [self.span.reserve(sid, 1) for sid in sessions]
-                batch, keep = self.span.build_batch([(st, 1) for st in states])
+                batch = self.span.build_batch([(st, 1) for st in states])
                 b = bufs[m]
                 self.span.run(batch, ids=b.get("ids"), x=b.get("x"), hidden=b.get("hidden_out"),
                               next_ids=b.get("next_ids"))
                 for st in states:
                     st.length += 1
-                del keep
         torch.cuda.synchronize(self.device)
         return self.span.profile_stop()
 
@@ -163,6 +163,9 @@ class PipelineStage:
         # host time per tick of the last decode() call, split into the hand-off (exchange wait
         # included) and the rest (graph launch, page-table advance, schedule bookkeeping)
         self.tick_stats = None
+        self.first_layer, self.n_layers = first_layer, n_layers
+        self._exchanged = False     # first hand-off done (logged once)
+        self._inflight = None       # the last exchange's transient tensors (see _exchange)
 
     @property
     def first(self):
@@ -184,9 +187,26 @@ class PipelineStage:
         return {"ids": None, "x": self.h_in[m], "hidden_out": self.h_out[m], "next_ids": None}
 
     def _exchange(self, send=None, send_to=None, recv=None, recv_from=None):
+        """One grouped hand-off of this tick: isend `send` to the next stage, irecv `recv` from
+        the previous one (the reference's HTTP hop node.py:102-130, as RCCL p2p over xGMI).
+
+        Tensor lifetimes on the nccl path (RCCL runs on its own stream; `work.wait()` makes
+        torch's current stream wait for it without blocking the host, and the process group
+        orders its stream after the current stream's earlier work):
+          * decode: send / recv are the stage's fixed per-microbatch buffers (h_out / ids_out,
+            h_in / ids), allocated once in __init__ and captured by the decode graphs: they
+            live as long as the stage.  A buffer is rewritten by its microbatch's next graph
+            replay, which runs on the current stream after the wait, i.e. after the send
+            finished reading it; a recv lands before the graph that reads it (same wait).
+          * prefill: the send is a per-chunk output popped from bufs_out and the recv a fresh
+            tensor per tick.  Both are kept referenced here until the NEXT exchange (one tick
+            later), so the caching allocator cannot hand their blocks to a new tensor while
+            the send may be in flight, whether or not the process group records its stream on
+            p2p inputs.
+          * the first-ids hand-off after prefill (`flat`): a one-off tensor, kept the same way.
+        On gloo (CPU-rank tests, GPU ranks rehearsing without RCCL) device tensors are staged
+        through host memory synchronously."""
         import torch.distributed as dist
-        # gloo (CPU-rank tests, or GPU ranks rehearsing without RCCL): device tensors are
-        # staged through host memory; RCCL moves them GPU to GPU
         staged = dist.get_backend(self.group) == "gloo"
         dst = None
         if staged:
@@ -199,11 +219,23 @@ class PipelineStage:
             ops.append(dist.P2POp(dist.isend, send, send_to, self.group))
         if recv is not None:
             ops.append(dist.P2POp(dist.irecv, recv, recv_from, self.group))
+        t0 = time.perf_counter() if not self._exchanged else 0.0
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
         if dst is not None:
             dst.copy_(recv)
+        self._inflight = (send, recv)     # released at the next exchange (lifetimes above)
+        if not self._exchanged and ops:
+            # first hand-off of this stage: confirm it completed, so a wedged p2p link names
+            # itself (with the process group's timeout) instead of hanging silently
+            self._exchanged = True
+            if self.device.type == "cuda":
+                torch.cuda.current_stream(self.device).synchronize()
+            print(f"[pipeline] rank {self.rank}/{self.S} ({self.device}, layers {self.first_layer}.."
+                  f"{self.first_layer + self.n_layers - 1}): first exchange done over {dist.get_backend(self.group)}"
+                  f" (send->{send_to if send is not None else '-'}, recv<-{recv_from if recv is not None else '-'},"
+                  f" {(time.perf_counter() - t0) * 1e3:.1f} ms)", file=sys.stderr, flush=True)
 
     # ------------------------------------------------------------------ prefill
     @torch.no_grad()

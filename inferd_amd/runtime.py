@@ -10,18 +10,17 @@ Semantics mirrored from the reference:
   * a session-less call is a stateless full recompute (positions 0..T-1) whose cache
     pages are released afterwards                    -- partitioned_models.py:139-151
 The page table and the batch descriptors are native (inferd_kv_*, kvtable.hip); device
-memory for activations is torch (plumbing); all compute runs in libinferd_span.so.
+memory for activations is torch (plumbing); all compute runs in libinferd_span.so, driven
+through its PyTorch-ROCm extension (torch.ops.inferd / torch.classes.inferd, csrc/torch_ops.cpp).
 """
 from __future__ import annotations
 
-import ctypes as C
 import itertools
 from dataclasses import dataclass
 
 import torch
 
-from . import _lib
-from ._lib import KV_PAGE  # noqa: F401  (re-exported: pipeline, tests)
+from .ops import KV_PAGE, PROF_CLASSES, ops as T  # noqa: F401  (KV_PAGE re-exported: pipeline, tests)
 
 
 @dataclass(frozen=True)
@@ -70,16 +69,32 @@ PROFILE_BOOST = {"peaked": EMBED_BOOST, "peaked_deep": 512.0}
 
 def gen_tensor(seed: int, tid: int, shape, norm: bool, device) -> torch.Tensor:
     """One synthetic weight tensor (bf16, row-major) generated on the device."""
-    lib = _lib.load()
     n = 1
     for s in shape:
         n *= s
     device = torch.device(device)
     t = torch.empty(n, dtype=torch.bfloat16, device=device)
     with torch.cuda.device(device):
-        _lib.check(lib.inferd_weightgen(t.data_ptr(), n, seed, tid, NORM_SCALE if norm else LINEAR_SCALE,
-                                        1.0 if norm else 0.0, torch.cuda.current_stream(device).cuda_stream))
+        T.weightgen(t, seed, tid, NORM_SCALE if norm else LINEAR_SCALE, 1.0 if norm else 0.0)
     return t.reshape(tuple(shape))
+
+
+class Batch:
+    """A batch descriptor: the device (or host) int32 words [seq_start | positions | slots |
+    ctx_lens | block_table] the native table wrote and their shape [n_seqs, n_tokens, max_q_len,
+    max_ctx_len, max_pages, decode] (InferdBatch, include/inferd_span.h).  Holding it keeps the
+    words alive for the launches that read them."""
+    __slots__ = ("words", "shape")
+
+    def __init__(self, words: torch.Tensor, shape):
+        self.words, self.shape = words, [int(v) for v in shape]
+
+    n_seqs = property(lambda self: self.shape[0])
+    n_tokens = property(lambda self: self.shape[1])
+    max_q_len = property(lambda self: self.shape[2])
+    max_ctx_len = property(lambda self: self.shape[3])
+    max_pages = property(lambda self: self.shape[4])
+    decode = property(lambda self: self.shape[5])
 
 
 class KvTable:
@@ -87,62 +102,45 @@ class KvTable:
     Sequences are 64-bit keys; pages come lowest id first."""
 
     def __init__(self, n_pages: int):
-        self.lib = _lib.load()
         self.n_pages = n_pages
-        h = _lib.c_p()
-        _lib.check(self.lib.inferd_kv_create(n_pages, h))
-        self.handle = h
+        self.handle = T.kv_create(n_pages)
 
     def __del__(self):
         h = getattr(self, "handle", None)
-        if h is not None and h.value:
-            self.lib.inferd_kv_destroy(h)
+        if h:
+            T.kv_destroy(h)
             self.handle = None
 
     def reserve(self, seq: int, n_new: int):
-        _lib.check(self.lib.inferd_kv_reserve(self.handle, seq, n_new))
+        T.kv_reserve(self.handle, seq, n_new)
 
     def advance(self, seq: int, n: int):
-        _lib.check(self.lib.inferd_kv_advance(self.handle, seq, n))
+        T.kv_advance(self.handle, [seq], n)
+
+    def advance_many(self, seqs, n: int):
+        """every sequence of `seqs` by n tokens; all or nothing"""
+        T.kv_advance(self.handle, list(seqs), n)
 
     def release(self, seq: int):
-        _lib.check(self.lib.inferd_kv_release(self.handle, seq))
+        T.kv_release(self.handle, seq)
 
     def query(self, seq: int):
         """(cached length or -1 if absent, reserved pages)"""
-        ln, npg = C.c_int32(0), C.c_int32(0)
-        _lib.check(self.lib.inferd_kv_query(self.handle, seq, C.byref(ln), C.byref(npg)))
-        return ln.value, npg.value
+        return tuple(T.kv_query(self.handle, seq))
 
     def pages(self, seq: int) -> list:
-        n = self.query(seq)[1]
-        buf = (C.c_int32 * max(n, 1))()
-        _lib.check(self.lib.inferd_kv_pages(self.handle, seq, buf, n))
-        return list(buf[:n])
+        return list(T.kv_pages(self.handle, seq))
 
     @property
     def n_free(self) -> int:
-        f = C.c_int32(0)
-        _lib.check(self.lib.inferd_kv_free_pages(self.handle, C.byref(f)))
-        return f.value
+        return T.kv_free_pages(self.handle)
 
-    def build_batch(self, seqs, device):
-        """seqs: [(key, n_new)], pages already reserved.  Returns (Batch, the device int32
-        tensor backing its arrays); the words are built natively, then copied to `device`."""
-        n = len(seqs)
-        keys = (C.c_uint64 * n)(*[k for k, _ in seqs])
-        nn = (C.c_int32 * n)(*[m for _, m in seqs])
-        words = self.lib.inferd_kv_batch_words(self.handle, keys, nn, n)
-        if words < 0:
-            _lib.check(_lib.INFERD_ERR_ARG)
-        host = torch.empty(int(words), dtype=torch.int32, pin_memory=torch.device(device).type == "cuda")
-        dev = torch.empty(int(words), dtype=torch.int32, device=device)
-        b = _lib.Batch()
-        _lib.check(self.lib.inferd_kv_build_batch(self.handle, keys, nn, n,
-                                                  C.cast(host.data_ptr(), C.POINTER(C.c_int32)), words,
-                                                  dev.data_ptr(), b))
-        dev.copy_(host, non_blocking=True)
-        return b, (dev, host)
+    def build_batch(self, seqs, device) -> Batch:
+        """seqs: [(key, n_new)], pages already reserved.  The words are built natively, then
+        copied to `device`."""
+        words, shape = T.kv_build_batch(self.handle, [k for k, _ in seqs], [m for _, m in seqs],
+                                        torch.device(device))
+        return Batch(words, shape)
 
 
 class SeqView:
@@ -168,59 +166,33 @@ class SeqView:
 
 class DecodeGraph:
     """One decode step of a fixed set of sessions captured as a HIP graph
-    (inferd_span_graph_capture with advance=1): every launch decodes one more token of
-    each session, reading `ids` (first span) or `x`, writing `hidden_out` and/or
-    `next_ids` -- fixed device buffers chosen at capture.  `ids` and `next_ids` may alias
-    (greedy feedback on a single-span model).  Pages for `n_steps` tokens are reserved
-    up front; launching more than n_steps times raises.  `logits` (last span, optional): bf16
-    [sessions, vocab] receives every replay's last-row logits."""
+    (torch.classes.inferd.DecodeGraph: inferd_span_graph_capture with advance=1 over the
+    native decode descriptor of inferd_kv_build_decode_batch): every launch decodes one more
+    token of each session, reading `ids` (first span) or `x`, writing `hidden_out` and/or
+    `next_ids` -- fixed device buffers chosen at capture, kept alive by the graph object.
+    `ids` and `next_ids` may alias (greedy feedback on a single-span model).  Pages for
+    `n_steps` tokens are reserved up front; launching more than n_steps times raises.
+    `logits` (last span, optional): bf16 [sessions, vocab] receives every replay's last-row
+    logits."""
 
     def __init__(self, span: "SpanRuntime", sessions, n_steps: int, ids=None, x=None, hidden_out=None,
                  next_ids=None, logits=None):
-        self.span, self.n_steps, self.launched = span, n_steps, 0
-        self.states = [span.reserve(sid, n_steps) for sid in sessions]
-        B = len(self.states)
-        pages = [st.pages for st in self.states]
-        max_pages = max(len(p) for p in pages)
-        table = []
-        for p in pages:
-            table.extend(p + [0] * (max_pages - len(p)))
-        lengths = [st.length for st in self.states]
-        host = torch.tensor(list(range(B + 1)) + [0] * B + [0] * B + lengths + table, dtype=torch.int32)
-        self.buf = host.to(span.device)
-        base = self.buf.data_ptr()
-        o = [0, B + 1, 2 * B + 1, 3 * B + 1, 4 * B + 1]
-        self.batch = _lib.Batch(n_seqs=B, n_tokens=B, max_q_len=1, max_ctx_len=max(lengths) + n_steps,
-                                max_pages=max_pages, decode=1, seq_start=base + 4 * o[0],
-                                positions=base + 4 * o[1], slots=base + 4 * o[2], ctx_lens=base + 4 * o[3],
-                                block_table=base + 4 * o[4])
-        self._keep = (ids, x, hidden_out, next_ids, logits)
-        self._seqs = (C.c_uint64 * B)(*[st.seq for st in self.states])
-        cur = torch.cuda.current_stream(span.device)
-        cs = torch.cuda.Stream(span.device)
-        cs.wait_stream(cur)
-        g = _lib.c_p()
+        self.span, self.n_steps = span, n_steps
+        self.states = [span._seq(sid) for sid in sessions]
         with torch.cuda.device(span.device):
-            _lib.check(span.lib.inferd_span_graph_capture(span.handle, self.batch, 1, _lib.ptr(ids), _lib.ptr(x),
-                                                          _lib.ptr(hidden_out), _lib.ptr(next_ids), _lib.ptr(logits),
-                                                          cs.cuda_stream, g))
-        cur.wait_stream(cs)
-        self.graph = g
+            self.graph = torch.classes.inferd.DecodeGraph(span.handle, span.kv.handle, [st.seq for st in self.states],
+                                                          n_steps, ids, x, hidden_out, next_ids, logits, span.device)
+
+    @property
+    def launched(self) -> int:
+        return self.n_steps - self.graph.steps_left()
 
     def launch(self, stream=None):
-        if self.launched >= self.n_steps:
-            raise RuntimeError("decode graph ran out of reserved steps")
-        s = stream if stream is not None else torch.cuda.current_stream(self.span.device)
-        _lib.check(self.span.lib.inferd_graph_launch(self.graph, s.cuda_stream))
-        self.launched += 1
-        # the host page table follows the device-side advance: one native call per replay
-        _lib.check(self.span.lib.inferd_kv_advance_many(self.span.kv.handle, self._seqs, len(self.states), 1))
-
-    def __del__(self):
-        g = getattr(self, "graph", None)
-        if g is not None and g.value:
-            self.span.lib.inferd_graph_destroy(g)
-            self.graph = None
+        if stream is None:
+            self.graph.launch()
+        else:
+            with torch.cuda.stream(stream):
+                self.graph.launch()
 
 
 class SpanRuntime:
@@ -229,7 +201,6 @@ class SpanRuntime:
     def __init__(self, dims: ModelDims, first_layer: int, n_layers: int, *, has_embed: bool,
                  has_lm_head: bool, kv_pages: int = 256, max_tokens: int = 4096, max_seqs: int = 64,
                  max_positions: int | None = None, device: str | torch.device = "cuda"):
-        self.lib = _lib.load()
         self.dims = dims
         self.first_layer, self.n_layers = first_layer, n_layers
         self.has_embed, self.has_lm_head = has_embed, has_lm_head
@@ -238,24 +209,18 @@ class SpanRuntime:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.max_tokens, self.max_seqs = max_tokens, max_seqs
         self.max_positions = max_positions or dims.max_positions
-        cfg = _lib.SpanConfig(hidden=dims.hidden, intermediate=dims.intermediate, heads=dims.heads,
-                              kv_heads=dims.kv_heads, head_dim=dims.head_dim, vocab=dims.vocab,
-                              first_layer=first_layer, n_layers=n_layers, has_embed=int(has_embed),
-                              has_lm_head=int(has_lm_head), rms_eps=dims.eps, rope_theta=dims.rope_theta,
-                              max_positions=self.max_positions, kv_pages=kv_pages,
-                              max_tokens=max_tokens, max_seqs=max_seqs)
-        h = _lib.c_p()
-        with torch.cuda.device(self.device):
-            _lib.check(self.lib.inferd_span_create(cfg, h))
-        self.handle = h
+        cfg = [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
+               n_layers, int(has_embed), int(has_lm_head), self.max_positions, kv_pages, max_tokens, max_seqs]
+        self.handle = None
+        self.handle = T.span_create(cfg, dims.eps, dims.rope_theta, self.device)
         self.kv = KvTable(kv_pages)
         self.sessions: dict = {}   # session key -> SeqView
         self._seq_ids = itertools.count(1)
 
     def __del__(self):
         h = getattr(self, "handle", None)
-        if h is not None and h.value:
-            self.lib.inferd_span_destroy(h)
+        if h:
+            T.span_destroy(h)
             self.handle = None
 
     # ----------------------------------------------------------------- weights
@@ -269,7 +234,7 @@ class SpanRuntime:
         if profile != "random" and profile not in PROFILE_BOOST:
             raise ValueError(f"unknown synthetic profile {profile!r}")
         with torch.cuda.device(self.device):
-            _lib.check(self.lib.inferd_span_init_synthetic(self.handle, seed, self._stream().cuda_stream))
+            T.span_init_synthetic(self.handle, seed, self.device)
             if profile in PROFILE_BOOST and (self.has_embed or self.has_lm_head):
                 d = self.dims
                 emb = gen_tensor(seed, GLOBAL_TENSOR_IDS["embed_tokens"], (d.vocab, d.hidden), False,
@@ -291,11 +256,8 @@ class SpanRuntime:
         span's device and stream, then waits so the source tensor may be freed."""
         with torch.cuda.device(self.device):
             w = w.to(device=self.device, dtype=torch.bfloat16).contiguous()
-            rows, cols = (1, w.shape[0]) if w.dim() == 1 else tuple(w.shape)
-            s = self._stream()
-            _lib.check(self.lib.inferd_span_set_weight(self.handle, layer, name.encode(), w.data_ptr(),
-                                                       rows, cols, s.cuda_stream))
-            s.synchronize()
+            T.span_set_weight(self.handle, layer, name, w)
+            self._stream().synchronize()
 
     def load_layer_state_dict(self, layer: int, sd: dict):
         """Keys as in Qwen3DecoderLayer (qwen3_server_module.py:165-176): self_attn.q_proj.weight ...
@@ -308,14 +270,11 @@ class SpanRuntime:
         """Read (and clear) the span's sticky device error flags; raise on any.  Bit 0: a
         token id outside [0, vocab) reached the embedding gather (the reference's
         nn.Embedding raises IndexError); bit 1: a decode graph ran past its reserved pages."""
-        import ctypes as C
-        f = C.c_int32(0)
-        with torch.cuda.device(self.device):
-            _lib.check(self.lib.inferd_span_error_flags(self.handle, C.byref(f)))
-        if f.value & 1:
+        f = T.span_error_flags(self.handle, self.device)
+        if f & 1:
             raise IndexError("index out of range in self (token id outside the vocabulary)")
-        if f.value:
-            raise RuntimeError(f"span device error flags 0x{f.value:x} (decode slot overflow)")
+        if f:
+            raise RuntimeError(f"span device error flags 0x{f:x} (decode slot overflow)")
 
     # ----------------------------------------------------------------- sessions
     def release(self, session_id):
@@ -333,30 +292,27 @@ class SpanRuntime:
             st = self.sessions[session_id] = SeqView(self.kv, next(self._seq_ids))
         return st
 
-    def build_batch(self, seqs):
-        """seqs: [(SeqView, n_new)] with pages reserved -> (Batch, keep-alive buffers)."""
+    def build_batch(self, seqs) -> Batch:
+        """seqs: [(SeqView, n_new)] with pages reserved -> the Batch (it holds its words)."""
         return self.kv.build_batch([(st.seq, n) for st, n in seqs], self.device)
 
     # ----------------------------------------------------------------- fast path
     def run(self, batch, ids=None, x=None, hidden=None, next_ids=None, logits=None, layers=None, stream=None):
         """Launch one span forward on a prebuilt Batch with caller-owned device tensors
         (no host sync, no allocation).  Used by the pipeline runtime and the bench."""
-        s = stream if stream is not None else self._stream()
-        _lib.check(self.lib.inferd_span_forward(self.handle, batch, _lib.ptr(ids), _lib.ptr(x), _lib.ptr(hidden),
-                                                _lib.ptr(next_ids), _lib.ptr(logits), _lib.ptr(layers),
-                                                s.cuda_stream))
+        if stream is None:
+            T.span_forward(self.handle, batch.words, batch.shape, ids, x, hidden, next_ids, logits, layers)
+        else:
+            with torch.cuda.stream(stream):
+                T.span_forward(self.handle, batch.words, batch.shape, ids, x, hidden, next_ids, logits, layers)
 
     def profile_start(self, max_pairs: int = 1 << 16):
-        _lib.check(self.lib.inferd_span_profile_start(self.handle, max_pairs))
+        T.span_profile_start(self.handle, max_pairs)
 
     def profile_stop(self) -> dict:
         """{class: (total_ms, launches)} from the HIP events recorded since profile_start."""
-        import ctypes as C
-        n = len(_lib.PROF_CLASSES)
-        ms = (C.c_double * n)()
-        cnt = (C.c_int32 * n)()
-        _lib.check(self.lib.inferd_span_profile_stop(self.handle, ms, cnt, n))
-        return {name: (ms[i], cnt[i]) for i, name in enumerate(_lib.PROF_CLASSES)}
+        ms, cnt = T.span_profile_stop(self.handle, len(PROF_CLASSES))
+        return {name: (ms[i], cnt[i]) for i, name in enumerate(PROF_CLASSES)}
 
     def reserve(self, session_id, n_tokens: int) -> SeqView:
         """Make sure `session_id` has pages for n_tokens more tokens (no forward)."""
@@ -372,11 +328,9 @@ class SpanRuntime:
         with torch.cuda.device(self.device):
             x = hidden.to(device=self.device, dtype=torch.bfloat16).reshape(-1, d.hidden).contiguous()
             out = torch.empty((x.shape[0], d.vocab), dtype=torch.bfloat16, device=self.device)
-            s = self._stream()
             for r0 in range(0, x.shape[0], self.max_tokens):
                 n = min(self.max_tokens, x.shape[0] - r0)
-                _lib.check(self.lib.inferd_span_lm_head(self.handle, x[r0].data_ptr(), n, out[r0].data_ptr(),
-                                                        s.cuda_stream))
+                T.span_lm_head(self.handle, x[r0:r0 + n], out[r0:r0 + n])
         return out
 
     # ----------------------------------------------------------------- forward
@@ -462,8 +416,8 @@ class SpanRuntime:
                     r0 = row0[call[0][0]] + call[0][1]
                     m = sum(t for _, _, t in call)
                     single = len(calls) == 1
-                    batch, bkeep = self.build_batch([(states[i], t) for i, _, t in call])
-                    keep.append(bkeep)
+                    batch = self.build_batch([(states[i], t) for i, _, t in call])
+                    keep.append(batch)
                     finals = [j for j, (i, s0, t) in enumerate(call) if s0 + t == requests[i][1]]
                     c_nid = nid if single else (torch.empty((len(call),), dtype=torch.int32, device=dev)
                                                 if nid is not None and finals else None)

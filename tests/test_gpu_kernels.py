@@ -137,16 +137,14 @@ def test_gemm_swiglu(lib, M, K):
     assert (bf16_ulp_diff(c.cpu(), ref.cpu()) > 2).float().mean() < 2e-3
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 192), (777, 768, 1088), (2048, 1024, 4096), (1300, 256, 640),
                                    (4096, 2048, 1024), (8092, 4096, 448), (300, 384, 1024)])
-def test_gemm_prefill_bodies(lib, monkeypatch, split, M, N, K):
+def test_gemm_prefill_bodies(lib, M, N, K):
     """The prefill GEMM bodies on ragged M, short and long K, all epilogues: persistent
     gemm_w4p; gemm_w4 with the tail split ((2048, 1024, 4096) and (4096, 2048, 1024) cut K
-    8 / 2 ways; INFERD_GEMM_SPLIT=0 runs them whole on w4p); (8092, 4096, 448): 512 whole
-    tiles, so w4p walks two tiles per workgroup (ragged last row block, cross-tile prefetch,
-    exact-count epilogue waits); (300, 384, 1024): the 128x128 gemm_tiled."""
-    monkeypatch.setenv("INFERD_GEMM_SPLIT", split)
+    8 / 2 ways); (8092, 4096, 448): 512 whole tiles, so w4p walks two tiles per workgroup
+    (ragged last row block, cross-tile prefetch, exact-count epilogue waits); (300, 384,
+    1024): the 128x128 gemm_tiled."""
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.03).to(torch.bfloat16)
@@ -255,7 +253,8 @@ def _attn_case(lib, H, KV, q_lens, past_lens, seed=0):
         Ks.append(K)
         Vs.append(V)
         Qs.append((torch.randn(T, H, 128) * 1.5).to(torch.bfloat16))
-    batch, keep = table.build_batch([(st.seq, T) for st, T in seqs], DEV)
+    bd = table.build_batch([(st.seq, T) for st, T in seqs], DEV)
+    batch = lib.batch_struct(bd.words, bd.shape)
     q = torch.cat(Qs, 0).contiguous().to(DEV)
     out = torch.empty(q.shape[0], H * 128, dtype=torch.bfloat16, device=DEV)
     ws_bytes = L.inferd_attention_workspace_bytes(len(seqs), H, max(t + p for t, p in zip(q_lens, past_lens)))
@@ -289,15 +288,11 @@ def test_attention_decode_many_chunks(lib, q_lens, past):
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
 
 
-@pytest.mark.parametrize("pfk", [0, 1, 2, 6])
 @pytest.mark.parametrize("H,KV", [(32, 8), (16, 8), (4, 2), (64, 8)])
-def test_attention_prefill(lib, monkeypatch, H, KV, pfk):
-    """Every prefill kernel (INFERD_ATTN_PREFILL=0: the 4-wave attn_prefill_kernel with 48 rows per
-    wave, 2: the same with 32 rows per wave, 6: 32 rows per wave at three workgroups per CU, 1: the
-    one-wave-per-SIMD attn_prefill.hip) on ragged prompts, with and without cached prefixes:
-    a 700-token prompt (several 128-row blocks, > 4 pages) and a 1000-token prompt behind 300
-    cached tokens (several 256-row blocks, masks on pages that start mid-block)."""
-    monkeypatch.setenv("INFERD_ATTN_PREFILL", str(pfk))
+def test_attention_prefill(lib, H, KV):
+    """The prefill attention (4 waves x 48 query rows) on ragged prompts, with and without
+    cached prefixes: a 700-token prompt (several 192-row blocks, > 4 pages) and a 1000-token
+    prompt behind 300 cached tokens (masks on pages that start mid-block)."""
     err, ref = _attn_case(lib, H, KV, [1, 17, 64, 130, 700, 1000], [0, 5, 0, 200, 61, 300], seed=H + 1)
     assert err.max().item() < 2e-2 * max(1.0, ref.abs().max().item()), err.max()
 

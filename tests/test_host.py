@@ -83,17 +83,22 @@ def test_kv_table_and_batch_descriptor():
     kv.reserve(2, 5)      # sequence b: 5 new tokens -> 1 page
     assert kv.pages(1) == [0, 1] and kv.pages(2) == [2] and kv.n_free == 7
     assert kv.query(1) == (70, 2) and kv.query(3) == (-1, 0)
-    batch, (buf, _) = kv.build_batch([(1, 3), (2, 5)], "cpu")
+    batch = kv.build_batch([(1, 3), (2, 5)], "cpu")
     assert (batch.n_seqs, batch.n_tokens, batch.max_q_len, batch.max_ctx_len, batch.decode) == (2, 8, 5, 73, 0)
+    w = batch.words.tolist()
+    assert w[0:3] == [0, 3, 8]                                       # seq_start
+    assert w[3:11] == [70, 71, 72, 0, 1, 2, 3, 4]                    # positions
+    assert w[11:19] == [1 * 64 + 6, 1 * 64 + 7, 1 * 64 + 8] + [2 * 64 + i for i in range(5)]  # slots
+    assert w[19:21] == [73, 5]                                       # ctx_lens
+    assert w[21:25] == [0, 1, 2, 0] and len(w) == 25                 # block table
+    # the same descriptor through the ctypes binding (the non-torch host's view)
+    from inferd_amd import _lib
+    cb = _lib.batch_struct(batch.words, batch.shape)
 
     def arr(ptr, n):
         return list((ctypes.c_int32 * n).from_address(ptr))
-    assert arr(batch.seq_start, 3) == [0, 3, 8]
-    assert arr(batch.positions, 8) == [70, 71, 72, 0, 1, 2, 3, 4]
-    assert arr(batch.slots, 8) == [1 * 64 + 6, 1 * 64 + 7, 1 * 64 + 8] + [2 * 64 + i for i in range(5)]
-    assert arr(batch.ctx_lens, 2) == [73, 5]
-    assert arr(batch.block_table, 4) == [0, 1, 2, 0]
-    assert batch.seq_start == buf.data_ptr()
+    assert arr(cb.seq_start, 3) == [0, 3, 8] and arr(cb.block_table, 4) == [0, 1, 2, 0]
+    assert cb.seq_start == batch.words.data_ptr()
     with pytest.raises(RuntimeError, match="KV pool exhausted"):
         kv.reserve(3, 8 * 64)
     assert kv.n_free == 7 and kv.query(3)[1] == 0          # nothing taken
@@ -104,13 +109,13 @@ def test_kv_table_and_batch_descriptor():
     with pytest.raises(RuntimeError):
         kv.advance(2, 65)                                   # past the reserved pages
     # a decode-graph replay's host advance: one native call for the whole batch, all or nothing
-    keys = (ctypes.c_uint64 * 2)(1, 2)
-    assert kv.lib.inferd_kv_advance_many(kv.handle, keys, 2, 3) == 0
+    kv.advance_many([1, 2], 3)
     assert kv.query(1)[0] == 73 and kv.query(2)[0] == 3
-    assert kv.lib.inferd_kv_advance_many(kv.handle, keys, 2, 62) != 0  # sequence a: past its 2 pages
+    with pytest.raises(RuntimeError, match="past the reserved pages"):
+        kv.advance_many([1, 2], 62)                                     # sequence a: past its 2 pages
     assert kv.query(1)[0] == 73 and kv.query(2)[0] == 3                 # nothing advanced
-    dup = (ctypes.c_uint64 * 2)(2, 2)
-    assert kv.lib.inferd_kv_advance_many(kv.handle, dup, 2, 1) != 0     # a sequence twice
+    with pytest.raises(RuntimeError, match="only once"):
+        kv.advance_many([2, 2], 1)                                      # a sequence twice
     kv.release(1)
     assert kv.n_free == 9
     kv.reserve(4, 64)                                       # a's first page comes back first
@@ -237,7 +242,8 @@ def test_build_batch_descriptor_layout():
             kv.advance(key, past)
             live[key] = key
             seqs.append((key, n))
-        batch, (dev, _) = kv.build_batch(seqs, "cpu")
+        batch = kv.build_batch(seqs, "cpu")
+        dev = batch.words
         pages = {k: kv.pages(k) for k, _ in seqs}
         max_pages = max(len(pages[k]) for k, _ in seqs)
         start, pos, slots, ctx, table = [0], [], [], [], []

@@ -42,7 +42,8 @@ def main():
     for b in range(B):
         table.reserve(b, n)
         table.advance(b, P)
-    batch, keep = table.build_batch([(b, T) for b in range(B)], dev)
+    bd = table.build_batch([(b, T) for b in range(B)], dev)
+    batch = _lib.batch_struct(bd.words, bd.shape)
     pool_pages = (B * pages_per + 15) // 16 * 16  # whole KV super-pages (common.h KV_SUPER)
     kv = (torch.rand(pool_pages * 2 * KV * 64 * 128, device=dev) * 2 - 1).to(torch.bfloat16)
     q = (torch.rand(B * T, H, 128, device=dev) * 4 - 2).to(torch.bfloat16)
