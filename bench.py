@@ -47,8 +47,8 @@ def latest_traffic(kind: str, workload: str):
     """The newest committed PMC traffic summary (profiles/traffic[_prefill]_rNN.json) measured
     on `workload`: {kernel class: HBM bytes per launch}, or None."""
     import glob
-    pat = os.path.join(ROOT, "profiles", f"traffic{'_prefill' if kind == 'prefill' else ''}_r[0-9]*.json")
-    for fn in sorted(glob.glob(pat), reverse=True):
+    pat = os.path.join(ROOT, "profiles", f"traffic{'_prefill' if kind == 'prefill' else ''}_*r[0-9]*.json")
+    for fn in sorted(glob.glob(pat), key=lambda f: f[-7:], reverse=True):
         with open(fn) as f:
             tr = json.load(f)
         if tr.get("workload") == workload:
@@ -169,7 +169,7 @@ def prefill_line(args, steps: int, warmup: int, dev, peaks: bool = True) -> dict
     # PMC-measured L2-to-fabric bytes per launch of the dominant kernel class
     # (tools/pmc_prefill.sh -> the newest profiles/traffic_prefill_rNN.json; MALL hits count)
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["launches"])
-    tr = latest_traffic("prefill", f"{d.name}-prefill-{L}layers-T{T}") if B == 1 else None
+    tr = latest_traffic("prefill", f"{d.name}-prefill-{L}layers-T{T}" + (f"-B{B}" if B > 1 else ""))
     traffic = None if tr is None else tr.get(dom)
     del span
     return {

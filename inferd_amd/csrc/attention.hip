@@ -664,11 +664,32 @@ void launch_attn_decode_fused(const u16* qkv, int64_t ldqkv, const u16* qn_w, co
 //  * l is kept per lane (each lane's share of its query's row sum) and reduced across the 4
 //    lanes of a query once, at the end;
 //  * row max reductions use v_permlane{32,16}_swap instead of ds_bpermute.
+// Lab switches (tools/build_probes.sh builds; the product default is the measured optimum):
+// PF_NB query rows per wave / 16, PF_CUTS the two softmax VALU cuts below.
+#ifndef PF_NB
+#define PF_NB 3
+#endif
+#ifndef PF_CUTS
+#define PF_CUTS 0
+#endif
+// Softmax VALU cuts (PF_CUTS):
+//  * the scale is folded into Q (q' = bf16(q * scale * log2 e), once per workgroup) and the
+//    running reference max -m rides the first S MFMA's C operand, so the accumulators come out
+//    as s' = q'.k - m and p = exp2(s') is one v_exp_f32 per score (no fma per score);
+//  * the row sum l comes out of the P.V MFMAs: one more 16x16x32 MFMA per 32 tokens against an
+//    all-ones A operand gives sum_t bf16(p_t) -- the sum of exactly the weights P.V uses -- in
+//    every lane of the query, with no VALU add and no cross-lane reduction.
+// The first page (token 0, visible to every row) sets m exactly; afterwards a row's max moves
+// only when it grows by more than RESCALE_THR (then o, l and this page's s' shift by the growth).
+struct PfState {
+  f32x4 negm;  // (-m) x 4: the S chains' initial C operand
+  f32x4 l;     // row sum (every element the same)
+};
 // S^T of a page (K at kl) + its online softmax -> P (bf16, the B operand of P.V) in pf
-template <bool MASK, int NB>
+template <bool MASK, bool FIRST, int NB>
 __device__ __forceinline__ void prefill_page_s(const char* __restrict__ kl, const bf16x8 (&qf)[NB][4], int page_tok0,
                                                const int (&lim)[NB], float c, float (&m_i)[NB], float (&l_i)[NB],
-                                               f32x4 (&o)[NB][8], int lane, bf16x8 (&pf)[NB][2]) {
+                                               PfState (&ps_)[NB], f32x4 (&o)[NB][8], int lane, bf16x8 (&pf)[NB][2]) {
   const char* lds = kl;
   f32x4 sc[NB][4];
   // k-slice outermost: eight accumulation chains in flight (tb outermost left two, with
@@ -679,8 +700,11 @@ __device__ __forceinline__ void prefill_page_s(const char* __restrict__ kl, cons
     for (int tb = 0; tb < 4; ++tb) {
       const bf16x8 kf = *(const bf16x8*)(lds + (tb * 4 + ks) * 1024 + lane * 16);
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-        sc[nb][tb] = mfma16(kf, qf[nb][ks], ks ? sc[nb][tb] : f32x4{0.f, 0.f, 0.f, 0.f});
+      for (int nb = 0; nb < NB; ++nb) {
+        f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (PF_CUTS && !FIRST) c0 = ps_[nb].negm;
+        sc[nb][tb] = mfma16(kf, qf[nb][ks], ks ? sc[nb][tb] : c0);
+      }
     }
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
@@ -697,24 +721,50 @@ __device__ __forceinline__ void prefill_page_s(const char* __restrict__ kl, cons
 #pragma unroll
     for (int tb = 0; tb < 4; ++tb)
       pm[tb] = fmaxf(fmaxf(sc[nb][tb][0], sc[nb][tb][1]), fmaxf(sc[nb][tb][2], sc[nb][tb][3]));
-    const float pmax = fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3]));
-    const float m_new = fmaxf(m_i[nb], max_q4(pmax) * c);
-    if (__builtin_amdgcn_ballot_w64(m_new > m_i[nb] + RESCALE_THR)) {
-      const float alpha = exp2_raw(m_i[nb] - m_new);
-      l_i[nb] *= alpha;
+    const float pmax = max_q4(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
+    if constexpr (PF_CUTS) {
+      // sc = s' = s*c - m (m = 0 on the first page)
+      float shift = 0.f;
+      if constexpr (FIRST) {
+        shift = pmax;  // finite: token 0 is visible to every row
+        m_i[nb] = pmax;
+        ps_[nb].negm = f32x4{-pmax, -pmax, -pmax, -pmax};
+      } else if (__builtin_amdgcn_ballot_w64(pmax > RESCALE_THR)) {
+        shift = fmaxf(pmax, 0.f);  // -inf (all masked) -> no shift
+        const float alpha = exp2_raw(-shift);
+        ps_[nb].l *= alpha;
 #pragma unroll
-      for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
-      m_i[nb] = m_new;
+        for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
+        m_i[nb] += shift;
+        ps_[nb].negm = f32x4{-m_i[nb], -m_i[nb], -m_i[nb], -m_i[nb]};
+      }
+      if (FIRST || shift != 0.f) {
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb) sc[nb][tb] -= shift;
+      }
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[nb][tb][r] = exp2_raw(sc[nb][tb][r]);
+    } else {
+      const float m_new = fmaxf(m_i[nb], pmax * c);
+      if (__builtin_amdgcn_ballot_w64(m_new > m_i[nb] + RESCALE_THR)) {
+        const float alpha = exp2_raw(m_i[nb] - m_new);
+        l_i[nb] *= alpha;
+#pragma unroll
+        for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
+        m_i[nb] = m_new;
+      }
+      const float mneg = -m_i[nb];
+      float ps[4];  // 4 independent sum chains
+#pragma unroll
+      for (int tb = 0; tb < 4; ++tb) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[nb][tb][r] = exp2_raw(fmaf(sc[nb][tb][r], c, mneg));
+        ps[tb] = (sc[nb][tb][0] + sc[nb][tb][1]) + (sc[nb][tb][2] + sc[nb][tb][3]);
+      }
+      l_i[nb] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
     }
-    const float mneg = -m_i[nb];
-    float ps[4];  // 4 independent sum chains
-#pragma unroll
-    for (int tb = 0; tb < 4; ++tb) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sc[nb][tb][r] = exp2_raw(fmaf(sc[nb][tb][r], c, mneg));
-      ps[tb] = (sc[nb][tb][0] + sc[nb][tb][1]) + (sc[nb][tb][2] + sc[nb][tb][3]);
-    }
-    l_i[nb] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -724,26 +774,34 @@ __device__ __forceinline__ void prefill_page_s(const char* __restrict__ kl, cons
       }
   }
 }
-// O^T += V^T P^T of a page (V at vl)
+// O^T += V^T P^T of a page (V at vl); PF_CUTS: l += 1^T P^T on the same operands
 template <int NB>
 __device__ __forceinline__ void prefill_page_pv(const char* __restrict__ vl, const bf16x8 (&pf)[NB][2],
-                                                f32x4 (&o)[NB][8], int lane) {
+                                                f32x4 (&o)[NB][8], PfState (&ps_)[NB], int lane) {
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
     for (int db = 0; db < 8; ++db) {
       const bf16x8 vf = *(const bf16x8*)(vl + (kt * 8 + db) * 1024 + lane * 16);
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) o[nb][db] = mfma16(vf, pf[nb][kt], o[nb][db]);
     }
+    if constexpr (PF_CUTS) {
+      bf16x8 ones;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) ps_[nb].l = mfma16(ones, pf[nb][kt], ps_[nb].l);
+    }
+  }
 }
-template <bool MASK, int NB>
+template <bool MASK, bool FIRST, int NB>
 __device__ __forceinline__ void prefill_page_lds(const char* __restrict__ lds, const bf16x8 (&qf)[NB][4],
-                                                 int page_tok0, const int (&lim)[NB], float c,
-                                                 float (&m_i)[NB], float (&l_i)[NB], f32x4 (&o)[NB][8], int lane) {
+                                                 int page_tok0, const int (&lim)[NB], float c, float (&m_i)[NB],
+                                                 float (&l_i)[NB], PfState (&ps_)[NB], f32x4 (&o)[NB][8], int lane) {
   bf16x8 pf[NB][2];
-  prefill_page_s<MASK, NB>(lds, qf, page_tok0, lim, c, m_i, l_i, o, lane, pf);
-  prefill_page_pv<NB>(lds + 16384, pf, o, lane);
+  prefill_page_s<MASK, FIRST, NB>(lds, qf, page_tok0, lim, c, m_i, l_i, ps_, o, lane, pf);
+  prefill_page_pv<NB>(lds + 16384, pf, o, ps_, lane);
 }
 
 // Block order (grid x = max_q_blocks * H per sequence, y = sequence): mode 1 (used when
@@ -799,6 +857,14 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
   }
+  if constexpr (PF_CUTS) {  // q' = bf16(q * scale * log2 e)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[nb][ks][j] = (__bf16)((float)qf[nb][ks][j] * scale_log2);
+  }
   // pages: up to the workgroup's last row; a wave computes up to its own last row and
   // masks only pages that reach past its smallest row limit
   const int wg_last = b.positions[t0 + min(qb0 + QB - 1, T - 1)];
@@ -833,11 +899,14 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
     }
   };
   float m_i[NB], l_i[NB];
+  PfState ps_[NB];
   f32x4 o[NB][8];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     m_i[nb] = -INFINITY;
     l_i[nb] = 0.f;
+    ps_[nb].negm = f32x4{0.f, 0.f, 0.f, 0.f};
+    ps_[nb].l = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb)
@@ -845,19 +914,26 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
     for (int db = 0; db < 8; ++db) o[nb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
   stage(0, 0);
   __syncthreads();
-  for (int pi = 0; pi < n_pages; ++pi) {
+  // page 0 (token 0: every row's first visible key) sets the rows' reference max
+  if (n_pages > 1) stage(1, 1);
+  if (KV_PAGE - 1 <= wave_min_lim)
+    prefill_page_lds<false, true, NB>(lds, qf, 0, lim, scale_log2, m_i, l_i, ps_, o, lane);
+  else if (0 <= wave_last)
+    prefill_page_lds<true, true, NB>(lds, qf, 0, lim, scale_log2, m_i, l_i, ps_, o, lane);
+  __syncthreads();
+  for (int pi = 1; pi < n_pages; ++pi) {
     const int cur = pi & 1;
     if (pi + 1 < n_pages) stage(cur ^ 1, pi + 1);
     const int tok0 = pi * KV_PAGE;
     if (tok0 + KV_PAGE - 1 <= wave_min_lim)
-      prefill_page_lds<false, NB>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, o, lane);
+      prefill_page_lds<false, false, NB>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, ps_, o, lane);
     else if (tok0 <= wave_last)
-      prefill_page_lds<true, NB>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, o, lane);
+      prefill_page_lds<true, false, NB>(lds + cur * 32768, qf, tok0, lim, scale_log2, m_i, l_i, ps_, o, lane);
     __syncthreads();  // next page landed (vmcnt(0)) and everyone is done with this buffer
   }
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    const float inv = 1.0f / sum_q4(l_i[nb]);
+    const float inv = 1.0f / (PF_CUTS ? ps_[nb].l[0] : sum_q4(l_i[nb]));
     if (!valid[nb]) continue;
     u16* op = out + (int64_t)tokrow[nb] * H * HEAD_DIM + h * HEAD_DIM;
 #pragma unroll
@@ -870,11 +946,264 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   }
 }
 
+// 8 waves, two per SIMD, one workgroup per CU (PF_KERNEL=8, lab).  The workgroup owns 256 query
+// rows of one head; wave w (half hf = w >> 2, k = w & 3) owns rows 64 k + 32 hf .. +31 (two 16-row
+// column blocks), so the two waves sharing a SIMD (w, w + 4) have neighbouring rows.  Per page i
+// two segments separated by raw barriers:
+//   seg1(i): S(i) = K(i) q' - m (16 MFMA chains, k-slice outermost) and O += V(i-1) P(i-1) (+ the
+//            row-sum MFMAs): matrix work only;
+//   seg2(i): softmax of page i (VALU), LDS-DMA of K(i+3) / V(i+2), counted wait.
+// Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave is in its matrix segment
+// while its partner is in its softmax segment (MI355X_MICROARCH.md, two waves per SIMD).  With
+// the softmax cuts (PF_CUTS) the softmax segment is shorter than the partner's matrix segment.
+// K and V each have a 4-slot ring of 16 KiB half pages; slot reuse: K(i+3) goes to K(i-1)'s slot,
+// V(i+2) to V(i-2)'s, both last read one segment earlier by the lagging half.
+__global__ __launch_bounds__(512, 1) void attn_prefill8_kernel(const u16* __restrict__ q,
+                                                             const u16* __restrict__ kv, AttnBatch b, int H,
+                                                             int KV, float scale_log2, u16* __restrict__ out) {
+  constexpr int NB = 2;
+  __shared__ __attribute__((aligned(16))) char lds[8 * 16384];
+  const int bseq = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int hf = wave >> 2, kw = wave & 3;
+  const int n_rep = H / KV;
+  const int mqb = (b.max_q_len + 255) / 256;
+  int h, qbi;
+  if (gridDim.x % 8 == 0) {
+    const int n = gridDim.x, x = blockIdx.x;
+    const int wg = (x & 7) * (n >> 3) + (x >> 3);
+    const int r = wg % n_rep, t = wg / n_rep;
+    qbi = t % mqb;
+    h = (t / mqb) * n_rep + r;
+  } else {
+    h = blockIdx.x / mqb;
+    qbi = blockIdx.x % mqb;
+  }
+  const int g = h / n_rep;
+  const int t0 = b.seq_start[bseq];
+  const int T = b.seq_start[bseq + 1] - t0;
+  const int nqb = (T + 255) / 256;
+  const int qbk = mqb - 1 - qbi;  // heaviest blocks dispatch first
+  if (qbk >= nqb) return;         // uniform over the workgroup
+  const int qb0 = qbk * 256;
+  const int row0 = qb0 + kw * 64 + hf * 32;
+  bf16x8 qf[NB][4];
+  int lim[NB], tokrow[NB];
+  bool valid[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int row = row0 + nb * 16 + (lane & 15);
+    valid[nb] = row < T;
+    tokrow[nb] = t0 + (valid[nb] ? row : T - 1);
+    lim[nb] = b.positions[tokrow[nb]];
+    const u16* qp = q + ((int64_t)tokrow[nb] * H + h) * HEAD_DIM + 8 * (lane >> 4);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[nb][ks] = *(const bf16x8*)(qp + ks * 32);
+  }
+  if constexpr (PF_CUTS) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[nb][ks][j] = (__bf16)((float)qf[nb][ks][j] * scale_log2);
+  }
+  const int wave_last = row0 < T ? b.positions[t0 + min(row0 + 31, T - 1)] : -1;
+  int wave_min_lim = min(lim[0], lim[1]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wave_min_lim = min(wave_min_lim, __shfl_xor(wave_min_lim, o));
+  const int n_pages = b.positions[t0 + min(qb0 + 255, T - 1)] / KV_PAGE + 1;
+  typedef const __attribute__((address_space(4))) int* cptr;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  const cptr bt = (cptr)(b.block_table + (int64_t)bseq * b.max_pages);
+  const int swave = __builtin_amdgcn_readfirstlane(wave);
+  // this wave's 2 of the 16 1-KiB pieces of K (kind 0) or V (kind 1) of page j (clamped to a
+  // real page past the end: every segment issues the same count, so the waits stay counted;
+  // the clamped copy lands in a free slot and is never read)
+  auto issue = [&](int kind, int j) {
+    const int jj = j < n_pages ? j : n_pages - 1;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(kv + kv_block(bt[jj], 0, g, KV)), 0, 2 * KV_BLOCK_ELEMS * 2, 0x00020000);
+    char* dst = lds + (kind * 4 + (j & 3)) * 16384;
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const int piece = swave * 2 + pc;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)(dst + piece * 1024), 16, lane * 16,
+                                               (kind * 16 + piece) * 1024, 0, 0);
+    }
+  };
+  float m_i[NB], l_i[NB];
+  PfState ps_[NB];
+  f32x4 o[NB][8], sc[NB][4];
+  bf16x8 pf[NB][2];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    m_i[nb] = -INFINITY;
+    l_i[nb] = 0.f;
+    ps_[nb].negm = f32x4{0.f, 0.f, 0.f, 0.f};
+    ps_[nb].l = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int db = 0; db < 8; ++db) o[nb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  issue(0, 0);
+  issue(0, 1);
+  issue(1, 0);
+  issue(0, 2);
+  issue(1, 1);
+  vm_wait<0>();
+  raw_barrier();
+  if (hf) raw_barrier();  // stagger: waves 4-7 one segment behind
+  for (int i = 0; i <= n_pages; ++i) {
+    const bool do_s = i < n_pages && i * KV_PAGE <= wave_last;
+    const bool do_pv = i > 0 && (i - 1) * KV_PAGE <= wave_last;
+    // ---------------- seg1(i): S(i) and P.V(i-1), matrix work only
+    if (do_s) {
+      const char* kb = lds + (i & 3) * 16384 + lane * 16;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb) {
+          const bf16x8 kf = *(const bf16x8*)(kb + (tb * 4 + ks) * 1024);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (PF_CUTS && i > 0) c0 = ps_[nb].negm;
+            sc[nb][tb] = mfma16(kf, qf[nb][ks], ks ? sc[nb][tb] : c0);
+          }
+        }
+    }
+    if (do_pv) {
+      const char* vb = lds + (4 + ((i - 1) & 3)) * 16384 + lane * 16;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int db = 0; db < 8; ++db) {
+          const bf16x8 vf = *(const bf16x8*)(vb + (kt * 8 + db) * 1024);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) o[nb][db] = mfma16(vf, pf[nb][kt], o[nb][db]);
+        }
+        if constexpr (PF_CUTS) {
+          bf16x8 ones;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) ps_[nb].l = mfma16(ones, pf[nb][kt], ps_[nb].l);
+        }
+      }
+    }
+    if (i == n_pages) break;
+    raw_barrier();
+    // ---------------- seg2(i): staging, softmax(i), counted wait
+    issue(0, i + 3);
+    issue(1, i + 2);
+    if (do_s) {
+      const int tok0 = i * KV_PAGE;
+      const bool mask = tok0 + KV_PAGE - 1 > wave_min_lim;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        if (mask) {
+#pragma unroll
+          for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int t = tok0 + tb * 16 + 4 * (lane >> 4) + r;
+              sc[nb][tb][r] = (t <= lim[nb]) ? sc[nb][tb][r] : -INFINITY;
+            }
+        }
+        float pm[4];
+#pragma unroll
+        for (int tb = 0; tb < 4; ++tb)
+          pm[tb] = fmaxf(fmaxf(sc[nb][tb][0], sc[nb][tb][1]), fmaxf(sc[nb][tb][2], sc[nb][tb][3]));
+        const float pmax = max_q4(fmaxf(fmaxf(pm[0], pm[1]), fmaxf(pm[2], pm[3])));
+        if constexpr (PF_CUTS) {
+          float shift = 0.f;
+          if (i == 0) {
+            shift = pmax;
+            m_i[nb] = pmax;
+            ps_[nb].negm = f32x4{-pmax, -pmax, -pmax, -pmax};
+          } else if (__builtin_amdgcn_ballot_w64(pmax > RESCALE_THR)) {
+            shift = fmaxf(pmax, 0.f);
+            const float alpha = exp2_raw(-shift);
+            ps_[nb].l *= alpha;
+#pragma unroll
+            for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
+            m_i[nb] += shift;
+            ps_[nb].negm = f32x4{-m_i[nb], -m_i[nb], -m_i[nb], -m_i[nb]};
+          }
+          if (shift != 0.f) {
+#pragma unroll
+            for (int tb = 0; tb < 4; ++tb) sc[nb][tb] -= shift;
+          }
+#pragma unroll
+          for (int tb = 0; tb < 4; ++tb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sc[nb][tb][r] = exp2_raw(sc[nb][tb][r]);
+        } else {
+          const float m_new = fmaxf(m_i[nb], pmax * scale_log2);
+          if (__builtin_amdgcn_ballot_w64(m_new > m_i[nb] + RESCALE_THR)) {
+            const float alpha = exp2_raw(m_i[nb] - m_new);
+            l_i[nb] *= alpha;
+#pragma unroll
+            for (int db = 0; db < 8; ++db) o[nb][db] *= alpha;
+            m_i[nb] = m_new;
+          }
+          const float mneg = -m_i[nb];
+          float ps[4];
+#pragma unroll
+          for (int tb = 0; tb < 4; ++tb) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sc[nb][tb][r] = exp2_raw(fmaf(sc[nb][tb][r], scale_log2, mneg));
+            ps[tb] = (sc[nb][tb][0] + sc[nb][tb][1]) + (sc[nb][tb][2] + sc[nb][tb][3]);
+          }
+          l_i[nb] += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+        }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            pf[nb][kt][j] = (__bf16)sc[nb][2 * kt][j];
+            pf[nb][kt][4 + j] = (__bf16)sc[nb][2 * kt + 1][j];
+          }
+      }
+    }
+    // K(i+1) and V(i) (read in seg1(i+1)) landed: the leading half leaves its two newer
+    // groups in flight, the lagging half (one segment later at every barrier) one
+    if (hf)
+      vm_wait<4>();
+    else
+      vm_wait<8>();
+    raw_barrier();
+  }
+  if (!hf) raw_barrier();  // close the stagger
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const float inv = 1.0f / (PF_CUTS ? ps_[nb].l[0] : sum_q4(l_i[nb]));
+    if (!valid[nb]) continue;
+    u16* op = out + (int64_t)tokrow[nb] * H * HEAD_DIM + h * HEAD_DIM;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[nb][db][r] * inv);
+      *(u16x4*)(op + db * 16 + 4 * (lane >> 4)) = v;
+    }
+  }
+}
+
+#ifndef PF_KERNEL
+#define PF_KERNEL 4
+#endif
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
                          hipStream_t s) {
   // 48 query rows per wave (32 per wave: 1.6 % slower at 32B / 8k, archived); XCD-grouped block
   // order whenever the grid allows it
-  const int n = (b.max_q_len + 191) / 192 * H;
-  hipLaunchKernelGGL(attn_prefill_kernel<3>, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out,
-                     n % 8 == 0 ? 1 : 0);
+  if constexpr (PF_KERNEL == 8) {
+    const int n = (b.max_q_len + 255) / 256 * H;
+    hipLaunchKernelGGL(attn_prefill8_kernel, dim3(n, b.B), dim3(512), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out);
+    return;
+  }
+  constexpr int QB = 64 * PF_NB;
+  const int n = (b.max_q_len + QB - 1) / QB * H;
+  hipLaunchKernelGGL(attn_prefill_kernel<PF_NB>, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E,
+                     out, n % 8 == 0 ? 1 : 0);
 }

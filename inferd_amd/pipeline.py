@@ -313,12 +313,18 @@ class PipelineStage:
         self.ex.prepare_decode(self.sessions, n_steps, [self._bufs(m) for m in range(self.n_mb)])
 
     @torch.no_grad()
-    def decode(self, n_steps: int, record=None, record_logits=None):
+    def decode(self, n_steps: int, record=None, record_logits=None, force=None):
         """Run n_steps decode steps of every microbatch.  `record` (stage 0 only): list that
         receives (absolute step, microbatch, ids tensor copy) of every input fed to the first
         span; `record_logits` (last stage of a want_logits pipeline): list that receives
-        (absolute step, microbatch, device copy of the step's last-row logits [B, vocab]).
+        (absolute step, microbatch, device copy of the step's last-row logits [B, vocab]);
+        `force` (stage 0 only, teacher forcing for parity runs): int tensor [steps, B] -- the
+        ids fed at absolute step k are force[k] instead of the last stage's greedy choice.
         Sets self.tick_stats: host microseconds per tick, hand-off (exchange) and the rest."""
+        def feed(k, m):
+            if force is not None and self.first:
+                self.ids[m].copy_(force[self.step_base + k].to(self.ids[m].device, torch.int32),
+                                  non_blocking=True)
         S = self.S
         n_items = n_steps * self.n_mb
         t_x = 0.0
@@ -326,6 +332,7 @@ class PipelineStage:
         if S == 1:
             for i in range(n_items):
                 k, m = divmod(i, self.n_mb)
+                feed(k, m)
                 if record is not None:
                     record.append((self.step_base + k, m, self.ids[m].clone()))
                 self.ex.decode(m)
@@ -352,6 +359,7 @@ class PipelineStage:
             t_x += time.perf_counter() - tx
             if 0 <= i_cur < n_items:
                 k, m = divmod(i_cur, self.n_mb)
+                feed(k, m)
                 if self.first and record is not None:
                     record.append((self.step_base + k, m, self.ids[m].clone()))
                 self.ex.decode(m)

@@ -5,7 +5,8 @@ written bytes = WRITE_SIZE * 1024; MI355X_MICROARCH.md §HBM).  Alongside each c
 algorithmic bytes of one launch (operands read once, output written once), so the ratio
 shows how much of the L2/MALL tile re-reading reaches HBM.
 
-  tools/pmc_prefill.sh   (on the GPU box) -> profiles/traffic_prefill_rNN.json
+  tools/pmc_prefill.sh [B]   (on the GPU box) -> profiles/traffic_prefill_rNN.json (B = 1) or
+                             traffic_prefill_b<B>_rNN.json (B sequences of 8k tokens per call)
 """
 import json
 import os
@@ -15,8 +16,9 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_traffic import per_dispatch  # noqa: E402
 
-# Qwen3-32B, T = 8192 prompt tokens
+# Qwen3-32B, T = 8192 prompt tokens per sequence, B sequences per call (PMC_BATCH)
 h, I, H, KV, hd, T = 5120, 25600, 64, 8, 128, 8192
+B = int(os.environ.get("PMC_BATCH", "1"))
 
 
 def classify(name, state):
@@ -35,13 +37,15 @@ def classify(name, state):
 
 
 def alg_bytes():
+    """operands read once and outputs written once per launch (weights once per call; M = B*T rows)"""
     qkvN = (H + 2 * KV) * hd
+    M = B * T
     return {
-        "qkv_gemm": T * h * 2 + qkvN * h * 2 + T * H * hd * 2 + 2 * T * KV * hd * 2,
-        "attention": T * H * hd * 2 + 2 * T * KV * hd * 2 + T * H * hd * 2,
-        "o_gemm": T * H * hd * 2 + h * H * hd * 2 + 2 * T * h * 2,
-        "gateup_gemm": T * h * 2 + 2 * I * h * 2 + T * I * 2,
-        "down_gemm": T * I * 2 + h * I * 2 + 2 * T * h * 2,
+        "qkv_gemm": M * h * 2 + qkvN * h * 2 + M * H * hd * 2 + 2 * M * KV * hd * 2,
+        "attention": M * H * hd * 2 + 2 * M * KV * hd * 2 + M * H * hd * 2,
+        "o_gemm": M * H * hd * 2 + h * H * hd * 2 + 2 * M * h * 2,
+        "gateup_gemm": M * h * 2 + 2 * I * h * 2 + M * I * 2,
+        "down_gemm": M * I * 2 + h * I * 2 + 2 * M * h * 2,
     }
 
 
@@ -60,7 +64,7 @@ def main():
     alg = alg_bytes()
     per = {k: int(fetch.get(k, 0) + write.get(k, 0)) for k in sorted(set(fetch) | set(write))}
     print(json.dumps({
-        "workload": "qwen3-32b-prefill-8layers-T8192",
+        "workload": "qwen3-32b-prefill-8layers-T8192" + (f"-B{B}" if B > 1 else ""),
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes); bytes = 2*FETCH_SIZE*1024 "
                   "+ WRITE_SIZE*1024; mean over launches",
         "per_launch_bytes": per,

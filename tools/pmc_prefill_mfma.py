@@ -25,7 +25,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_prefill import H, KV, I, T, classify, h, hd  # noqa: E402
+from pmc_prefill import B, H, KV, I, T, classify, h, hd  # noqa: E402
 from pmc_traffic import rows  # noqa: E402
 
 COUNTERS = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU",
@@ -34,12 +34,13 @@ COUNTERS = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_
 
 def flops():
     qkvN = (H + 2 * KV) * hd
+    M = B * T
     return {
-        "qkv_gemm": 2.0 * T * qkvN * h,
-        "attention": 4.0 * H * hd * T * (T + 1) / 2,  # causal: QK^T and PV over the lower triangle
-        "o_gemm": 2.0 * T * h * H * hd,
-        "gateup_gemm": 2.0 * T * 2 * I * h,
-        "down_gemm": 2.0 * T * h * I,
+        "qkv_gemm": 2.0 * M * qkvN * h,
+        "attention": B * 4.0 * H * hd * T * (T + 1) / 2,  # causal: QK^T and PV over the lower triangle
+        "o_gemm": 2.0 * M * h * H * hd,
+        "gateup_gemm": 2.0 * M * 2 * I * h,
+        "down_gemm": 2.0 * M * h * I,
     }
 
 
