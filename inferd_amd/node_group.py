@@ -26,6 +26,11 @@ successor blocked; rank 0 then drops the request's sessions on every rank and ra
 failing rank's error, and every rank keeps serving.
 Layer split inside the group: pipeline.balanced_split (the lm_head priced on the rank that
 owns it, in decode bytes) over the stage's [start_layer, end_layer].
+
+A SpanGroup adds CAPACITY (a stage too large for one GPU's memory, KV pages for more sessions),
+not throughput: the reference's node serves one request at a time (task_scheduler.py:18), so a
+request walks the group's ranks one after another and N GPUs each run 1/N of the time.  The
+throughput of N GPUs is the RCCL pipeline of inferd_amd/pipeline.py (N microbatches in flight).
 """
 from __future__ import annotations
 

@@ -221,6 +221,48 @@ def test_bench_stage_split_qwen3_8b():
     assert [k for _, k in bench.stage_split(d, 1, 16, 2048)] == [36]
 
 
+def test_build_decode_batch_descriptor():
+    """inferd_kv_build_decode_batch (the descriptor a decode graph is captured on, advance = 1):
+    reserves n_steps more tokens per sequence all or nothing, positions / slots start at 0 (the
+    graph's scheduler step writes them), ctx_lens = the cached lengths, max_ctx_len = capacity."""
+    import ctypes as C
+    from inferd_amd import _lib
+    L = _lib.load()
+    t = _lib.c_p()
+    _lib.check(L.inferd_kv_create(12, t))
+    try:
+        for seq, n in ((5, 70), (6, 10)):
+            _lib.check(L.inferd_kv_reserve(t, seq, n))
+            _lib.check(L.inferd_kv_advance(t, seq, n))
+        keys = (C.c_uint64 * 2)(5, 6)
+        nw = L.inferd_kv_decode_batch_words(t, keys, 2, 60)
+        assert nw == 3 + 2 + 2 + 2 + 2 * 3          # max pages after the reservation: 3 (130 tokens)
+        host = (C.c_int32 * nw)()
+        b = _lib.Batch()
+        _lib.check(L.inferd_kv_build_decode_batch(t, keys, 2, 60, host, nw, None, b))
+        assert (b.n_seqs, b.n_tokens, b.max_q_len, b.max_ctx_len, b.max_pages, b.decode) == (2, 2, 1, 130, 3, 1)
+        w = list(host)
+        assert w[0:3] == [0, 1, 2] and w[3:5] == [0, 0] and w[5:7] == [0, 0]   # seq_start, positions, slots
+        assert w[7:9] == [70, 10]                                               # ctx_lens = cached lengths
+        assert w[9:12] == [0, 1, 3] and w[12:15] == [2, 4, 0]                   # block table (pages in order)
+        ln, npg = C.c_int32(), C.c_int32()
+        _lib.check(L.inferd_kv_query(t, 5, C.byref(ln), C.byref(npg)))
+        assert (ln.value, npg.value) == (70, 3)                                 # reserved, not advanced
+        # all or nothing: 512 more tokens of both sequences need 14 pages, 7 are free
+        free = C.c_int32()
+        _lib.check(L.inferd_kv_free_pages(t, C.byref(free)))
+        assert L.inferd_kv_build_decode_batch(t, keys, 2, 64 * 8, host, nw, None, b) == _lib.INFERD_ERR_ARG  # buffer
+        big = L.inferd_kv_decode_batch_words(t, keys, 2, 64 * 8)
+        hb = (C.c_int32 * big)()
+        assert L.inferd_kv_build_decode_batch(t, keys, 2, 64 * 8, hb, big, None, b) == _lib.INFERD_ERR_NOMEM
+        free2 = C.c_int32()
+        _lib.check(L.inferd_kv_free_pages(t, C.byref(free2)))
+        assert free2.value == free.value                                        # nothing taken
+        assert L.inferd_kv_decode_batch_words(t, (C.c_uint64 * 1)(99), 1, 1) == -1   # unknown sequence
+    finally:
+        L.inferd_kv_destroy(t)
+
+
 def test_build_batch_descriptor_layout():
     """The native batch builder (inferd_kv_build_batch) against a per-token restatement of
     the descriptor: seq_start | positions | slots (page * 64 + offset) | ctx_lens | block

@@ -7,6 +7,7 @@ log=$1; to=$2; cmd=$3
 for i in $(seq 1 20); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
   rc=$?
+  cat "$log" >> "$log.all"
   if [ $rc -eq 3 ] || { { grep -q "nothing was charged" "$log" && grep -q -i "busy\|no box\|no free" "$log"; } || grep -q "status=transient rc=None charged=0.0s\|status=transient rc=None charged=Nones" "$log"; }; then
     echo "[retry $i] no slot (rc=$rc), waiting" >> "$log.retries"
     sleep 90
