@@ -70,7 +70,13 @@ def _split(d, world, sizes):
     return [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
 
 
-def _worker(rank, world, port, n_steps, q, sizes=None):
+def _forced(world, n_steps, vocab):
+    """teacher-forcing table: ids fed at step k to microbatch m, [n_steps, world, B]"""
+    return torch.tensor([[[(37 * k + 11 * m + 5 * b) % vocab for b in range(3)] for m in range(world)]
+                         for k in range(n_steps)], dtype=torch.int32)
+
+
+def _worker(rank, world, port, n_steps, q, sizes=None, force=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -87,15 +93,32 @@ def _worker(rank, world, port, n_steps, q, sizes=None):
     st.prefill(prompts)
     st.prepare_decode(n_steps)
     rec = []
-    st.decode(2, record=rec)
-    st.decode(n_steps - 2, record=rec)
+    if force:   # PipelineStage.decode(force=...): [steps, B] per microbatch -> this test's table
+        f = _forced(world, n_steps, d.vocab)
+        tab = {m: f[:, m] for m in range(world)}
+
+        class ByMb:
+            """force[k] for the microbatch being fed (decode() indexes force by absolute step)"""
+            def __init__(self):
+                self.m = 0
+
+            def __getitem__(self, k):
+                v = tab[self.m][k]
+                self.m = (self.m + 1) % world
+                return v
+        fz = ByMb()
+        st.decode(2, record=rec, force=fz)
+        st.decode(n_steps - 2, record=rec, force=fz)
+    else:
+        st.decode(2, record=rec)
+        st.decode(n_steps - 2, record=rec)
     if rank == 0:
         q.put([(k, m, t.tolist()) for k, m, t in rec] + [("final", m, st.ids[m].tolist()) for m in range(world)])
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _reference(world, n_steps, sizes=None):
+def _reference(world, n_steps, sizes=None, force=False):
     """Single process: the same spans chained directly (bf16 hand-off, like the pipeline)."""
     d = R.CONFIGS["tiny"]
     split = _split(d, world, sizes)
@@ -112,10 +135,13 @@ def _reference(world, n_steps, sizes=None):
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, d.vocab, (B, 9), generator=g) for _ in range(world)]
     feeds = {}
+    f = _forced(world, n_steps, d.vocab) if force else None
     for m in range(world):
         for b in range(B):
             nxt = int(torch.argmax(sp.forward_cached((m, b), prompts[m][b:b + 1])[0, -1]))
             for k in range(n_steps + 1):
+                if f is not None and k < n_steps:
+                    nxt = int(f[k, m, b])
                 feeds[(k, m, b)] = nxt
                 nxt = int(torch.argmax(sp.forward_cached((m, b), torch.tensor([[nxt]]))[0, -1]))
     return feeds
@@ -141,5 +167,32 @@ def test_pipeline_matches_single_process(world, sizes):
             assert ids == [ref[(n_steps, m, b)] for b in range(3)]
             continue
         assert ids == [ref[(k, m, b)] for b in range(3)], (k, m)
+        seen += 1
+    assert seen == n_steps * world
+
+
+def test_pipeline_teacher_forcing():
+    """PipelineStage.decode(force=...): stage 0 feeds the given ids instead of the ring's greedy
+    choice at every step; the fed ids are exactly the table and the last stage's final choice is
+    the single-process chain's after the same forced steps."""
+    world, n_steps = 3, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_steps, q, None, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    rec = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = _reference(world, n_steps, None, force=True)
+    f = _forced(world, n_steps, R.CONFIGS["tiny"].vocab)
+    seen = 0
+    for k, m, ids in rec:
+        if k == "final":
+            assert ids == [ref[(n_steps, m, b)] for b in range(3)]
+            continue
+        assert ids == f[k, m].tolist(), (k, m)
         seen += 1
     assert seen == n_steps * world
