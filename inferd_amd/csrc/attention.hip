@@ -1381,13 +1381,37 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_pipe_kernel(const u16* __
     const bool nxt = live && (i + 1) < n_pages && (i + 1) * KV_PAGE <= wave_last;
     bf16x8 pf[NB][2];
     f32x4 sn[NB][4];
-    // phase A: S(i+1) beside exp / packing of page i
-    if (nxt) s_mfma(i + 1, sn);
-    if (cur) s_exp(sc, pf);
-    // phase B: P.V(i) beside the max of page i+1 (its rescale waits for P.V(i) by data dependence)
-    if (cur) pv_mfma(i, pf);
-    if (nxt) {
+#ifdef PF_PIPE_BLOCK
+    if (cur && nxt) {
+      // steady state: each phase one basic block, MFMAs interleaved with the other page's VALU
+      __builtin_amdgcn_sched_barrier(0);
+      s_mfma(i + 1, sn);
+      s_exp(sc, pf);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read (the 16 K fragments)
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (exp / pack)
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      pv_mfma(i, pf);
       s_max(i + 1, sn, false);
+    } else
+#endif
+    {
+      // phase A: S(i+1) beside exp / packing of page i
+      if (nxt) s_mfma(i + 1, sn);
+      if (cur) s_exp(sc, pf);
+      // phase B: P.V(i) beside the max of page i+1 (its rescale waits for P.V(i) by data dependence)
+      if (cur) pv_mfma(i, pf);
+      if (nxt) s_max(i + 1, sn, false);
+    }
+    if (nxt) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
