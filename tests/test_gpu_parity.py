@@ -484,7 +484,9 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     replays.  Checked against the oracle: the last stage's prefill logits of sequence 0 (a
     2048-token CPU forward through all 36 layers) are no further from the fp32 oracle than the
     bf16 oracle is (NOISE_RATIO on the rms over the vocabulary; the distance to the bf16 oracle is
-    recorded); the first stage boundary's hidden state (sequences 0 and 1) matches the oracle.  Checked against a single 36-layer HIP span: the greedy ids fed back to stage 0."""
+    recorded); the first stage boundary's hidden state of sequence 0 is no further from an fp32
+    oracle than the bf16 oracle is, and (boundaries up to 9 layers deep, sequences 0 and 1) is
+    within the span tolerance of the bf16 oracle.  Checked against a single 36-layer HIP span: the greedy ids fed back to stage 0."""
     world = len(sizes)
     port = _free_port()
     _spawn(_pipe_worker, [(r, world, port, sizes, str(tmp_path)) for r in range(world)])
@@ -500,16 +502,19 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     ref = R.RefSpan(d, SEED, 0, sizes[0] - 1, True, False, torch.bfloat16, "sdpa").forward(ids)
     h = pipe["hidden"].reshape(2, T8, -1)
     e = [errs(h[b], ref[b]) for b in range(2)]
-    noise = None
-    if sizes[0] <= 5:   # fp32 oracle on sequence 0: the bf16 noise floor of this boundary
-        ref32 = R.RefSpan(d, SEED, 0, sizes[0] - 1, True, False, torch.float32, "sdpa").forward(ids[:1])[0]
-        noise = {"engine_vs_fp32": errs(h[0], ref32), "bf16_ref_vs_fp32": errs(ref[0], ref32)}
-        print(f"noise floor: engine vs fp32 rms {noise['engine_vs_fp32']['rms_rel']:.2e}, "
-              f"bf16 reference vs fp32 rms {noise['bf16_ref_vs_fp32']['rms_rel']:.2e}")
-        assert noise["engine_vs_fp32"]["rms_rel"] <= NOISE_RATIO * noise["bf16_ref_vs_fp32"]["rms_rel"]
+    # fp32 oracle on sequence 0: the bf16 noise floor of this boundary, at every depth
+    ref32 = R.RefSpan(d, SEED, 0, sizes[0] - 1, True, False, torch.float32, "sdpa").forward(ids[:1])[0]
+    noise = {"engine_vs_fp32": errs(h[0], ref32), "bf16_ref_vs_fp32": errs(ref[0], ref32)}
+    print(f"noise floor: engine vs fp32 rms {noise['engine_vs_fp32']['rms_rel']:.2e}, "
+          f"bf16 reference vs fp32 rms {noise['bf16_ref_vs_fp32']['rms_rel']:.2e}")
+    assert noise["engine_vs_fp32"]["rms_rel"] <= NOISE_RATIO * noise["bf16_ref_vs_fp32"]["rms_rel"]
     print(f"{sizes}: ids identical over {STEPS8} steps x {world} microbatches; stage-0 boundary "
           f"max_norm {[x['max_norm'] for x in e]} rms_rel {[x['rms_rel'] for x in e]}")
-    assert all(span_ok(x) for x in e)
+    # the span tolerance (TOL_SPAN / TOL_SPAN_RMS) holds for the shallow boundaries (<= 9 layers);
+    # 18 layers deep the engine is 3.6 % (rms) from the bf16 oracle, as far as the bf16 oracle
+    # itself is from fp32 arithmetic there, so deeper than 9 layers the noise floor above decides
+    if sizes[0] <= 9:
+        assert all(span_ok(x) for x in e)
     lg = torch.load(os.path.join(tmp_path, "logits0.pt"), weights_only=True)
     o16, o32 = q8b_prefill_logits_oracle["bf16"], q8b_prefill_logits_oracle["fp32"]
     el = errs(lg, o16)
