@@ -1625,8 +1625,9 @@ void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
 // launch_gemm's persistent whole-tile path with the EPI_QKV epilogue: q/k RMSNorm + RoPE to
 // q_out and the K cache, V to the cache (what launch_qk_norm_rope_kv does from a stored q/k/v
 // row).  Needs that path: the 4-wave persistent kernel selected, no tail split, 32-bit C offsets
-// (C is unused here) and one head per wave column (N = (H + 2 KV) * 128).  The span skips it
-// (two-kernel path, A/B) when created with INFERD_FUSE_QKV_EPI=0.
+// (C is unused here) and one head per wave column (N = (H + 2 KV) * 128).  The span uses it for
+// every prefill; the two-kernel path (plain GEMM + qk_norm_rope) remains the reference the
+// parity tests compare it with.
 bool launch_gemm_qkv_fused(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, const QkvEpilogue& e,
                            hipStream_t s) {
   if (!gemm_uses_tiled(M, N, K, EPI_NONE) || !use_w4(M, N, K, EPI_NONE)) return false;

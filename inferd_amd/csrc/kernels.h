@@ -93,7 +93,7 @@ struct DecodeNorm {
 // at span creation (gemm_ws_alloc: the split's fixed maximum, 8 XCDs x 32 slices of a 256x256
 // fp32 tile = 64 MiB, and 512 zeroed tickets), so a forward call never allocates and a graph
 // capture may contain the split (one workspace per span: spans on different streams never
-// share tickets).  split = 0 disables the tail split (INFERD_GEMM_SPLIT=0, read at creation).
+// share tickets).  split = 0 disables the tail split (spans whose max_tokens < 512 never split).
 struct GemmWs {
   float* ws = nullptr;
   unsigned* cnt = nullptr;

@@ -3,10 +3,10 @@
 prefill: Qwen3-32B dims (H=64, KV=8), B x T causal prompt (BASELINE config 5)
 decode : Qwen3-8B dims (H=32, KV=8), B=16 single tokens at ctx 2048 (BASELINE config 3)
 Random bf16 q and K/V (uniform, rule 25); algorithmic flops count T(T+1)/2 keys per row.
-Variants are selected per call through environment variables (e.g. INFERD_ATTN_PREFILL=<v>),
-interleaved over rounds in one process.
+The library is the span library (a lab build is selected with INFERD_LIB; tools/attn_ab.py
+compares several builds in one process).
 
-usage: python tools/attn_bench.py [--mode prefill|decode] [--env NAME=v1,v2]
+usage: python tools/attn_bench.py [--mode prefill|decode]
 """
 import argparse
 import os
@@ -28,7 +28,6 @@ def main():
     p.add_argument("--ctx", type=int, default=2048)
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=3)
-    p.add_argument("--env", default="", help="NAME=v1,v2 : variants to interleave")
     args = p.parse_args()
     L = _lib.load()
     dev = torch.device("cuda", 0)
@@ -57,34 +56,26 @@ def main():
     else:
         flops = B * 4.0 * H * 128 * n
         bytes_ = B * n * KV * 128 * 2 * 2
-    name, vals = (args.env.split("=") + [""])[:2] if args.env else ("", "")
-    variants = vals.split(",") if vals else [""]
-    times = {v: [] for v in variants}
-    outs = {}
-    for rnd in range(args.rounds):
-        for v in variants:
-            if name:
-                os.environ[name] = v
-            call = lambda: _lib.check(L.inferd_attention(q.data_ptr(), kv.data_ptr(), batch, H, KV,  # noqa: E731
-                                                         out.data_ptr(), ws.data_ptr(), ws_bytes, st))
+    times = []
+
+    def call():
+        _lib.check(L.inferd_attention(q.data_ptr(), kv.data_ptr(), batch, H, KV,
+                                      out.data_ptr(), ws.data_ptr(), ws_bytes, st))
+    for _ in range(args.rounds):
+        call()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
             call()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(args.reps):
-                call()
-            e1.record()
-            torch.cuda.synchronize()
-            times[v].append(e0.elapsed_time(e1) / args.reps)
-            if rnd == 0:
-                outs[v] = out.clone()
-    for v in variants:
-        t = sorted(times[v])
-        med = t[len(t) // 2]
-        line = f"{args.mode} {name}={v!r}: {med * 1e3:9.1f} us  {flops / med / 1e9:7.1f} TF/s"
-        if bytes_:
-            line += f"  {bytes_ / med / 1e6:7.1f} GB/s"
-        d = (outs[v].float() - outs[variants[0]].float()).abs().max().item()
-        print(line + f"  maxdiff={d:.3g}", flush=True)
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1) / args.reps)
+    t = sorted(times)
+    med = t[len(t) // 2]
+    line = f"{args.mode}: {med * 1e3:9.1f} us  {flops / med / 1e9:7.1f} TF/s"
+    if bytes_:
+        line += f"  {bytes_ / med / 1e6:7.1f} GB/s"
+    print(line, flush=True)
 
 
 if __name__ == "__main__":

@@ -1,8 +1,9 @@
-"""Prefill GEMM A/B on the GPU box: every INFERD_GEMM_TILE variant on the Qwen3-32B
-projection shapes (BASELINE config 5, M = 8192 prompt rows), interleaved rounds in ONE
-process (cdna_hip_programming.md §5.4 rule 24), uniform random operands (rule 25).
+"""Prefill GEMM timing on the GPU box: the span library's GEMM (inferd_gemm; a lab build is
+selected with INFERD_LIB, see tools/build_probes.sh) on the Qwen3-32B projection shapes
+(BASELINE config 5, M = 8192 prompt rows), interleaved rounds in ONE process
+(cdna_hip_programming.md §5.4 rule 24), uniform random operands (rule 25).
 
-usage: python tools/gemm_bench.py [--m 8192] [--rounds 5] [--variants ring,256,torch]
+usage: python tools/gemm_bench.py [--m 8192] [--rounds 5] [--variants span,torch]
 ("torch" times torch.matmul = hipBLASLt on the same operands, no epilogue: the library ceiling.)
 """
 import argparse
@@ -31,8 +32,7 @@ def main():
     p.add_argument("--m", type=int, default=8192)
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--reps", type=int, default=3)
-    p.add_argument("--variants", default="ring,256")
-    p.add_argument("--env-name", default="INFERD_GEMM_TILE", help="environment variable the variants set")
+    p.add_argument("--variants", default="span")
     p.add_argument("--shapes", default=",".join(SHAPES))
     args = p.parse_args()
     L = _lib.load()
@@ -62,7 +62,6 @@ def main():
                 if v == "torch":  # hipBLASLt through torch.matmul: plain GEMM, no epilogue (ceiling probe)
                     call = lambda: torch.matmul(a, w.t())  # noqa: E731
                 else:
-                    os.environ[args.env_name] = v
                     call = lambda: _lib.check(L.inferd_gemm(a.data_ptr(), wp.data_ptr(), c.data_ptr(),  # noqa: E731
                                                             None if r is None else r.data_ptr(), M, n, k, epi, st))
                 call()
