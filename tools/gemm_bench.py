@@ -24,6 +24,11 @@ SHAPES = {  # name: (N_out, K, epilogue)
     # K sweep on the qkv shape: time(K) = per-tile overhead + K-proportional main loop
     "qkv_k1": (10240, 1024, 0),
     "qkv_k2": (10240, 2048, 0),
+    # the 2.5-round o/down grids against whole-round neighbours (512 tiles = 2 rounds, 768 = 3)
+    "o_n4096": (4096, 8192, 1),
+    "o_n6144": (6144, 8192, 1),
+    "down_n4096": (4096, 25600, 1),
+    "down_n6144": (6144, 25600, 1),
 }
 
 

@@ -106,7 +106,7 @@ def main():
             })
         out[c] = row
     print(json.dumps({
-        "workload": "qwen3-32b-prefill-8layers-T8192",
+        "workload": "qwen3-32b-prefill-8layers-T8192" + (f"-B{B}" if B > 1 else ""),
         "method": "rocprofv3 --pmc " + " ".join(COUNTERS) + " (one pass); durations from a separate "
                   "--kernel-trace pass; means over launches; see tools/pmc_prefill_mfma.py for each field",
         "classes": out,
