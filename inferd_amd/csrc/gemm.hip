@@ -753,6 +753,55 @@ __device__ __forceinline__ void tile_order(const SplitTail& st, int grid_m, int 
   tile_order_v(st, grid_m, grid_n, blockIdx.x, gridDim.x, bm, bn, slice, nsl, sidx);
 }
 
+#ifdef W4_STAMP
+// Lab builds only (tools/build_probes.sh gemm.hip st='-DW4_STAMP=1'; tools/w4_stamps.py):
+// per workgroup of gemm_w4_kernel, 100 MHz real-time stamps at start / after the K-loop /
+// after the tail-split publish or combine / end, and the XCC and HW ids.
+__device__ unsigned long long w4_stamp_buf[4096 * 6];
+extern "C" int inferd_lab_w4_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(w4_stamp_buf), (size_t)min(n, 4096) * 6 * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#define W4_STAMP_AT(k)                                                               \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                       \
+    w4_stamp_buf[blockIdx.x * 6 + (k)] = __builtin_amdgcn_s_memrealtime();           \
+    if ((k) == 0) {                                                                  \
+      w4_stamp_buf[blockIdx.x * 6 + 4] = __builtin_amdgcn_s_getreg((20 << 0) | (15 << 11)); \
+      w4_stamp_buf[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_getreg((4 << 0) | (31 << 11));  \
+    }                                                                                \
+  }
+#else
+#define W4_STAMP_AT(k)
+#endif
+
+// Tail-split partials: slice sl of split tile sidx is 65536 fp32 at ws + (sidx * nsl + sl) *
+// 65536; accumulator tile (i, j) of thread x is the 16 bytes at ((i * 8 + j) * 256 + x) (one
+// 1 KiB run per wave store).  The publisher stores straight from the accumulator AGPRs
+// (global_store_dwordx4 with an AGPR source, sc1: write-through to the coherence point), so no
+// accumulator is copied to VGPRs; the combiner, after an agent-scope acquire, reads them with
+// plain loads in its epilogue and sums over the slices in slice order (two slices: p0 + p1, the
+// same bits whichever slice combines).
+__device__ __forceinline__ void split_publish(const f32x4 (&acc)[8][8], float* part, int slice) {
+  f32x4* dst = (f32x4*)(part + (size_t)slice * 65536) + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + (i * 8 + j) * 256), "a"(acc[i][j]) : "memory");
+}
+
+__device__ __forceinline__ f32x4 split_tile_sum(const f32x4& mine, const float* part, int nsl, int slice, int i,
+                                                int j) {
+  const f32x4* src = (const f32x4*)part + (i * 8 + j) * 256 + threadIdx.x;
+  if (nsl == 2) return mine + src[(size_t)(1 - slice) * 16384];
+  f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+  for (int sl = 0; sl < nsl; ++sl) {
+    const f32x4 l = src[(size_t)sl * 16384];
+    sum += (sl == slice) ? mine : l;
+  }
+  return sum;
+}
+
 // ============================================================ 4-wave 256x256 prefill GEMM
 // gemm_w4_kernel: the same 256x256 output tile and K-step 64, on FOUR waves of 128x128
 // (8x8 accumulator tiles = 256 AGPRs each, one wave per SIMD).  Per K-step a wave issues
@@ -774,6 +823,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   __shared__ __attribute__((aligned(16))) char lds[2 * 65536];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
+  W4_STAMP_AT(0);
   int bm, bn, slice = 0, nsl = 1, sidx = 0;
   tile_order(st, grid_m, grid_n, bm, bn, slice, nsl, sidx);
   const int m0 = bm * 256;
@@ -935,7 +985,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   iter(std::integral_constant<int, 1>{}, t);
   iter(std::integral_constant<int, 2>{}, t + 1);
   acc_fence();
+  W4_STAMP_AT(1);
 
+  float* part = nsl > 1 ? st.ws + (size_t)sidx * nsl * 65536 : nullptr;
+  auto tile_sum = [&](int i, int j) -> f32x4 {
+    return nsl > 1 ? split_tile_sum(acc[i][j], part, nsl, slice, i, j) : acc[i][j];
+  };
   if (nsl > 1) {  // ---- tail split: publish or combine (tools/archive/gemm_superseded.hip had the same in the 8-wave ring)
     __syncthreads();
     unsigned* ticket_lds = (unsigned*)lds;
@@ -944,23 +999,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     if (threadIdx.x == 0) ticket_lds[0] = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     const unsigned ticket = ticket_lds[0];
-    float* part = st.ws + (size_t)sidx * nsl * 65536;
     if (ticket + 1 < (unsigned)nsl) {
-      unsigned long long* dst = (unsigned long long*)(part + (size_t)slice * 65536);
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const unsigned long long v = ((unsigned long long)__float_as_uint(acc[i][j][2 * hh + 1]) << 32) |
-                                         __float_as_uint(acc[i][j][2 * hh]);
-            __hip_atomic_store(dst + (((i * 8 + j) * 2 + hh) * 256 + threadIdx.x), v, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          }
+      split_publish(acc, part, slice);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      W4_STAMP_AT(2);
+      W4_STAMP_AT(3);
       return;
     }
     if (threadIdx.x == 0) {
@@ -970,29 +1015,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
       __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          float v0 = 0.f, v1 = 0.f;
-          for (int sl = 0; sl < nsl; ++sl) {
-            if (sl == slice) {
-              v0 += acc[i][j][2 * hh];
-              v1 += acc[i][j][2 * hh + 1];
-            } else {
-              const unsigned long long* src = (const unsigned long long*)(part + (size_t)sl * 65536);
-              const unsigned long long v = __hip_atomic_load(src + ((i * 8 + j) * 2 + hh) * 256 + threadIdx.x,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              v0 += __uint_as_float((unsigned)v);
-              v1 += __uint_as_float((unsigned)(v >> 32));
-            }
-          }
-          acc[i][j][2 * hh] = v0;
-          acc[i][j][2 * hh + 1] = v1;
-        }
+    // acquire (L1 / non-coherent L2 lines invalidated); the epilogue adds the other slices'
+    // partials with plain loads (relaxed atomic loads were issued one round trip at a time:
+    // tools/w4_stamps.py measured 54 us of combine for 256 KiB)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  W4_STAMP_AT(2);
 
   // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
 #pragma unroll
@@ -1004,10 +1032,11 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
       for (int nt = 0; nt < 4; ++nt) {
         const int col = n0 + wc * 64 + nt * 16 + 4 * (lane >> 4);
         u16x4 v;
+        const f32x4 g4 = tile_sum(i, nt), u4 = tile_sum(i, 4 + nt);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float gg = rbf(acc[i][nt][r]);
-          const float uu = rbf(acc[i][4 + nt][r]);
+          const float gg = rbf(g4[r]);
+          const float uu = rbf(u4[r]);
           v[r] = f2bf(rbf(silu_f(gg)) * uu);
         }
         *(u16x4*)(C + (int64_t)row * ldc + col) = v;
@@ -1019,9 +1048,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
         u16x4 v;
         u16x4 rr;
         if constexpr (EPI == EPI_RESID) rr = *(const u16x4*)(R + (int64_t)row * ldr + col);
+        const f32x4 a4 = tile_sum(i, j);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float o = acc[i][j][r];
+          float o = a4[r];
           if constexpr (EPI == EPI_RESID) o = rbf(o) + bf2f(rr[r]);
           v[r] = f2bf(o);
         }
@@ -1029,6 +1059,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
       }
     }
   }
+  W4_STAMP_AT(3);
 }
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1150,7 +1181,9 @@ __device__ __forceinline__ void qkv_epilogue(const f32x4 (&acc)[8][8], const Qkv
 // iterations), i.e. BEFORE the epilogue: the next tile's HBM latency overlaps the store
 // tail instead of following it.  The first K-step of a unit starts its accumulators with a
 // zero C operand (no zeroing pass).  Buffer of step t = (t + par) & 1, par carried across
-// units.  Whole tiles only: grids that need the tail split run gemm_w4_kernel.
+// units.  Whole tiles only: grids that need the tail split run gemm_w4_kernel (the split
+// inside this loop, as a separate instantiation, spilled 60 VGPRs and ran o / down 2-4 %
+// slower than gemm_w4_kernel's: tools/gemm_bench.py A/B, round 4).
 template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     const u16* __restrict__ A, int64_t lda, const u16* __restrict__ Wp, int KT, int n_tiles_w,

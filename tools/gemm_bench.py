@@ -3,10 +3,13 @@ selected with INFERD_LIB, see tools/build_probes.sh) on the Qwen3-32B projection
 (BASELINE config 5, M = 8192 prompt rows), interleaved rounds in ONE process
 (cdna_hip_programming.md §5.4 rule 24), uniform random operands (rule 25).
 
-usage: python tools/gemm_bench.py [--m 8192] [--rounds 5] [--variants span,torch]
-("torch" times torch.matmul = hipBLASLt on the same operands, no epilogue: the library ceiling.)
+usage: python tools/gemm_bench.py [--m 8192] [--rounds 5] [--variants span,torch,name=lib.so,...]
+("torch" times torch.matmul = hipBLASLt on the same operands, no epilogue: the library ceiling;
+name=lib.so loads another build of the span library -- e.g. a tools/probe_libs/ build -- so
+A/B variants run interleaved in one process on one box.)
 """
 import argparse
+import ctypes
 import os
 import sys
 
@@ -41,6 +44,15 @@ def main():
     p.add_argument("--shapes", default=",".join(SHAPES))
     args = p.parse_args()
     L = _lib.load()
+    libs = {"span": L}
+    for v in args.variants.split(","):
+        if "=" in v:
+            lab = ctypes.CDLL(v.split("=", 1)[1])
+            for name in ("inferd_gemm", "inferd_last_error"):
+                res, a = _lib.SIGNATURES[name]
+                getattr(lab, name).restype = res
+                getattr(lab, name).argtypes = a
+            libs[v.split("=", 1)[0]] = lab
     dev = torch.device("cuda", 0)
     M = args.m
     st = _lib.stream_ptr()
@@ -58,7 +70,7 @@ def main():
         r = (torch.rand(M, n, device=dev) * 2 - 1).to(torch.bfloat16) if epi == 1 else None
         bufs[name] = (a, wp, c, r, n, k, epi, w)
     torch.cuda.synchronize()
-    variants = args.variants.split(",")
+    variants = [v.split("=", 1)[0] for v in args.variants.split(",")]
     times = {(s, v): [] for s in bufs for v in variants}
     outs = {}
     for rnd in range(args.rounds):
@@ -67,8 +79,9 @@ def main():
                 if v == "torch":  # hipBLASLt through torch.matmul: plain GEMM, no epilogue (ceiling probe)
                     call = lambda: torch.matmul(a, w.t())  # noqa: E731
                 else:
-                    call = lambda: _lib.check(L.inferd_gemm(a.data_ptr(), wp.data_ptr(), c.data_ptr(),  # noqa: E731
-                                                            None if r is None else r.data_ptr(), M, n, k, epi, st))
+                    LL = libs[v]
+                    call = lambda: _lib.check(LL.inferd_gemm(a.data_ptr(), wp.data_ptr(), c.data_ptr(),  # noqa: E731
+                                                             None if r is None else r.data_ptr(), M, n, k, epi, st))
                 call()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
