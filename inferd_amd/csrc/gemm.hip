@@ -725,6 +725,8 @@ __device__ __forceinline__ void tile_order_v(const SplitTail& st, int grid_m, in
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
   int tile = wg;
   if (st.split > 1) {  // grid = 8 * units_per_xcd
+    // (the split slices first instead, so the publishing CUs take whole tiles while the
+    // combining ones finish: no change, o 534.4 vs 534.4 us, round 4)
     const int x = wg / st.units_per_xcd, li = wg - x * st.units_per_xcd;
     if (li < st.full_per_xcd) {
       tile = x * st.tiles_per_xcd + li;
@@ -770,8 +772,19 @@ extern "C" int inferd_lab_w4_stamps(unsigned long long* host, int n) {
       w4_stamp_buf[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_getreg((4 << 0) | (31 << 11));  \
     }                                                                                \
   }
+// gemm_w4p_kernel<EPI_QKV>: per unit v and wave, stamps at the unit's start (step 0 landed),
+// after its K-loop and after its epilogue: w4p_stamp_buf[(v * 4 + wave) * 4 + k]
+__device__ unsigned long long w4p_stamp_buf[2048 * 16];
+extern "C" int inferd_lab_w4p_stamps(unsigned long long* host, int n_units) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(w4p_stamp_buf), (size_t)min(n_units, 2048) * 16 * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#define W4P_STAMP_AT(k)                                                                     \
+  if (EPI == EPI_QKV && (threadIdx.x & 63) == 0 && v < 2048)                                \
+    w4p_stamp_buf[(v * 4 + (threadIdx.x >> 6)) * 4 + (k)] = __builtin_amdgcn_s_memrealtime();
 #else
 #define W4_STAMP_AT(k)
+#define W4P_STAMP_AT(k)
 #endif
 
 // Tail-split partials: slice sl of split tile sidx is 65536 fp32 at ws + (sidx * nsl + sl) *
@@ -1357,6 +1370,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     }
     first = false;
     raw_barrier();
+    W4P_STAMP_AT(0);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       read_b(0, g, par);
@@ -1370,7 +1384,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     Unit un = u;
     // EPI_QKV: no cross-tile prefetch -- its epilogue's own loads (positions, cos/sin,
     // slots) would wait behind the next tile's 32 in-flight pieces (in-order vmcnt); the
-    // next tile's sources are then computed after the epilogue (fewer live registers in it)
+    // next tile's sources are then computed after the epilogue (fewer live registers in it).
+    // Round 4 (tools/span_ab.py, tools/w4p_stamps.py): with the prefetch, -14 / -13 / +3 us
+    // per 32B launch on three boxes; issuing the pieces inside the epilogue once its own loads
+    // were in flight spilled into the K-loop (14x slower); V accumulated transposed for 8-byte
+    // V^T stores and every cos/sin load issued up front: no change.  The epilogue's ~19 us per
+    // unit (every CU at once) stays.
     constexpr bool XPF = EPI != EPI_QKV;
     if (has_next) {
       un = unit_of(vn);
@@ -1379,6 +1398,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     iter(std::integral_constant<int, 1>{}, ZF{}, u.nK - 2, par, XPF && has_next);
     iter(std::integral_constant<int, 2>{}, ZF{}, u.nK - 1, par, XPF && has_next);
     acc_fence();
+    W4P_STAMP_AT(1);
 
     if constexpr (EPI == EPI_QKV) {
       qkv_epilogue(acc, qe, u.m0 + wr * 128, (u.n0 >> 7) + wc, M, lane);
@@ -1423,6 +1443,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
         }
       }
     }
+    W4P_STAMP_AT(2);
     if (!has_next) break;
     par = (par + u.nK) & 1;
     u = un;

@@ -366,6 +366,33 @@ def test_prefill_qkv_epilogue_and_separate_kernel_vs_oracle():
         assert e < TOL_REL
 
 
+def test_prefill_qkv_epilogue_unaligned_slots_vs_oracle():
+    """The q/k/v GEMM epilogue's V^T store takes 4 consecutive tokens per 8-byte store when their
+    cache slots are consecutive and 4-aligned, else token by token: a sequence with 3 cached
+    tokens extended by 600 (every group unaligned) beside a fresh 520-token one (aligned), then
+    a decode step reading both caches.  One Qwen3-8B-dims layer against the oracle."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["qwen3-8b"]
+    g = torch.Generator().manual_seed(11)
+    x0 = (torch.randn(3, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+    x1 = (torch.randn(600 + 520, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+    x2 = (torch.randn(2, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+    oracle = R.RefSpan(R.CONFIGS["qwen3-8b"], SEED, 5, 5, False, False, torch.bfloat16, "sdpa")
+    oracle.forward_cached("c", x0[None])
+    refs = [torch.cat([oracle.forward_cached("c", x1[None, :600])[0], oracle.forward_cached("d", x1[None, 600:])[0]]),
+            torch.cat([oracle.forward_cached("c", x2[None, :1])[0], oracle.forward_cached("d", x2[None, 1:])[0]])]
+    s = SpanRuntime(d, 5, 1, has_embed=False, has_lm_head=False, device=DEV, max_positions=1280,
+                    kv_pages=48, max_tokens=1280, max_seqs=4)
+    s.init_synthetic(SEED)
+    s.forward([("c", 3)], x=x0, want_hidden=True)
+    outs = [s.forward([("c", 600), ("d", 520)], x=x1, want_hidden=True)["hidden"].cpu(),
+            s.forward([("c", 1), ("d", 1)], x=x2, want_hidden=True)["hidden"].cpu()]
+    for name, o, r in zip(("prefill 1120 (unaligned + aligned V^T stores)", "decode"), outs, refs):
+        e = rel_err(o, r)
+        print(f"{name}: vs oracle rel err {e:.2e}")
+        assert e < TOL_REL
+
+
 def test_config3_q8b_layer_b16_ctx2048_decode_graph():
     """BASELINE config 3 at its full size, on the exact bench path: one Qwen3-8B layer,
     16 sequences prefilled with 2048 tokens each (two sequences per call, as bench.py does),
