@@ -38,6 +38,7 @@ def main():
     p.add_argument("--rounds", type=int, default=7)
     p.add_argument("--reps", type=int, default=3)
     p.add_argument("--heads", default="0,21,42,63")
+    p.add_argument("--qscale", type=float, default=1.2, help="q ~ N(0, qscale^2): larger scores, more rescales")
     args = p.parse_args()
     libs = [(s.split("=", 1)[0], load(s.split("=", 1)[1])) for s in args.libs]
     dev = torch.device("cuda", 0)
@@ -51,7 +52,7 @@ def main():
     pool_pages = (B * pages_per + 15) // 16 * 16
     g = torch.Generator(device=dev).manual_seed(5)
     kv = (torch.randn(pool_pages * 2 * KV * 64 * 128, device=dev, generator=g)).to(torch.bfloat16)
-    q = (torch.randn(B * T, H, 128, device=dev, generator=g) * 1.2).to(torch.bfloat16)
+    q = (torch.randn(B * T, H, 128, device=dev, generator=g) * args.qscale).to(torch.bfloat16)
     out = torch.empty(B * T, H * 128, dtype=torch.bfloat16, device=dev)
     st = _lib.stream_ptr()
     flops = B * 4.0 * H * 128 * T * (T + 1) / 2
