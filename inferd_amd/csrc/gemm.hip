@@ -26,7 +26,14 @@
 #include "common.h"
 #include "kernels.h"
 
-__device__ __forceinline__ float silu_f(float g) { return g / (1.0f + expf(-g)); }
+// SiLU of the bf16 gate value g in fp32 (torch: x / (1 + exp(-x)) in float opmath, then bf16):
+// v_exp_f32 on -g * log2 e and v_rcp_f32 instead of the libm expf and an IEEE division (~18
+// VALU -> 4 per element in the prefill gate/up epilogue, which runs exposed between tiles).  Both
+// are within ~1 ulp of fp32, far below the bf16 rounding that follows (a different bf16 result
+// only when the fp32 value sits within ~1.5 fp32 ulp of a bf16 rounding boundary).
+__device__ __forceinline__ float silu_f(float g) {
+  return g * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-g * 1.44269504088896341f));
+}
 
 // sum over the 16 lanes of a DPP row (lanes 16k .. 16k+15), in every lane: rotations by 8, 4,
 // 2, 1 (row_ror DPP moves, no LDS); a fixed tree, so the result is deterministic
