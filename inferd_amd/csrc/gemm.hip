@@ -507,18 +507,34 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
 }
 
 // ring shape per (row tiles, streams): tuned on the Qwen3-8B decode shapes (tools/gemv_lab.hip)
+// Round 4 re-sweep of the one-stream, one-row-tile shape (tools/decode_lib_ab.sh, eager event
+// means, one box): D = 4 takes the o GEMV (K = 4096, four batches per wave) from 11.4 to 10.9 us,
+// but the lm_head GEMV from 214 to 239 us and down from 22.1 to 22.3; D = 5, TW = 2 / D = 4 and
+// TW = 8 / D = 2 were slower in the step.  So D = 4 only for short-K residual GEMVs (DecodeShortK).
 template <int MT, int S>
 struct DecodeCfg {
   static constexpr int NW = S == 1 ? 8 : 4;
   static constexpr int TW = (MT <= 2) ? 4 : 2;
   static constexpr int D = (S == 1 && MT == 1) ? 3 : 2;
 };
+constexpr int DECODE_SHORT_KT = 128;  // K <= 4096: the whole K range is <= 4 batches per wave
 
 template <int MT, int EPI, int NORM>
 static void decode_launch(const DecodeArgs& a, hipStream_t s) {
   constexpr int S = (EPI == EPI_SILU) ? 2 : 1;
   using C = DecodeCfg<MT, S>;
   constexpr int T = decode_threads<C::NW, NORM>();
+  if constexpr (S == 1 && MT == 1 && EPI == EPI_RESID) {  // short K: one more batch in flight
+    if (a.KT <= DECODE_SHORT_KT && a.KT % C::TW == 0) {
+      if (a.pack & GEMM_PACK_A)
+        hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, 4, EPI, NORM, true>), dim3(a.n_tiles), dim3(T),
+                           (dn_lds_bytes<NORM, S, C::NW, C::TW, MT>(a.KT)), s, a);
+      else
+        hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, 4, EPI, NORM>), dim3(a.n_tiles), dim3(T),
+                           (dn_lds_bytes<NORM, S, C::NW, C::TW, MT>(a.KT)), s, a);
+      return;
+    }
+  }
   if (a.pack & GEMM_PACK_A) {
     if (a.KT % C::TW == 0)
       hipLaunchKernelGGL((gemm_decode_kernel<MT, S, C::NW, C::TW, C::D, EPI, NORM, true>), dim3(a.n_tiles), dim3(T),
