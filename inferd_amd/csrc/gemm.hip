@@ -511,6 +511,8 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
 // means, one box): D = 4 takes the o GEMV (K = 4096, four batches per wave) from 11.4 to 10.9 us,
 // but the lm_head GEMV from 214 to 239 us and down from 22.1 to 22.3; D = 5, TW = 2 / D = 4 and
 // TW = 8 / D = 2 were slower in the step.  So D = 4 only for short-K residual GEMVs (DecodeShortK).
+// Also slower: the q/k/v partial GEMV at D = 4 (14.9 -> 16.6 us) and the gate/up GEMV at D = 3
+// (35.3 -> 37.2 us); the q/k/v one at D = 2 changed nothing.
 template <int MT, int S>
 struct DecodeCfg {
   static constexpr int NW = S == 1 ? 8 : 4;
