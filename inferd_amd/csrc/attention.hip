@@ -809,6 +809,24 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   bf16x8 qf[NB][4];
   int lim[NB], tokrow[NB];
   bool valid[NB];
+  // page 0's K/V go in flight first: the q loads and their prescale below then overlap its
+  // latency instead of preceding it (one round trip per workgroup instead of two)
+  typedef const __attribute__((address_space(4))) int* cptr;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  const cptr bt = (cptr)(b.block_table + (int64_t)bseq * b.max_pages);
+  const int swave = __builtin_amdgcn_readfirstlane(wave);
+  auto stage = [&](int buf, int pi) {
+    const __amdgpu_buffer_rsrc_t pg_rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(kv + kv_block(bt[pi], 0, g, KV)), 0, 2 * KV_BLOCK_ELEMS * 2, 0x00020000);
+    char* base = lds + buf * 32768;
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc) {
+      const int piece = swave * 8 + pc;  // 0..15 K tiles, 16..31 V tiles
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(pg_rsrc, (lds_ptr)(base + piece * 1024), 16, lane * 16, piece * 1024, 0,
+                                               0);
+    }
+  };
+  stage(0, 0);
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int row = qb0 + wave * RW + nb * 16 + (lane & 15);
@@ -837,28 +855,12 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wave_min_lim = min(wave_min_lim, __shfl_xor(wave_min_lim, o));
   const int n_pages = wg_last / KV_PAGE + 1;
-  // K/V staging by buffer_load ... lds: one wave-uniform descriptor per page (its 64-bit base
-  // from a scalar load of the block table, in SGPRs), the piece offsets in SGPRs, lane * 16 the
-  // only VGPR -- the per-piece 64-bit address arithmetic of global_load_lds was ~60 VALU per
-  // page per wave.  A page's K block is followed by its V block (common.h kv_block), so its 32
-  // pieces are one contiguous 32 KiB run: the descriptor covers exactly that run, whatever the
-  // pool size (a single descriptor over the whole pool with 32-bit page offsets wrapped past
-  // page ~8192 at 8 kv heads).
-  typedef const __attribute__((address_space(4))) int* cptr;
-  typedef __attribute__((address_space(3))) void* lds_ptr;
-  const cptr bt = (cptr)(b.block_table + (int64_t)bseq * b.max_pages);
-  const int swave = __builtin_amdgcn_readfirstlane(wave);
-  auto stage = [&](int buf, int pi) {
-    const __amdgpu_buffer_rsrc_t pg_rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(kv + kv_block(bt[pi], 0, g, KV)), 0, 2 * KV_BLOCK_ELEMS * 2, 0x00020000);
-    char* base = lds + buf * 32768;
-#pragma unroll
-    for (int pc = 0; pc < 8; ++pc) {
-      const int piece = swave * 8 + pc;  // 0..15 K tiles, 16..31 V tiles
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(pg_rsrc, (lds_ptr)(base + piece * 1024), 16, lane * 16, piece * 1024, 0,
-                                               0);
-    }
-  };
+  // (K/V staging, `stage` above: buffer_load ... lds with one wave-uniform descriptor per page --
+  // its 64-bit base from a scalar load of the block table, in SGPRs -- the piece offsets in
+  // SGPRs, lane * 16 the only VGPR; the per-piece 64-bit address arithmetic of global_load_lds
+  // was ~60 VALU per page per wave.  A page's K block is followed by its V block (common.h
+  // kv_block), so its 32 pieces are one contiguous 32 KiB run: the descriptor covers exactly
+  // that run, whatever the pool size.)
   float m_i[NB];
   PfState ps_[NB];
   f32x4 o[NB][8];
@@ -872,7 +874,6 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int db = 0; db < 8; ++db) o[nb][db] = f32x4{0.f, 0.f, 0.f, 0.f};
-  stage(0, 0);
   __syncthreads();
   // page 0 (token 0: every row's first visible key) sets the rows' reference max
   if (n_pages > 1) stage(1, 1);
