@@ -113,12 +113,19 @@ def parse():
     p.add_argument("--profile-steps", type=int, default=8, help="eager event-instrumented decode steps")
     p.add_argument("--prefill-chunk", type=int, default=2, help="sequences per prefill call")
     p.add_argument("--spans", default="", help="comma-separated layers per stage (BASELINE config 4: an uneven, "
-                                                "balance.py-like split, e.g. 5,27,4); overrides --split")
-    p.add_argument("--split", choices=("balanced", "even"), default="even",
+                                                "balance.py-like split, e.g. 5,27,4; multiples of 0.5 cut between a "
+                                                "layer's attention and MLP halves, e.g. 4.5,4.5,5,...); overrides "
+                                                "--split")
+    p.add_argument("--split", choices=("balanced", "even", "halves"), default="even",
                    help="stage layer counts: even = counts differing by at most one (BASELINE config 3, the "
-                        "default), balanced = min-max of per-stage decode bytes (lm_head priced on the last stage)")
-    p.add_argument("--mode", choices=("decode", "prefill"), default="decode",
-                   help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline)")
+                        "default), balanced = min-max of per-stage decode bytes (lm_head priced on the last stage), "
+                        "halves = min-max of per-stage decode time with cuts between a layer's attention and MLP "
+                        "halves allowed (pipeline.halves_split)")
+    p.add_argument("--mode", choices=("decode", "prefill", "stages"), default="decode",
+                   help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline); "
+                        "stages: the per-stage decode projection of the 2/4/8-GPU splits on one GPU")
+    p.add_argument("--no-stage-projection", action="store_true",
+                   help="N=1 decode runs: skip the per-stage projection of the 2/4/8-GPU splits")
     p.add_argument("--prefill-layers", type=int, default=8)
     p.add_argument("--prefill-batch", type=int, default=1)
     p.add_argument("--prefill-len", type=int, default=8192)
@@ -136,6 +143,19 @@ def prefill_flops(d, n_layers: int, B: int, T: int) -> float:
 def run_prefill(args):
     """`--mode prefill`: the config-5 line alone."""
     print(json.dumps(prefill_line(args, args.steps, args.warmup, torch.device("cuda", 0))), flush=True)
+
+
+def run_stages(args):
+    """`--mode stages`: the per-stage decode projection alone."""
+    from inferd_amd.runtime import MODELS
+    dev = torch.device("cuda", 0)
+    d = MODELS[args.model]
+    splits = projection_splits(d, args.batch, args.ctx)
+    if args.spans:
+        from inferd_amd.pipeline import ranges_from_sizes
+        splits = {"spans": ranges_from_sizes(args.spans.split(","))}
+    print(json.dumps({"stage_projection": stage_projection(d, splits, args.batch, args.ctx, dev, args.seed,
+                                                           reps=args.steps)}), flush=True)
 
 
 def prefill_line(args, steps: int, warmup: int, dev, peaks: bool = True) -> dict:
@@ -225,6 +245,98 @@ def step_bytes(d, n_layers: int, B: int, ctx_mean: float, lm_head: bool) -> floa
     return n_layers * per_layer + (kb["lm_head_argmax"] if lm_head else 0)
 
 
+def range_bytes(d, r, B: int, ctx_mean: float, lm_head: bool) -> float:
+    """Algorithmic decode bytes of a StageRange: per attention half its input norm, q/k/v,
+    QK-norm/RoPE/cache write, attention and o; per MLP half its norm, gate/up and down."""
+    kb = kernel_bytes(d, B, ctx_mean)
+    attn = kb["rmsnorm"] + kb["qkv_gemm"] + kb["qk_norm_rope_kv"] + kb["attention"] + kb["o_gemm"]
+    mlp = kb["rmsnorm"] + kb["gateup_gemm"] + kb["down_gemm"]
+    n_attn = sum(1 for u in range(r.first_unit, r.first_unit + r.n_units) if u % 2 == 0)
+    return n_attn * attn + (r.n_units - n_attn) * mlp + (kb["lm_head_argmax"] if lm_head else 0)
+
+
+def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: int = 3, reps: int = 20) -> dict:
+    """Every stage of every split measured alone on this GPU with its real role (embedding on
+    stage 0, final norm + lm_head + argmax on the last): the span is built, B sequences are
+    prefilled with ctx tokens through the real prefill path (stage 0 from random ids, later
+    stages from random hidden states), one microbatch's decode step is captured as the stage's
+    decode graph, and `reps` replays are timed with HIP events on the launch stream outside the
+    graph (after `warmup` replays).  The lockstep pipeline (pipeline.py) ticks at its slowest
+    stage, so per split: tick = max stage ms, each stage's fraction of the HBM roofline at that
+    tick = its algorithmic bytes / (tick x 8 TB/s), bubble = 1 - sum / (S x
+    tick), and the compute-only projected rate S x B / tick (the xGMI hand-off excluded)."""
+    from inferd_amd.runtime import DecodeGraph, SpanRuntime
+    out = {}
+    g = torch.Generator(device="cpu").manual_seed(seed + 5)
+    chunk = 2
+    for name, ranges in splits.items():
+        S = len(ranges)
+        stages = []
+        for s, r in enumerate(ranges):
+            first, last = s == 0, s == S - 1
+            span = SpanRuntime(d, r.first_layer, r.n_layers, has_embed=first, has_lm_head=last,
+                               kv_pages=B * ((ctx + warmup + reps) // 64 + 2) + 4, max_tokens=chunk * ctx,
+                               max_seqs=B, max_positions=ctx + warmup + reps + 64, device=dev,
+                               skip_first_attn=r.skip_first_attn, skip_last_mlp=r.skip_last_mlp)
+            span.init_synthetic(seed)
+            sess = [("proj", b) for b in range(B)]
+            for c in range(0, B, chunk):
+                reqs = [(sid, ctx) for sid in sess[c:c + chunk]]
+                if first:
+                    ids = torch.randint(0, d.vocab, (len(reqs) * ctx,), generator=g, dtype=torch.int32)
+                    span.forward(reqs, ids=ids, want_hidden=False, want_next_ids=last)
+                else:
+                    x = (torch.randn(len(reqs) * ctx, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
+                    span.forward(reqs, x=x, want_hidden=False, want_next_ids=last)
+            ids = torch.zeros(B, dtype=torch.int32, device=dev) if first else None
+            x = None if first else (torch.randn(B, d.hidden, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+            hout = None if last else torch.empty(B, d.hidden, dtype=torch.bfloat16, device=dev)
+            nid = torch.empty(B, dtype=torch.int32, device=dev) if last else None
+            graph = DecodeGraph(span, sess, warmup + reps, ids=ids, x=x, hidden_out=hout, next_ids=nid)
+            for _ in range(warmup):
+                graph.launch()
+            stream = torch.cuda.current_stream(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                graph.launch()
+            e1.record(stream)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            span.check_errors()
+            nb = range_bytes(d, r, B, ctx + warmup + (reps + 1) / 2.0, last)
+            stages.append({"range": r.label(), "units": r.n_units, "ms": round(ms, 4), "alg_bytes": int(nb),
+                           "frac_own": round(nb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            del graph, span
+            torch.cuda.synchronize(dev)
+        tick = max(st["ms"] for st in stages)
+        for st in stages:
+            st["frac_at_tick"] = round(st["alg_bytes"] / (tick * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        out[name] = {"stages": stages, "tick_ms": tick,
+                     "min_frac_at_tick": min(st["frac_at_tick"] for st in stages),
+                     "bubble_frac": round(1 - sum(st["ms"] for st in stages) / (S * tick), 4),
+                     "projected_tokens_per_s": round(S * B / (tick * 1e-3), 1)}
+    return out
+
+
+def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
+    """The splits stage_projection measures: BASELINE config 3's even splits, the layer-granular
+    byte-balanced split and the half-layer time-balanced split at each stage count."""
+    from inferd_amd.pipeline import StageRange, halves_split
+    out = {}
+    for n in sizes:
+        if n > d.layers:
+            continue
+        out[f"even{n}"] = [StageRange.layers(f, k) for f, k in stage_split(d, n, B, ctx, "even")]
+        bal = [StageRange.layers(f, k) for f, k in stage_split(d, n, B, ctx, "balanced")]
+        if bal != out[f"even{n}"]:
+            out[f"balanced{n}"] = bal
+        hv = halves_split(d.layers, n)
+        if all(hv != v for v in out.values()):
+            out[f"halves{n}"] = hv
+    return out
+
+
 # ------------------------------------------------------------------ CPU baseline
 def _cpu_model() -> str:
     try:
@@ -280,6 +392,7 @@ def cpu_baseline(d_name: str, B: int, ctx: int, seed: int, n_layers_sample: int)
             c.k, c.v = k, v
             caches.append(c)
         sp.sessions["bench"] = caches
+        sp.lengths["bench"] = ctx
         sp.forward_cached("bench", x)
     t_layers = _median_time(step) / n_layers_sample
     gw = R.gen_global_weights(d, seed)
@@ -326,6 +439,8 @@ def main():
     args = parse()
     if args.mode == "prefill":
         return run_prefill(args)
+    if args.mode == "stages":
+        return run_stages(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -365,20 +480,23 @@ def main():
     d = MODELS[args.model]
     B, ctx, K, W = args.batch, args.ctx, args.steps, args.warmup
     if args.spans:
-        sizes = [int(v) for v in args.spans.split(",")]
-        assert len(sizes) == world and sum(sizes) == d.layers, f"--spans {args.spans}: need {world} stages, {d.layers} layers"
-        spans = [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
+        ranges = P.ranges_from_sizes(args.spans.split(","))
+        assert len(ranges) == world and sum(r.n_units for r in ranges) == 2 * d.layers, \
+            f"--spans {args.spans}: need {world} stages, {d.layers} layers"
+    elif args.split == "halves":
+        ranges = P.halves_split(d.layers, world)
     else:
-        spans = stage_split(d, world, B, ctx, args.split)
-    first, n_layers = spans[rank]
+        ranges = [P.StageRange.layers(f, k) for f, k in stage_split(d, world, B, ctx, args.split)]
+    rg = ranges[rank]
     if world > 1:
-        print(f"bench.py: rank {rank} on cuda:{dev_index}: layers {first}..{first + n_layers - 1} of {d.layers}"
+        print(f"bench.py: rank {rank} on cuda:{dev_index}: layers {rg.label()} of {d.layers}"
               f"{' + embed' if rank == 0 else ''}{' + norm/lm_head' if rank == world - 1 else ''}",
               file=sys.stderr, flush=True)
     n_mb = world                                   # microbatches in flight
-    st = P.PipelineStage(d, rank, world, first, n_layers, device=dev, seed=args.seed,
+    st = P.PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=args.seed,
                          n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + args.profile_steps + 64,
-                         prefill_chunk=args.prefill_chunk)
+                         prefill_chunk=args.prefill_chunk, skip_first_attn=rg.skip_first_attn,
+                         skip_last_mlp=rg.skip_last_mlp)
     # ---- prefill (untimed): every microbatch's sequences get `ctx` real tokens
     g = torch.Generator().manual_seed(args.seed + 17)
     prompts = [torch.randint(0, d.vocab, (B, ctx), generator=g) for _ in range(n_mb)]
@@ -463,7 +581,7 @@ def main():
             "config": {"workload": f"{args.model} greedy decode, batch {B} per microbatch at {ctx} context "
                                    f"(prefilled), {n_mb} microbatch(es) in flight",
                        "global_batch": B * n_mb, "seq_len": ctx, "parallelism": f"pp{world}",
-                       "spans": [n for _, n in spans]},
+                       "spans": [r.n_units / 2 for r in ranges], "stage_ranges": [r.label() for r in ranges]},
             "roofline": roof,
             "roofline_step": {"bound": "hbm", "alg_bytes_per_step": int(sb),
                               "achieved": round(sb / (ms_per_step * 1e-3) / 1e9 / world, 1),
@@ -471,7 +589,7 @@ def main():
                               "frac": round(sb / (ms_per_step * 1e-3) / 1e9 / world / HBM_PEAK_GBS, 4)},
             "kernels": kernels,
             "stages": None if not prof else {
-                "spans": [n for _, n in spans],
+                "spans": [r.label() for r in ranges],
                 "compute_ms_per_microbatch": [round(v, 4) for v in stage_ms],
                 "tick_ms": round(ms_per_step / n_mb, 4),
                 "bubble_frac": round(1 - sum(stage_ms) / (world * max(stage_ms)), 4) if max(stage_ms) > 0 else None,
@@ -500,6 +618,10 @@ def main():
             pf = prefill_line(args, 4, 1, dev, peaks=False)
             args.prefill_batch = 1
             out["prefill_config5_b4"] = {k: pf[k] for k in keep}
+        if world == 1 and not args.no_stage_projection:
+            # the 2/4/8-GPU splits, every stage's decode graph timed alone on this GPU
+            st.release()
+            out["stage_projection"] = stage_projection(d, projection_splits(d, B, ctx), B, ctx, dev, args.seed)
         if world == 1 and not args.no_cpu_baseline:
             st.release()
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)

@@ -63,6 +63,14 @@ typedef struct InferdSpanConfig {
   int32_t kv_pages;       /* KV pool capacity, in INFERD_KV_PAGE_TOKENS-token pages */
   int32_t max_tokens;     /* activation workspace rows (tokens per forward call) */
   int32_t max_seqs;       /* sequences per forward call */
+  /* Sub-layer stage boundaries (ABI 3).  The reference cuts spans at layer boundaries only
+   * (split_model.py:92-108); a pipeline balanced to the last stage's lm_head needs a finer
+   * cut.  A decoder layer (qwen3_server_module.py:179-206) is two halves: attention
+   * (input_layernorm .. o_proj + residual) and MLP (post_attention_layernorm .. down_proj +
+   * residual).  The hidden state handed over between the halves is the residual stream h1,
+   * the same bf16 [n_tokens][hidden] tensor a layer boundary hands over. */
+  int32_t skip_first_attn; /* the span begins at its first layer's MLP half (input: h1; no embed) */
+  int32_t skip_last_mlp;   /* the span ends after its last layer's attention half (output: h1; no lm_head) */
 } InferdSpanConfig;
 
 /* One forward call's batch: n_seqs sequences, their new tokens concatenated
@@ -222,7 +230,8 @@ int inferd_kv_build_decode_batch(InferdKvTable* table, const uint64_t* seqs, int
 /* Device base pointer of one layer's KV pool: bf16
  * [pages / 16][kv_heads][pages % 16][K|V][64*128] (super-pages of 16 pages; a pool spans
  * whole super-pages, so callers of the single-op entry points below round their pool up to a
- * multiple of 16 pages). */
+ * multiple of 16 pages).  `layer` is span-local; a layer the span runs only the MLP half of
+ * (skip_first_attn) has no KV here (INFERD_ERR_ARG). */
 int inferd_span_kv_layer(InferdSpan* span, int32_t layer, void** out);
 /* Zero the KV pool. */
 int inferd_span_kv_clear(InferdSpan* span, void* stream);

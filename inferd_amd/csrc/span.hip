@@ -49,7 +49,7 @@ int inferd_fail(int code, const std::string& msg) { return fail(code, msg); }
   } while (0)
 
 extern "C" const char* inferd_last_error(void) { return g_err.c_str(); }
-extern "C" int inferd_abi_version(void) { return 2; }
+extern "C" int inferd_abi_version(void) { return 3; }
 
 namespace {
 
@@ -148,6 +148,12 @@ struct InferdSpan {
     return INFERD_OK;
   }
   int qkv_rows() const { return (cfg.heads + 2 * cfg.kv_heads) * HEAD_DIM; }
+  // the halves of span-local layer l this span runs (InferdSpanConfig skip_first_attn /
+  // skip_last_mlp); only layers with an attention half own a KV pool layer
+  bool has_attn(int l) const { return !(l == 0 && cfg.skip_first_attn); }
+  bool has_mlp(int l) const { return !(l == cfg.n_layers - 1 && cfg.skip_last_mlp); }
+  int kv_layers() const { return cfg.n_layers - (cfg.skip_first_attn ? 1 : 0); }
+  u16* kv_of(int l) const { return kv_pool + kv_layer_elems * (l - (cfg.skip_first_attn ? 1 : 0)); }
 };
 
 #define ALLOC(ptr, bytes)                                   \
@@ -170,6 +176,15 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   if (c.has_lm_head && c.max_seqs > 64)
     return fail(INFERD_ERR_ARG, "a span with lm_head takes max_seqs <= 64 (the greedy argmax is per call of <= 64 rows)");
   if (c.kv_pages > (1 << 24)) return fail(INFERD_ERR_ARG, "kv_pages must be <= 2^24");
+  if ((c.skip_first_attn | c.skip_last_mlp) & ~1) return fail(INFERD_ERR_ARG, "skip_first_attn / skip_last_mlp are 0 or 1");
+  if (c.skip_first_attn && c.has_embed)
+    return fail(INFERD_ERR_ARG, "a span with the embedding starts at a layer's attention half (skip_first_attn = 0)");
+  if (c.skip_last_mlp && c.has_lm_head)
+    return fail(INFERD_ERR_ARG, "a span with lm_head ends at a layer's MLP half (skip_last_mlp = 0)");
+  if ((c.skip_first_attn || c.skip_last_mlp) && c.n_layers < 1)
+    return fail(INFERD_ERR_ARG, "a half-layer boundary needs n_layers >= 1");
+  if (c.skip_first_attn && c.skip_last_mlp && c.n_layers == 1)
+    return fail(INFERD_ERR_ARG, "a one-layer span cannot skip both of its halves");
   InferdSpan* s = new InferdSpan();
   s->cfg = c;
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
@@ -184,15 +199,20 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
     rc = s->alloc((void**)&(ptr), (size_t)(bytes));         \
     if (rc) return bail(rc);                                \
   } while (0)
-  for (auto& L : s->layers) {
-    SALLOC(L.qkv, (size_t)s->qkv_rows() * h * 2);
-    SALLOC(L.o, (size_t)h * H * HEAD_DIM * 2);
-    SALLOC(L.gateup, (size_t)2 * I * h * 2);
-    SALLOC(L.down, (size_t)h * I * 2);
-    SALLOC(L.in_ln, (size_t)h * 2);
-    SALLOC(L.post_ln, (size_t)h * 2);
-    SALLOC(L.q_norm, HEAD_DIM * 2);
-    SALLOC(L.k_norm, HEAD_DIM * 2);
+  for (int l = 0; l < c.n_layers; ++l) {
+    LayerW& L = s->layers[l];
+    if (s->has_attn(l)) {
+      SALLOC(L.qkv, (size_t)s->qkv_rows() * h * 2);
+      SALLOC(L.o, (size_t)h * H * HEAD_DIM * 2);
+      SALLOC(L.in_ln, (size_t)h * 2);
+      SALLOC(L.q_norm, HEAD_DIM * 2);
+      SALLOC(L.k_norm, HEAD_DIM * 2);
+    }
+    if (s->has_mlp(l)) {
+      SALLOC(L.gateup, (size_t)2 * I * h * 2);
+      SALLOC(L.down, (size_t)h * I * 2);
+      SALLOC(L.post_ln, (size_t)h * 2);
+    }
   }
   if (c.has_embed) SALLOC(s->embed, (size_t)c.vocab * h * 2);
   if (c.has_lm_head) {
@@ -218,9 +238,9 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   // KV pool
   // whole super-pages (common.h: KV_SUPER)
   s->kv_layer_elems = (size_t)((c.kv_pages + KV_SUPER - 1) / KV_SUPER * KV_SUPER) * 2 * KV * KV_BLOCK_ELEMS;
-  if (c.n_layers > 0) {
-    SALLOC(s->kv_pool, s->kv_layer_elems * c.n_layers * 2);
-    if (hipMemset(s->kv_pool, 0, s->kv_layer_elems * c.n_layers * 2) != hipSuccess)
+  if (s->kv_layers() > 0) {
+    SALLOC(s->kv_pool, s->kv_layer_elems * s->kv_layers() * 2);
+    if (hipMemset(s->kv_pool, 0, s->kv_layer_elems * s->kv_layers() * 2) != hipSuccess)
       return bail(fail(INFERD_ERR_HIP, "kv memset failed"));
   }
   // workspace
@@ -279,7 +299,11 @@ int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
     return fail(INFERD_ERR_ARG, std::string("unknown/unowned global weight ") + name);
   }
   if (layer >= c.n_layers) return fail(INFERD_ERR_ARG, "layer index out of span");
-  return resolve_layer(s, layer, name, t);
+  if (resolve_layer(s, layer, name, t)) return INFERD_ERR_ARG;
+  if (!t->dst)
+    return fail(INFERD_ERR_ARG, std::string(name) + ": layer " + std::to_string(layer) +
+                                    " of this span runs only its other half (skip_first_attn / skip_last_mlp)");
+  return 0;
 }
 
 int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t) {
@@ -299,6 +323,13 @@ int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t) {
   if (!strcmp(name, "input_layernorm")) { *t = {L.in_ln, 0, 1, h, T_INLN}; return 0; }
   if (!strcmp(name, "post_attention_layernorm")) { *t = {L.post_ln, 0, 1, h, T_POSTLN}; return 0; }
   return fail(INFERD_ERR_ARG, std::string("unknown layer weight ") + name);
+}
+
+// 1 if span-local layer `layer` runs the half that weight `name` belongs to
+bool owns_weight(const InferdSpan* s, int layer, const char* name) {
+  const bool mlp = !strcmp(name, "gate_proj") || !strcmp(name, "up_proj") || !strcmp(name, "down_proj") ||
+                   !strcmp(name, "post_attention_layernorm");
+  return mlp ? s->has_mlp(layer) : s->has_attn(layer);
 }
 // packed sub-blocks start at an n-tile boundary: offset rows*K elements == (rows/16)*KT*512
 }  // namespace
@@ -352,7 +383,7 @@ extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* st
   int rc = 0;
   for (int l = 0; l < c.n_layers && !rc; ++l)
     for (const char* nm : layer_names)
-      if ((rc = gen(l, nm))) break;
+      if (owns_weight(s, l, nm) && (rc = gen(l, nm))) break;
   if (!rc && c.has_embed) rc = gen(-1, "embed_tokens");
   if (!rc && c.has_lm_head) rc = gen(-1, "norm");
   if (!rc && c.has_lm_head) rc = gen(-1, "lm_head");
@@ -446,7 +477,38 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   long pe = -1;
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
-    u16* kv_l = s->kv_pool + s->kv_layer_elems * l;
+    // the residual written by this layer's last half: x_out after the span's last layer
+    u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
+    const bool out_packed = pkx && l < c.n_layers - 1;
+    if (!s->has_attn(l)) {
+      // ---- a span starting at this layer's MLP half: x is h1 (row-major, the caller's), so
+      // post_attention_layernorm runs as the span's first RMSNorm launch (slot zeroing and
+      // the graph prologue included, like layer 0's input norm)
+      pe = s->prof_begin(PROF_NORM, st);
+      launch_rmsnorm(x, h, nullptr, 0, W.post_ln, s->xn, h, M, h, c.rms_eps, st, false, gemv ? s->ssq : nullptr,
+                     2 * c.n_layers, &pro);
+      s->prof_end(pe, st);
+      const DecodeNorm dm = {DN_NONE, c.rms_eps, nullptr, nullptr};
+      const int pk =
+          (gemv && !gemm_uses_tiled(M, I, h, EPI_SILU) && !gemm_uses_tiled(M, h, I, EPI_RESID)) ? 1 : 0;
+      pe = s->prof_begin(PROF_GATEUP, st);
+      GEMM_TRY(launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, &s->gws, &dm,
+                           nullptr, pk ? GEMM_PACK_C : 0));
+      s->prof_end(pe, st);
+      pe = s->prof_begin(PROF_DOWN, st);
+      GEMM_TRY(launch_gemm(s->act, I, W.down, M, h, I, out, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
+                           (gemv && l + 1 < c.n_layers) ? slot(2 * l + 1) : nullptr,
+                           (pk ? GEMM_PACK_A : 0) | (out_packed ? GEMM_PACK_C : 0)));
+      s->prof_end(pe, st);
+      x = out;
+      x_packed = out_packed;
+      if (layer_out)
+        HIP_TRY(hipMemcpyAsync((u16*)layer_out + (size_t)l * M * h, x, (size_t)M * h * 2,
+                               hipMemcpyDeviceToDevice, st));
+      LAUNCH_CHECK();
+      continue;
+    }
+    u16* kv_l = s->kv_of(l);
     // decode: QK-norm + RoPE + the cache write run inside the attention
     const bool fused = b->decode;
     // decode q/k/v K-slices (reduced inside the fused attention): M <= 16 and K/32 divisible
@@ -510,14 +572,29 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // to s->xn (free after the q/k/v projection) where s->h holds a row-major x (the first
     // span's embedding output) or is to receive this layer's row-major output (the last layer
     // without x_out).
-    u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
-    const bool out_packed = pkx && l < c.n_layers - 1;
     u16* h1 = (pkx && ((x == s->h && !x_packed) || (out == s->h && !out_packed))) ? s->xn : s->h;
+    bool h1_packed = pkx;
+    if (!s->has_mlp(l)) {
+      // a span ending at this layer's attention half: h1 is the span's (row-major) output;
+      // without x_out it goes to s->xn (free after the q/k/v projection), never in place over
+      // a packed x
+      h1 = x_out ? (u16*)x_out : s->xn;
+      h1_packed = false;
+    }
     pe = s->prof_begin(PROF_O, st);
     GEMM_TRY(launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
                 gemv ? slot(2 * l) : nullptr,
-                (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (pkx ? GEMM_PACK_C : 0)));
+                (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (h1_packed ? GEMM_PACK_C : 0)));
     s->prof_end(pe, st);
+    if (!s->has_mlp(l)) {
+      x = h1;
+      x_packed = false;
+      if (layer_out)
+        HIP_TRY(hipMemcpyAsync((u16*)layer_out + (size_t)l * M * h, x, (size_t)M * h * 2,
+                               hipMemcpyDeviceToDevice, st));
+      LAUNCH_CHECK();
+      continue;
+    }
     // ---- post_attention_layernorm -> gate/up (+SwiGLU)
     const u16* m_in = h1;
     DecodeNorm dm = {DN_NONE, c.rms_eps, nullptr, nullptr};
@@ -688,14 +765,15 @@ extern "C" int inferd_span_profile_stop(InferdSpan* s, double* total_ms, int32_t
 extern "C" int inferd_span_kv_layer(InferdSpan* s, int32_t layer, void** out) {
   if (!s || !out) return fail(INFERD_ERR_ARG, "null argument");
   if (layer < 0 || layer >= s->cfg.n_layers) return fail(INFERD_ERR_ARG, "layer out of range");
-  *out = s->kv_pool + s->kv_layer_elems * layer;
+  if (!s->has_attn(layer)) return fail(INFERD_ERR_ARG, "layer runs only its MLP half here (no KV)");
+  *out = s->kv_of(layer);
   return INFERD_OK;
 }
 
 extern "C" int inferd_span_kv_clear(InferdSpan* s, void* stream) {
   if (!s) return fail(INFERD_ERR_ARG, "null span");
   if (s->kv_pool)
-    HIP_TRY(hipMemsetAsync(s->kv_pool, 0, s->kv_layer_elems * s->cfg.n_layers * 2, (hipStream_t)stream));
+    HIP_TRY(hipMemsetAsync(s->kv_pool, 0, s->kv_layer_elems * s->kv_layers() * 2, (hipStream_t)stream));
   return INFERD_OK;
 }
 

@@ -87,15 +87,17 @@ void check_forward_args(const InferdSpanConfig& c, const at::Tensor& words, cons
 
 // ---- span lifetime ------------------------------------------------------------------------
 // cfg: [hidden, intermediate, heads, kv_heads, head_dim, vocab, first_layer, n_layers, has_embed,
-//       has_lm_head, max_positions, kv_pages, max_tokens, max_seqs]
+//       has_lm_head, max_positions, kv_pages, max_tokens, max_seqs, skip_first_attn, skip_last_mlp]
+// (the two sub-layer boundary flags may be omitted: 14 ints = whole layers)
 int64_t span_create(at::IntArrayRef cfg, double rms_eps, double rope_theta, at::Device device) {
-  TORCH_CHECK(cfg.size() == 14, "span_create: 14 config ints");
+  TORCH_CHECK(cfg.size() == 14 || cfg.size() == 16, "span_create: 14 or 16 config ints");
   TORCH_CHECK(device.is_cuda(), "span_create: a GPU device");
   c10::hip::HIPGuard g(device.index());
   InferdSpanConfig c{(int32_t)cfg[0], (int32_t)cfg[1], (int32_t)cfg[2], (int32_t)cfg[3], (int32_t)cfg[4],
                      (int32_t)cfg[5], (int32_t)cfg[6], (int32_t)cfg[7], (int32_t)cfg[8], (int32_t)cfg[9],
                      (float)rms_eps, (float)rope_theta, (int32_t)cfg[10], (int32_t)cfg[11], (int32_t)cfg[12],
-                     (int32_t)cfg[13]};
+                     (int32_t)cfg[13], cfg.size() == 16 ? (int32_t)cfg[14] : 0,
+                     cfg.size() == 16 ? (int32_t)cfg[15] : 0};
   InferdSpan* s = nullptr;
   ok(inferd_span_create(&c, &s), "span_create");
   return reinterpret_cast<int64_t>(s);
@@ -106,7 +108,8 @@ void span_destroy(int64_t span) { inferd_span_destroy(handle<InferdSpan>(span, "
 std::vector<int64_t> span_config(int64_t span) {
   const InferdSpanConfig c = config_of(handle<InferdSpan>(span, "span_config"));
   return {c.hidden, c.intermediate, c.heads, c.kv_heads, c.head_dim, c.vocab, c.first_layer, c.n_layers,
-          c.has_embed, c.has_lm_head, c.max_positions, c.kv_pages, c.max_tokens, c.max_seqs};
+          c.has_embed, c.has_lm_head, c.max_positions, c.kv_pages, c.max_tokens, c.max_seqs,
+          c.skip_first_attn, c.skip_last_mlp};
 }
 
 void span_init_synthetic(int64_t span, int64_t seed, at::Device device) {

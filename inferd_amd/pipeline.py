@@ -76,6 +76,96 @@ def balanced_split(n_layers: int, n: int, layer_cost: float, head_cost: float = 
     return [(sum(sizes[:i]), k) for i, k in enumerate(sizes)]
 
 
+class StageRange:
+    """A stage's slice of the model in half-layer units: unit 2*l is layer l's attention half
+    (input_layernorm .. o_proj + residual), unit 2*l + 1 its MLP half (post_attention_layernorm
+    .. down_proj + residual), qwen3_server_module.py:179-206.  The reference cuts spans at
+    layer boundaries only (split_model.py:92-108); a cut between the halves hands over the
+    residual stream h1, a bf16 [tokens, hidden] tensor like a layer boundary's."""
+    __slots__ = ("first_unit", "n_units")
+
+    def __init__(self, first_unit: int, n_units: int):
+        assert first_unit >= 0 and n_units >= 1
+        self.first_unit, self.n_units = first_unit, n_units
+
+    @classmethod
+    def layers(cls, first_layer: int, n_layers: int) -> "StageRange":
+        return cls(2 * first_layer, 2 * n_layers)
+
+    first_layer = property(lambda self: self.first_unit // 2)
+    last_layer = property(lambda self: (self.first_unit + self.n_units - 1) // 2)
+    n_layers = property(lambda self: self.last_layer - self.first_layer + 1)
+    skip_first_attn = property(lambda self: self.first_unit % 2 == 1)
+    skip_last_mlp = property(lambda self: (self.first_unit + self.n_units) % 2 == 1)
+
+    def label(self) -> str:
+        """e.g. '4m..8' = layer 4's MLP half through layer 8; '9..13a' ends with 13's attention half"""
+        a = f"{self.first_layer}{'m' if self.skip_first_attn else ''}"
+        b = f"{self.last_layer}{'a' if self.skip_last_mlp else ''}"
+        return f"{a}..{b}"
+
+    def __eq__(self, o):
+        return isinstance(o, StageRange) and (o.first_unit, o.n_units) == (self.first_unit, self.n_units)
+
+    def __repr__(self):
+        return f"StageRange({self.first_unit}, {self.n_units})"
+
+
+def ranges_from_sizes(sizes) -> list:
+    """Stage sizes in layers, multiples of one half (e.g. [4.5, 4.5, 5, ...]) -> StageRanges."""
+    units = [int(round(2 * float(s))) for s in sizes]
+    if any(u < 1 or abs(u - 2 * float(s)) > 1e-9 for u, s in zip(units, sizes)):
+        raise ValueError(f"stage sizes must be positive multiples of 0.5 layers: {sizes}")
+    return [StageRange(sum(units[:i]), u) for i, u in enumerate(units)]
+
+
+def balanced_units(unit_costs, n: int, head_cost: float = 0.0, stage_cost: float = 0.0):
+    """[StageRange] cutting the unit sequence (half layers, in order) into n contiguous stages
+    minimising the slowest stage's cost -- each stage costs its units, plus stage_cost (its
+    first RMSNorm launch) plus head_cost on the last stage -- ties to the smallest sum of
+    squares.  Every stage gets at least one unit."""
+    U = len(unit_costs)
+    assert 1 <= n <= U
+    pre = [0.0]
+    for c in unit_costs:
+        pre.append(pre[-1] + c)
+    INF = (float("inf"), float("inf"))
+    best = [[INF] * (U + 1) for _ in range(n + 1)]
+    cut = [[0] * (U + 1) for _ in range(n + 1)]
+    best[0][0] = (0.0, 0.0)
+    for s in range(1, n + 1):
+        for u in range(s, U - (n - s) + 1):
+            for j in range(s - 1, u):
+                mx, sq = best[s - 1][j]
+                if mx == float("inf"):
+                    continue
+                c = pre[u] - pre[j] + stage_cost + (head_cost if s == n else 0.0)
+                cand = (max(mx, c), sq + c * c)
+                if cand < best[s][u]:
+                    best[s][u], cut[s][u] = cand, j
+    out, u = [], U
+    for s in range(n, 0, -1):
+        j = cut[s][u]
+        out.append(StageRange(j, u - j))
+        u = j
+    return out[::-1]
+
+
+# In-graph decode kernel means at Qwen3-8B, B = 16, ctx ~2.1k (rocprofv3 kernel trace of the
+# round-4 decode graph, profiles/r04/decode_kernel_trace.json), us: the attention half
+# (q/k/v GEMV + fused attention + o GEMV), the MLP half (gate/up + down GEMVs), a stage's first
+# RMSNorm launch, and the last stage's final norm + lm_head GEMV + argmax.
+DECODE_US_8B = {"attn_half": 12.70 + 26.88 + 8.73, "mlp_half": 33.57 + 19.99, "stage_norm": 5.19,
+                "head": 5.19 + 201.5 + 4.24}
+
+
+def halves_split(n_layers: int, n: int, costs: dict = DECODE_US_8B):
+    """The half-layer split minimising the slowest stage's decode time (balanced_units over
+    the measured per-half costs)."""
+    units = [costs["attn_half"], costs["mlp_half"]] * n_layers
+    return balanced_units(units, n, costs["head"], costs["stage_norm"])
+
+
 class SpanExecutor:
     """Runs one span's compute for pipeline items on this rank's GPU."""
 
@@ -127,10 +217,12 @@ class PipelineStage:
 
     def __init__(self, dims: ModelDims, rank: int, world: int, first_layer: int, n_layers: int, *,
                  device, seed: int, n_microbatches: int, batch: int, max_ctx: int, prefill_chunk: int = 2,
-                 executor=None, group=None, profile: str = "random", want_logits: bool = False):
+                 executor=None, group=None, profile: str = "random", want_logits: bool = False,
+                 skip_first_attn: bool = False, skip_last_mlp: bool = False):
         """profile: the synthetic weight profile (runtime.SpanRuntime.init_synthetic: "peaked"
         for token-exact parity runs).  want_logits (last stage): every decode step's and the
-        prefill's last-row logits are kept, for parity checks against the oracle's."""
+        prefill's last-row logits are kept, for parity checks against the oracle's.
+        skip_first_attn / skip_last_mlp: a half-layer stage boundary (StageRange)."""
         assert n_microbatches == world, "the ring schedule keeps exactly one microbatch per stage in flight"
         self.dims, self.rank, self.world = dims, rank, world
         self.S = world
@@ -143,7 +235,8 @@ class PipelineStage:
             span = SpanRuntime(dims, first_layer, n_layers, has_embed=(rank == 0), has_lm_head=(rank == world - 1),
                                kv_pages=n_microbatches * batch * pages_per_seq + 4,
                                max_tokens=max(prefill_chunk * max_ctx, batch), max_seqs=max(batch, prefill_chunk),
-                               max_positions=max_ctx, device=self.device)
+                               max_positions=max_ctx, device=self.device, skip_first_attn=skip_first_attn,
+                               skip_last_mlp=skip_last_mlp)
             span.init_synthetic(seed, profile)
             executor = SpanExecutor(span)
         self.ex = executor

@@ -178,7 +178,9 @@ class DecodeGraph:
     def __init__(self, span: "SpanRuntime", sessions, n_steps: int, ids=None, x=None, hidden_out=None,
                  next_ids=None, logits=None):
         self.span, self.n_steps = span, n_steps
-        self.states = [span._seq(sid) for sid in sessions]
+        # reserve(sid, 0) enters a never-prefilled session into the native table (empty), so a
+        # graph may also start a session from position 0
+        self.states = [span.reserve(sid, 0) for sid in sessions]
         with torch.cuda.device(span.device):
             self.graph = torch.classes.inferd.DecodeGraph(span.handle, span.kv.handle, [st.seq for st in self.states],
                                                           n_steps, ids, x, hidden_out, next_ids, logits, span.device)
@@ -200,17 +202,23 @@ class SpanRuntime:
 
     def __init__(self, dims: ModelDims, first_layer: int, n_layers: int, *, has_embed: bool,
                  has_lm_head: bool, kv_pages: int = 256, max_tokens: int = 4096, max_seqs: int = 64,
-                 max_positions: int | None = None, device: str | torch.device = "cuda"):
+                 max_positions: int | None = None, device: str | torch.device = "cuda",
+                 skip_first_attn: bool = False, skip_last_mlp: bool = False):
+        """skip_first_attn / skip_last_mlp: sub-layer stage boundaries (InferdSpanConfig): the
+        span starts at its first layer's MLP half (x = that layer's post-attention residual)
+        and/or ends after its last layer's attention half (hidden out = that residual)."""
         self.dims = dims
         self.first_layer, self.n_layers = first_layer, n_layers
         self.has_embed, self.has_lm_head = has_embed, has_lm_head
+        self.skip_first_attn, self.skip_last_mlp = bool(skip_first_attn), bool(skip_last_mlp)
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.max_tokens, self.max_seqs = max_tokens, max_seqs
         self.max_positions = max_positions or dims.max_positions
         cfg = [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
-               n_layers, int(has_embed), int(has_lm_head), self.max_positions, kv_pages, max_tokens, max_seqs]
+               n_layers, int(has_embed), int(has_lm_head), self.max_positions, kv_pages, max_tokens, max_seqs,
+               int(skip_first_attn), int(skip_last_mlp)]
         self.handle = None
         self.handle = T.span_create(cfg, dims.eps, dims.rope_theta, self.device)
         self.kv = KvTable(kv_pages)

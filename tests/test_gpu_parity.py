@@ -381,6 +381,9 @@ def _free_port():
 
 
 B8, T8, STEPS8 = 16, 2048, 4
+# the 8-stage half-layer split bench.py --split halves runs (pipeline.halves_split: cuts between a
+# layer's attention and MLP halves; stage sizes in layers)
+HALVES8 = [4.5, 4.5, 5, 5, 4.5, 5, 5, 2.5]
 
 
 def _prompts(n_mb):
@@ -398,10 +401,11 @@ def _pipe_worker(rank, world, port, sizes, out_dir):
     d = MODELS["qwen3-8b"]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    spans = [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
-    first, n = spans[rank]
-    st = PipelineStage(d, rank, world, first, n, device=dev, seed=SEED, n_microbatches=world, batch=B8,
-                       max_ctx=T8 + STEPS8 + 8, prefill_chunk=2, want_logits=True)
+    from inferd_amd.pipeline import ranges_from_sizes
+    rg = ranges_from_sizes(sizes)[rank]
+    st = PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=SEED, n_microbatches=world,
+                       batch=B8, max_ctx=T8 + STEPS8 + 8, prefill_chunk=2, want_logits=True,
+                       skip_first_attn=rg.skip_first_attn, skip_last_mlp=rg.skip_last_mlp)
     cap = {} if rank in (0, world - 1) else None
     st.prefill(_prompts(world), capture=cap)
     st.prepare_decode(STEPS8)
@@ -473,9 +477,9 @@ def q8b_prefill_logits_oracle():
 
 @pytest.mark.timeout(1200)
 @pytest.mark.parametrize("sizes", [[18, 18], [9, 9, 9, 9], [5, 5, 5, 5, 4, 4, 4, 4], [5, 27, 4], [6, 12, 12, 6],
-                                   [2, 3, 5, 6, 6, 6, 5, 3]],
+                                   [2, 3, 5, 6, 6, 6, 5, 3], HALVES8],
                          ids=["config3_even2", "config3_even4", "config3_even8", "config4_uneven3", "config4_uneven4",
-                              "config4_uneven8"])
+                              "config4_uneven8", "halves8"])
 def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_logits_oracle):
     """BASELINE configs 3 (Qwen3-8B, the even splits [18,18], [9,9,9,9], [5,5,5,5,4,4,4,4]) and 4
     (SURVEY §8(d)'s uneven splits [5, 27, 4], [6, 12, 12, 6], [2, 3, 5, 6, 6, 6, 5, 3]) at full
@@ -499,11 +503,15 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     assert got == one
     d = R.CONFIGS["qwen3-8b"]
     ids = _prompts(world)[0][:2]
-    ref = R.RefSpan(d, SEED, 0, sizes[0] - 1, True, False, torch.bfloat16, "sdpa").forward(ids)
+    from inferd_amd.pipeline import ranges_from_sizes
+    r0 = ranges_from_sizes(sizes)[0]
+    ref = R.RefSpan(d, SEED, 0, r0.last_layer, True, False, torch.bfloat16, "sdpa",
+                    skip_last_mlp=r0.skip_last_mlp).forward(ids)
     h = pipe["hidden"].reshape(2, T8, -1)
     e = [errs(h[b], ref[b]) for b in range(2)]
     # fp32 oracle on sequence 0: the bf16 noise floor of this boundary, at every depth
-    ref32 = R.RefSpan(d, SEED, 0, sizes[0] - 1, True, False, torch.float32, "sdpa").forward(ids[:1])[0]
+    ref32 = R.RefSpan(d, SEED, 0, r0.last_layer, True, False, torch.float32, "sdpa",
+                      skip_last_mlp=r0.skip_last_mlp).forward(ids[:1])[0]
     noise = {"engine_vs_fp32": errs(h[0], ref32), "bf16_ref_vs_fp32": errs(ref[0], ref32)}
     print(f"noise floor: engine vs fp32 rms {noise['engine_vs_fp32']['rms_rel']:.2e}, "
           f"bf16 reference vs fp32 rms {noise['bf16_ref_vs_fp32']['rms_rel']:.2e}")
@@ -609,10 +617,11 @@ def _pipe_exact_worker(rank, world, port, sizes, out_dir, profile="peaked_deep",
     d = MODELS["qwen3-8b"]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    spans = [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
-    first, n = spans[rank]
-    st = PipelineStage(d, rank, world, first, n, device=dev, seed=SEED, n_microbatches=world, batch=b,
-                       max_ctx=T8X + steps + 8, prefill_chunk=2, profile=profile, want_logits=True)
+    from inferd_amd.pipeline import ranges_from_sizes
+    rg = ranges_from_sizes(sizes)[rank]
+    st = PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=SEED, n_microbatches=world,
+                       batch=b, max_ctx=T8X + steps + 8, prefill_chunk=2, profile=profile, want_logits=True,
+                       skip_first_attn=rg.skip_first_attn, skip_last_mlp=rg.skip_last_mlp)
     force = None
     fp = os.path.join(out_dir, "force.pt")
     if os.path.exists(fp):
@@ -637,8 +646,9 @@ def _pipe_exact_worker(rank, world, port, sizes, out_dir, profile="peaked_deep",
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("sizes", [[18, 18], [9, 9, 9, 9], [5, 5, 5, 5, 4, 4, 4, 4], [4, 5, 5, 5, 5, 5, 5, 2],
-                                   [5, 27, 4]],
-                         ids=["config3_even2", "config3_even4", "config3_even8", "balanced8", "config4_uneven3"])
+                                   [5, 27, 4], HALVES8],
+                         ids=["config3_even2", "config3_even4", "config3_even8", "balanced8", "config4_uneven3",
+                              "halves8"])
 def test_q8b_pipeline_token_exact_vs_oracle(tmp_path, sizes, q8b_oracle_greedy):
     """Qwen3-8B through the span pipeline against the CPU oracle ("peaked_deep" profile, see the
     section comment for what each check proves):

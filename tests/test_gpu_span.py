@@ -218,6 +218,79 @@ def test_decode_graph_hidden_bit_exact(first):
     assert torch.equal(runs[0], runs[1]), (runs[0] - runs[1]).abs().max()
 
 
+def test_half_layer_stage_chain_bit_exact():
+    """Sub-layer stage boundaries (InferdSpanConfig skip_first_attn / skip_last_mlp): Qwen3-0.6B
+    layers 0..3 as three spans cut between a layer's attention and MLP halves -- [0..1a] (embed),
+    [1m..2a], [2m..3] (lm_head) -- give bit-identical logits to one span over the same layers,
+    for a 70-token prefill of 3 sequences and 5 decode-graph steps (teacher-forced, the chain's
+    graphs replayed in stage order on fixed hand-off buffers); the first boundary's hidden state
+    (layer 1's post-attention residual h1) is within the span tolerance of the oracle's."""
+    from inferd_amd.pipeline import StageRange
+    from inferd_amd.runtime import DecodeGraph
+    d = R.CONFIGS["qwen3-0.6b"]
+    B, T, STEPS = 3, 70, 5
+    gen = torch.Generator().manual_seed(31)
+    prompts = torch.randint(0, d.vocab, (B, T), generator=gen)
+    forced = torch.randint(0, d.vocab, (STEPS, B), generator=gen)
+    ranges = [StageRange(0, 3), StageRange(3, 2), StageRange(5, 3)]
+    chain = [span("qwen3-0.6b", r.first_layer, r.n_layers, i == 0, i == 2, kv_pages=16, max_tokens=B * T,
+                  max_seqs=B, max_positions=1024, skip_first_attn=r.skip_first_attn, skip_last_mlp=r.skip_last_mlp)
+             for i, r in enumerate(ranges)]
+    one = span("qwen3-0.6b", 0, 4, True, True, kv_pages=16, max_tokens=B * T, max_seqs=B, max_positions=1024)
+    sess = [f"c{b}" for b in range(B)]
+    reqs = [(sid, T) for sid in sess]
+    h0 = chain[0].forward(reqs, ids=prompts.reshape(-1))["hidden"]
+    h1 = chain[1].forward(reqs, x=h0)["hidden"]
+    lc = chain[2].forward(reqs, x=h1, want_logits=True, want_hidden=False)["logits"]
+    lo = one.forward(reqs, ids=prompts.reshape(-1), want_logits=True, want_hidden=False)["logits"]
+    assert torch.equal(lc, lo), (lc.float() - lo.float()).abs().max()
+    ref = R.RefSpan(d, SEED, 0, 1, True, False, skip_last_mlp=True).forward(prompts)
+    e = rel_err(h0.reshape(B, T, -1), ref)
+    print(f"half-layer boundary (layer 1's h1) vs oracle: rel err {e:.2e}")
+    assert e < TOL_REL
+    ids_c = torch.zeros(B, dtype=torch.int32, device=DEV)
+    ids_o = torch.zeros(B, dtype=torch.int32, device=DEV)
+    hb = [torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+    lg_c = torch.zeros(B, d.vocab, dtype=torch.bfloat16, device=DEV)
+    lg_o = torch.zeros(B, d.vocab, dtype=torch.bfloat16, device=DEV)
+    nid_c = torch.zeros(B, dtype=torch.int32, device=DEV)
+    nid_o = torch.zeros(B, dtype=torch.int32, device=DEV)
+    graphs = [DecodeGraph(chain[0], sess, STEPS, ids=ids_c, hidden_out=hb[0]),
+              DecodeGraph(chain[1], sess, STEPS, x=hb[0], hidden_out=hb[1]),
+              DecodeGraph(chain[2], sess, STEPS, x=hb[1], next_ids=nid_c, logits=lg_c)]
+    g1 = DecodeGraph(one, sess, STEPS, ids=ids_o, next_ids=nid_o, logits=lg_o)
+    for k in range(STEPS):
+        ids_c.copy_(forced[k])
+        ids_o.copy_(forced[k])
+        for g in graphs:
+            g.launch()
+        g1.launch()
+        assert torch.equal(lg_c, lg_o), (k, (lg_c.float() - lg_o.float()).abs().max())
+        assert torch.equal(nid_c, nid_o), k
+    for s in chain + [one]:
+        s.check_errors()
+
+
+def test_half_layer_span_rejects_bad_configs():
+    """A span with the embedding cannot start at a MLP half, one with lm_head cannot end at an
+    attention half, a one-layer span cannot skip both halves, and a layer's absent half has no
+    weights to set."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["tiny"]
+    for kw in ({"has_embed": True, "has_lm_head": False, "skip_first_attn": True},
+               {"has_embed": False, "has_lm_head": True, "skip_last_mlp": True}):
+        with pytest.raises(RuntimeError, match="half"):
+            SpanRuntime(d, 1, 2, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2, **kw)
+    with pytest.raises(RuntimeError, match="both"):
+        SpanRuntime(d, 1, 1, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
+                    skip_first_attn=True, skip_last_mlp=True)
+    s = SpanRuntime(d, 1, 2, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
+                    skip_first_attn=True)
+    with pytest.raises(RuntimeError, match="other half"):
+        s.set_weight(0, "q_proj", torch.zeros(d.heads * 128, d.hidden, dtype=torch.bfloat16))
+    s.set_weight(0, "down_proj", torch.zeros(d.hidden, d.intermediate, dtype=torch.bfloat16))
+
+
 def test_q06_full_model_greedy_cached():
     """Config 2: Qwen3-0.6B single full span (peaked profile), prefill 32 + 12 cached greedy
     decode steps teacher-forced on the oracle's ids: every id identical, every oracle margin

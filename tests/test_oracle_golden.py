@@ -97,3 +97,31 @@ def test_q06_layer_cached():
 
 def test_q8b_layer_cached():
     _check_server("q8b_layer.npz", "qwen3-8b", (("bf16", torch.bfloat16, 0),))
+
+
+def test_half_layer_spans_chain_equals_whole_layers():
+    """The oracle's sub-layer stage boundaries (RefSpan skip_first_attn / skip_last_mlp, the
+    engine's InferdSpanConfig flags) compose to the whole-layer span bit-exactly: the tiny model
+    cut as [0..1a] [1m..2a] [2m..3] against one span, full recompute and cached prefill + 3 decode
+    steps (the hand-off between halves is the bf16 residual h1 both compute); and the whole-layer
+    span is still pinned to the reference-generated golden logits."""
+    d = R.CONFIGS["tiny"]
+    g = load("tiny_petals.npz")
+    prompt = torch.from_numpy(g["prompt"])[None]
+    cuts = [(0, 1, True, False, False, True), (1, 2, False, False, True, True), (2, 3, False, True, True, False)]
+    chain = [R.RefSpan(d, SEED, a, b, f, l, torch.bfloat16, "sdpa", skip_first_attn=sf, skip_last_mlp=sl)
+             for a, b, f, l, sf, sl in cuts]
+    one = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa")
+    x = prompt
+    for sp in chain:
+        x = sp.forward(x)
+    assert torch.equal(x, one.forward(prompt))
+    assert torch.equal(x, tensor(g["bf16_logits"]))
+    ids = prompt
+    for step in range(4):
+        x = ids
+        for sp in chain:
+            x = sp.forward_cached("s", x)
+        y = one.forward_cached("s", ids)
+        assert torch.equal(x, y), step
+        ids = torch.argmax(y[:, -1], -1)[:, None]

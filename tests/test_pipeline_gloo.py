@@ -21,8 +21,9 @@ SEED = 1234
 class OracleExecutor:
     """CPU stand-in for SpanExecutor: same interface, oracle compute (bf16)."""
 
-    def __init__(self, d, first, n_layers, first_span, last_span):
-        self.sp = R.RefSpan(d, SEED, first, first + n_layers - 1, first_span, last_span, torch.bfloat16, "sdpa")
+    def __init__(self, d, r, first_span, last_span):
+        self.sp = R.RefSpan(d, SEED, r.first_layer, r.last_layer, first_span, last_span, torch.bfloat16, "sdpa",
+                            skip_first_attn=r.skip_first_attn, skip_last_mlp=r.skip_last_mlp)
         self.device = torch.device("cpu")
         self.has_embed, self.has_lm_head = first_span, last_span
         self.dims = d
@@ -62,12 +63,13 @@ def _free_port():
 
 
 def _split(d, world, sizes):
-    """layer ranges per stage: even (bench.even_split) or the given sizes (BASELINE config 4's
-    uneven, balance.py-like split; bench.py --spans)"""
-    from bench import even_split
+    """StageRanges per stage: even (bench.even_split) or the given sizes in layers (BASELINE
+    config 4's uneven, balance.py-like split; multiples of 0.5 cut between a layer's attention
+    and MLP halves; bench.py --spans)"""
+    from inferd_amd.pipeline import StageRange, even_split, ranges_from_sizes
     if not sizes:
-        return even_split(d.layers, world)
-    return [(sum(sizes[:i]), n) for i, n in enumerate(sizes)]
+        return [StageRange.layers(f, n) for f, n in even_split(d.layers, world)]
+    return ranges_from_sizes(sizes)
 
 
 def _forced(world, n_steps, vocab):
@@ -83,11 +85,12 @@ def _worker(rank, world, port, n_steps, q, sizes=None, force=False):
     torch.set_num_threads(1)
     from inferd_amd.pipeline import PipelineStage
     d = R.CONFIGS["tiny"]
-    first, n = _split(d, world, sizes)[rank]
-    ex = OracleExecutor(d, first, n, rank == 0, rank == world - 1)
+    rg = _split(d, world, sizes)[rank]
+    ex = OracleExecutor(d, rg, rank == 0, rank == world - 1)
     B = 3
-    st = PipelineStage(d, rank, world, first, n, device="cpu", seed=SEED, n_microbatches=world, batch=B,
-                       max_ctx=64, prefill_chunk=2, executor=ex)
+    st = PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device="cpu", seed=SEED, n_microbatches=world,
+                       batch=B, max_ctx=64, prefill_chunk=2, executor=ex, skip_first_attn=rg.skip_first_attn,
+                       skip_last_mlp=rg.skip_last_mlp)
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, d.vocab, (B, 9), generator=g) for _ in range(world)]
     st.prefill(prompts)
@@ -119,18 +122,10 @@ def _worker(rank, world, port, n_steps, q, sizes=None, force=False):
 
 
 def _reference(world, n_steps, sizes=None, force=False):
-    """Single process: the same spans chained directly (bf16 hand-off, like the pipeline)."""
+    """Single process: the whole model as one oracle span (no split: the stages' bf16 hand-offs,
+    at layer or half-layer boundaries, are the bf16 residuals a single span computes too)."""
     d = R.CONFIGS["tiny"]
-    split = _split(d, world, sizes)
-    spans = [R.RefSpan(d, SEED, f, f + n - 1, i == 0, i == world - 1, torch.bfloat16, "sdpa")
-             for i, (f, n) in enumerate(split)]
-
-    class Chain:
-        def forward_cached(self, sid, x):
-            for s in spans:
-                x = s.forward_cached(sid, x)
-            return x
-    sp = Chain()
+    sp = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa")
     B = 3
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, d.vocab, (B, 9), generator=g) for _ in range(world)]
@@ -147,7 +142,8 @@ def _reference(world, n_steps, sizes=None, force=False):
     return feeds
 
 
-@pytest.mark.parametrize("world,sizes", [(2, None), (3, None), (3, [1, 2, 1]), (2, [3, 1])])
+@pytest.mark.parametrize("world,sizes", [(2, None), (3, None), (3, [1, 2, 1]), (2, [3, 1]),
+                                         (2, [1.5, 2.5]), (3, [0.5, 2, 1.5])])
 def test_pipeline_matches_single_process(world, sizes):
     n_steps = 4
     ctx = mp.get_context("spawn")
