@@ -73,6 +73,16 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// The lane index recomputed by the instruction that defines it (v_mbcnt, no input register),
+// inside an asm volatile the compiler can neither hoist nor CSE: per-lane addresses derived from
+// it are recomputed where they are used instead of being kept live (and spilled) across a
+// register-heavy loop -- threadIdx.x itself is only an initial register that would have to live.
+__device__ __forceinline__ int opaque_lane() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // Host+device splitmix64 (oracle/weightgen.py defines the same function).
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ull;

@@ -19,8 +19,11 @@ TensorBlob payloads:
     that sends raw blobs gets raw blobs back (`blob_to_tensor` / `tensor_to_blob`).
 The server answers in the format the request's hidden_states used.
 
-Only hidden_states, cache_position and session_id drive the computation: the causal mask
-and (cos, sin) are derived on the device from the positions (Qwen3Server.send docstring).
+hidden_states, cache_position and session_id drive the computation; the causal mask and
+(cos, sin) are derived on the device from the positions, and the request's attention_mask /
+cos_embedding / sin_embedding, when present, must be the ones the engine derives
+(Qwen3Server.send docstring): anything else is refused with INTERNAL, as an exception in the
+reference's forward is (server.py:49-50).
 """
 from __future__ import annotations
 
@@ -120,12 +123,16 @@ class Qwen3LayerServicer:
         try:
             hidden = blob_to_tensor(request.hidden_states.data)
             cache_pos = blob_to_tensor(request.cache_position.data) if request.cache_position.data else None
+            mask = blob_to_tensor(request.attention_mask.data) if request.attention_mask.data else None
+            pe = None
+            if request.cos_embedding.data and request.sin_embedding.data:
+                pe = (blob_to_tensor(request.cos_embedding.data), blob_to_tensor(request.sin_embedding.data))
         except Exception as e:  # noqa: BLE001 -- mirrors server.py:36-37
             context.abort(grpc.StatusCode.INVALID_ARGUMENT, f"Failed to deserialize tensors: {e}")
         sid = request.session_id or None          # server.py:39
         try:
             out = self.server_module.send(session_id=sid, hidden_states=hidden.to(torch.bfloat16),
-                                          attention_mask=None, cache_position=cache_pos, position_embeddings=None)
+                                          attention_mask=mask, cache_position=cache_pos, position_embeddings=pe)
         except Exception as e:  # noqa: BLE001 -- mirrors server.py:49-50
             context.abort(grpc.StatusCode.INTERNAL, f"Error in model forward: {e}")
         out = out.to(hidden.dtype)

@@ -18,9 +18,10 @@ Differences, all on purpose:
     `.numpy()` raises on bf16;  fp32 payloads keep the reference format, and
     INFERD_WIRE_DTYPE=float32 makes a GPU stage emit fp32 for a stock reference node
     downstream (partitioned_models.py:20-26 cannot decode bf16);
-  * the decoder mask argument is accepted for API compatibility but not materialised:
-    causality is implicit in the attention kernels (partitioned_models.py:139-143 only
-    ever builds a full causal mask with positions 0..T-1);
+  * the decoder mask is not materialised: causality is implicit in the attention kernels
+    (partitioned_models.py:139-143 only ever builds the full causal mask of positions
+    0..T-1); any other mask -- padding, non-causal -- raises ValueError (semantics.py) instead
+    of being silently ignored;
   * parts_path is a stage file written by inferd_amd.split_model (safetensors, loaded
     with a loader that executes nothing) or "synthetic:<seed>" for the counter-based
     weights; the reference's pickled `torch.save(module)` (split_model.py:107) is converted
@@ -40,6 +41,7 @@ import numpy as np
 import torch
 
 from .runtime import MODELS, ModelDims, SpanRuntime
+from .semantics import check_bool_causal_mask
 
 _BF16 = "bfloat16"
 
@@ -99,6 +101,7 @@ class _Stage:
 
     def forward(self, model_in, decoder_attn_mask=None, position_ids=None):
         B, T = model_in.shape[0], model_in.shape[1]
+        check_bool_causal_mask(decoder_attn_mask, B, T)
         if position_ids is not None:
             pos = position_ids.reshape(-1, T)[0].tolist()
             if pos != list(range(T)):

@@ -7,12 +7,14 @@ Same constructor `Qwen3Server(start_layer, end_layer)` and the same
 prefill appends T tokens, each decode call appends one, positions continue from the
 cached length (client.py:244-266).
 
-Arguments the GPU path derives itself:
-  * attention_mask -- the client's additive causal mask (client.py:221-224 for prefill,
-    the all-zero (1,1,1,1) mask for decode, :249-250); causality over the cached prefix is
-    implicit in the attention kernels;
-  * position_embeddings -- (cos, sin) of the HF default rope at cache_position
-    (client.py:56-71); the engine keeps the same table (bf16) on the device.
+Arguments the GPU path derives itself, checked (semantics.py) rather than ignored:
+  * attention_mask -- must be the client's additive causal mask (client.py:221-224 for
+    prefill, the all-zero (1,1,1,1) mask for decode, :249-250); causality over the cached
+    prefix is implicit in the attention kernels.  Any other mask (padding, non-causal, a
+    T > 1 call without one) raises ValueError: the reference would apply it;
+  * position_embeddings -- must be (cos, sin) of the HF default rope at cache_position
+    (client.py:56-71); the engine keeps the same table (bf16) on the device.  A shifted or
+    non-default rotary raises ValueError.
 `cache_position` must continue the session's cached length; anything else raises
 (the reference would silently concatenate onto the cache).
 
@@ -29,6 +31,7 @@ from collections import OrderedDict
 import torch
 
 from .runtime import MODELS, ModelDims, SpanRuntime
+from .semantics import check_additive_causal_mask, check_rotary
 
 
 class Qwen3Server:
@@ -85,6 +88,8 @@ class Qwen3Server:
             if cp != list(range(past, past + T)):
                 raise ValueError(f"cache_position {cp[:3]}... does not continue session {session_id!r} "
                                  f"(cached length {past})")
+        check_additive_causal_mask(attention_mask, B, T, past)
+        check_rotary(position_embeddings, torch.arange(past, past + T), self.dims.rope_theta, self.dims.head_dim)
         if self.max_sessions is not None and session_id not in self._lru and len(self._lru) >= self.max_sessions:
             old, _ = self._lru.popitem(last=False)
             self.release(old)

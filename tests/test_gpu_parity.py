@@ -816,14 +816,15 @@ def test_qwen3_server_sessions_files_and_grpc(tmp_path):
     xp = tensor(g["bf16_in_prefill"])
     xd = tensor(g["bf16_in_dec0"])
     srv = Qwen3Server(0, 3, model="tiny", kv_pages=16, max_tokens=64, max_sessions=2)
-    ref_p = srv.send("a", xp.to(DEV), cache_position=torch.arange(8)).cpu()
+    m8 = _client_inputs(d, xp, 0)[0].to(DEV)      # the client's causal mask of an 8-token prefill
+    ref_p = srv.send("a", xp.to(DEV), m8, cache_position=torch.arange(8)).cpu()
     ref_d = srv.send("a", xd.to(DEV), cache_position=torch.tensor([8])).cpu()
     # None: persistent, shared by every None call
-    assert torch.equal(srv.send(None, xp.to(DEV), cache_position=torch.arange(8)).cpu(), ref_p)
+    assert torch.equal(srv.send(None, xp.to(DEV), m8, cache_position=torch.arange(8)).cpu(), ref_p)
     assert torch.equal(srv.send(None, xd.to(DEV), cache_position=torch.tensor([8])).cpu(), ref_d)
     # LRU: a, None resident; b evicts a
     free_before = srv.span.kv.n_free
-    srv.send("b", xp.to(DEV), cache_position=torch.arange(8))
+    srv.send("b", xp.to(DEV), m8, cache_position=torch.arange(8))
     assert srv.span.kv.n_free == free_before  # a's page went back, b took one
     with pytest.raises(ValueError):
         srv.send("a", xd.to(DEV), cache_position=torch.tensor([9]))
@@ -835,7 +836,7 @@ def test_qwen3_server_sessions_files_and_grpc(tmp_path):
         torch.save(sd, os.path.join(tmp_path, f"layer_{i:02d}.pt"))
     srv2 = Qwen3Server(0, 3, model="tiny", weights=os.path.join(tmp_path, "layer_{idx:02d}.pt"), kv_pages=16,
                        max_tokens=64)
-    assert torch.equal(srv2.send("a", xp.to(DEV), cache_position=torch.arange(8)).cpu(), ref_p)
+    assert torch.equal(srv2.send("a", xp.to(DEV), m8, cache_position=torch.arange(8)).cpu(), ref_p)
     # gRPC, both blob formats, session continued across calls
     servicer = Qwen3LayerServicer(0, 3, model="tiny", kv_pages=16, max_tokens=64)
     server, port = make_server(servicer, 0, host="127.0.0.1")
@@ -858,6 +859,52 @@ def test_qwen3_server_sessions_files_and_grpc(tmp_path):
     finally:
         server.stop(0)
     record("qwen3_server_sessions_files_grpc", none_session=True, lru=True, layer_files=True, grpc_blobs=["torch.save", "raw"])
+
+
+def test_nonstandard_masks_and_rotary_raise():
+    """Inputs the engine does not compute are refused, not silently ignored (semantics.py):
+    Qwen3Server.send with a padded or non-causal additive mask, with no mask on a T > 1 call, or
+    with a shifted / scaled (cos, sin) raises ValueError before any kernel runs and leaves the
+    session untouched; the client's own inputs (client.py:221-226, :249-250) give the golden
+    outputs unchanged.  A petals stage module refuses a padded bool mask (the padding half of
+    build_decoder_attention_mask, partitioned_models.py:28-35) and runs the all-ones one."""
+    from inferd_amd.partitioned_models import build_decoder_attention_mask
+    from inferd_amd.qwen3_server import Qwen3Server
+    g = load("tiny_server.npz")
+    d = R.CONFIGS["tiny"]
+    xp, xd = tensor(g["bf16_in_prefill"]).to(DEV), tensor(g["bf16_in_dec0"]).to(DEV)
+    srv = Qwen3Server(0, 3, model="tiny", kv_pages=16, max_tokens=64)
+    mask, pos, cos, sin = _client_inputs(d, xp, 0)
+    padded = mask.clone()
+    padded[..., 0] = torch.finfo(torch.bfloat16).min           # key 0 padded out
+    noncausal = torch.zeros_like(mask)                          # every query sees every key
+    shifted = R.rope_cos_sin(d, (pos + 1)[None], torch.bfloat16)
+    for bad in (dict(attention_mask=padded), dict(attention_mask=noncausal), dict(attention_mask=None),
+                dict(position_embeddings=shifted), dict(position_embeddings=(cos * 1.5, sin))):
+        kw = {"attention_mask": mask.to(DEV), "position_embeddings": (cos.to(DEV), sin.to(DEV)), **bad}
+        with pytest.raises(ValueError):
+            srv.send("s", xp, cache_position=pos, **kw)
+    assert "s" not in {k[1] for k in srv.span.sessions}           # nothing was appended
+    out_p = srv.send("s", xp, mask.to(DEV), pos, (cos.to(DEV), sin.to(DEV))).cpu()
+    m1, p1, c1, s1 = _client_inputs(d, xd, 8)
+    out_d = srv.send("s", xd, m1.to(DEV), p1, (c1.to(DEV), s1.to(DEV))).cpu()
+    assert errs(out_p, tensor(g["bf16_out0"]))["max_norm"] < TOL_REL_EAGER
+    assert errs(out_d, tensor(g["bf16_out1"]))["max_norm"] < TOL_REL_EAGER
+    with pytest.raises(ValueError):    # a decode token whose (1,1,1,1) mask hides a cached key
+        srv.send("s", xd, torch.full((1, 1, 1, 1), torch.finfo(torch.bfloat16).min, device=DEV),
+                 torch.tensor([9]), None)
+    assert out_d.shape == xd.shape
+    from inferd_amd.partitioned_models import load_stage
+    st = load_stage(f"synthetic:{SEED}:tiny:0:3", "tiny", 1, 0, torch.device(DEV))
+    ids = torch.randint(0, d.vocab, (1, 6), generator=torch.Generator().manual_seed(3))
+    pad2d = torch.ones(1, 6, dtype=torch.long)
+    pad2d[0, :2] = 0
+    with pytest.raises(ValueError):
+        st.forward(ids, build_decoder_attention_mask(pad2d), torch.arange(6)[None])
+    ok = st.forward(ids, build_decoder_attention_mask(torch.ones(1, 6, dtype=torch.long)), torch.arange(6)[None])
+    assert torch.equal(ok, st.forward(ids, None, torch.arange(6)[None]))
+    record("nonstandard_masks_rotary_raise", cases=["padded", "noncausal", "none_T>1", "shifted_rope",
+                                                    "scaled_cos", "decode_mask_hides_key", "petals_padding"])
 
 
 # ------------------------------------------------------------------ f4: stage files from checkpoints

@@ -780,6 +780,37 @@ __device__ __forceinline__ void tile_order(const SplitTail& st, int grid_m, int 
   tile_order_v(st, grid_m, grid_n, blockIdx.x, gridDim.x, bm, bn, slice, nsl, sidx);
 }
 
+#ifdef W4_STAMP
+// Lab builds only (tools/build_probes.sh gemm.hip st='-DW4_STAMP=1'; tools/w4_stamps.py):
+// per workgroup of gemm_w4_kernel, 100 MHz real-time stamps at start / after the K-loop /
+// after the tail-split publish or combine / end, and the XCC and HW ids.
+__device__ unsigned long long w4_stamp_buf[4096 * 6];
+extern "C" int inferd_lab_w4_stamps(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(w4_stamp_buf), (size_t)min(n, 4096) * 6 * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#define W4_STAMP_AT(k)                                                               \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                       \
+    w4_stamp_buf[blockIdx.x * 6 + (k)] = __builtin_amdgcn_s_memrealtime();           \
+    if ((k) == 0) {                                                                  \
+      w4_stamp_buf[blockIdx.x * 6 + 4] = __builtin_amdgcn_s_getreg((20 << 0) | (15 << 11)); \
+      w4_stamp_buf[blockIdx.x * 6 + 5] = __builtin_amdgcn_s_getreg((4 << 0) | (31 << 11));  \
+    }                                                                                \
+  }
+// gemm_w4p_kernel<EPI_QKV>: per unit v and wave, stamps at the unit's start (step 0 landed),
+// after its K-loop and after its epilogue: w4p_stamp_buf[(v * 4 + wave) * 4 + k]
+__device__ unsigned long long w4p_stamp_buf[2048 * 16];
+extern "C" int inferd_lab_w4p_stamps(unsigned long long* host, int n_units) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(w4p_stamp_buf), (size_t)min(n_units, 2048) * 16 * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#define W4P_STAMP_AT(k)                                                                     \
+  if (EPI == EPI_QKV && (threadIdx.x & 63) == 0 && v < 2048)                                \
+    w4p_stamp_buf[(v * 4 + (threadIdx.x >> 6)) * 4 + (k)] = __builtin_amdgcn_s_memrealtime();
+#else
+#define W4_STAMP_AT(k)
+#define W4P_STAMP_AT(k)
+#endif
 
 // Tail-split partials: slice sl of split tile sidx is 65536 fp32 at ws + (sidx * nsl + sl) *
 // 65536; accumulator tile (i, j) of thread x is the 16 bytes at ((i * 8 + j) * 256 + x) (one
@@ -830,6 +861,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   __shared__ __attribute__((aligned(16))) char lds[2 * 65536];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wr = wave >> 1, wc = wave & 1;
+  W4_STAMP_AT(0);
   int bm, bn, slice = 0, nsl = 1, sidx = 0;
   tile_order(st, grid_m, grid_n, bm, bn, slice, nsl, sidx);
   const int m0 = bm * 256;
@@ -991,6 +1023,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
   iter(std::integral_constant<int, 1>{}, t);
   iter(std::integral_constant<int, 2>{}, t + 1);
   acc_fence();
+  W4_STAMP_AT(1);
 
   float* part = nsl > 1 ? st.ws + (size_t)sidx * nsl * 65536 : nullptr;
   auto tile_sum = [&](int i, int j) -> f32x4 {
@@ -1009,6 +1042,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      W4_STAMP_AT(2);
+      W4_STAMP_AT(3);
       return;
     }
     if (threadIdx.x == 0) {
@@ -1023,6 +1058,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     // tools/w4_stamps.py measured 54 us of combine for 256 KiB)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  W4_STAMP_AT(2);
 
   // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
 #pragma unroll
@@ -1061,6 +1097,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
       }
     }
   }
+  W4_STAMP_AT(3);
 }
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -1233,18 +1270,12 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
   auto src_of = [&](const Unit& u) {
     const int k0 = u.slice * u.nK;
     src_a = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)u.m0 * lda + k0 * 64), 0, 0x7fffffff, 0x00020000);
-    // the lane from opaque_lane() and the wave from its SGPR: what derives from them is
-    // recomputed per unit instead of hoisted out of the persistent loop and kept live across the
-    // K-loop (hipcc spilled those per-lane invariants in the EPI_QKV instantiation -- 35 VGPRs --
-    // and reloaded them every unit behind vmcnt(0) waits)
-    const int ln = opaque_lane();
-    const int lda2 = (int)lda * 2;  // rr < 256 rows past the unit's base: 32-bit offsets
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
-      const int i = 64 * wv + 8 * p + (ln >> 3);  // image row 0..255
+      const int i = 64 * wave + 8 * p + (lane >> 3);  // image row 0..255
       const int rr = (u.m0 + i < M ? i : M - 1 - u.m0);
-      const int chunk = (ln & 7) ^ ((i >> 1) & 7);
-      a_voff[p] = (unsigned)(rr * lda2 + chunk * 16);
+      const int chunk = (lane & 7) ^ ((i >> 1) & 7);
+      a_voff[p] = (unsigned)(rr * lda * 2 + chunk * 16);
     }
     const int g0 = gnt_of(u, 0);
     src_b = __builtin_amdgcn_make_buffer_rsrc((void*)(Wp + ((int64_t)g0 * KT + 2 * k0) * 512), 0, 0x7fffffff,
@@ -1364,6 +1395,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     }
     first = false;
     raw_barrier();
+    W4P_STAMP_AT(0);
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       read_b(0, g, par);
@@ -1391,11 +1423,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
     iter(std::integral_constant<int, 1>{}, ZF{}, u.nK - 2, par, XPF && has_next);
     iter(std::integral_constant<int, 2>{}, ZF{}, u.nK - 1, par, XPF && has_next);
     acc_fence();
+    W4P_STAMP_AT(1);
 
     if constexpr (EPI == EPI_QKV) {
-      // opaque lane (src_of): the epilogue's per-lane addresses are computed here, not hoisted
-      // across the K-loop (they were the other spills of this instantiation)
-      qkv_epilogue(acc, qe, u.m0 + (wv >> 1) * 128, (u.n0 >> 7) + (wv & 1), M, opaque_lane());
+      qkv_epilogue(acc, qe, u.m0 + wr * 128, (u.n0 >> 7) + wc, M, lane);
     } else {  // ---- epilogue: lane holds C[row = ... + (lane & 15)][col = ... + 4 * (lane >> 4) + r]
       // buffer loads/stores: rows >= M are issued and dropped by the range check, so the
       // epilogue's vector-memory count is fixed (EPI_OPS) and the next unit's wait is exact
@@ -1437,6 +1468,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4p_kernel(
         }
       }
     }
+    W4P_STAMP_AT(2);
     if (!has_next) break;
     par = (par + u.nK) & 1;
     u = un;

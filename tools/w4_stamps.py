@@ -1,6 +1,8 @@
 """Lab: where the time of a tail-split prefill GEMM goes (Qwen3-32B o / down: 640 tiles = 2.5
 rounds of 256 CUs).  Needs a library built with the workgroup stamps:
-    tools/build_probes.sh gemm.hip st='-DW4_STAMP=1'
+    tools/build_probes.sh gemm.hip st='-DW4_STAMP=1' with tools/archive/gemm_stamps_r04.hip (the
+    round-4 kernels with the W4_STAMP hooks) copied over inferd_amd/csrc/gemm.hip in a scratch
+    checkout: the product gemm.hip carries no lab hooks
     python tools/w4_stamps.py tools/probe_libs/libinferd_span_st.so [--shape o|down]
 Runs inferd_gemm (EPI_RESID, the op API's tail split) a few times, then reads the last call's
 per-workgroup stamps (100 MHz real-time clock): start, end of the K-loop, after the tail-split

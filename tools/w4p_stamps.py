@@ -1,6 +1,8 @@
 """Lab: per-tile timeline of the persistent q/k/v GEMM with its fused epilogue (Qwen3-32B, 8k
 prompt: 1280 tiles of 256 x 256 = 5 per CU).  Needs a stamp build:
-    tools/build_probes.sh gemm.hip st='-DW4_STAMP=1'
+    tools/build_probes.sh gemm.hip st='-DW4_STAMP=1' with tools/archive/gemm_stamps_r04.hip (the
+    round-4 kernels with the W4_STAMP hooks) copied over inferd_amd/csrc/gemm.hip in a scratch
+    checkout: the product gemm.hip carries no lab hooks
     python tools/w4p_stamps.py tools/probe_libs/libinferd_span_st.so
 Runs one 1-layer span prefill through that library's C-ABI, then reads the q/k/v GEMM's stamps
 (100 MHz clock; per unit and wave: start with step 0 landed, end of K-loop, end of epilogue)
