@@ -37,7 +37,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-from inferd_amd.pipeline import balanced_split, even_split  # noqa: E402  (host logic only, no GPU)
+from inferd_amd.pipeline import balanced_split, even_split, record_elems  # noqa: E402  (host logic only)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFLOPS = 2500.0
@@ -116,11 +116,12 @@ def parse():
                                                 "balance.py-like split, e.g. 5,27,4; multiples of 0.5 cut between a "
                                                 "layer's attention and MLP halves, e.g. 4.5,4.5,5,...); overrides "
                                                 "--split")
-    p.add_argument("--split", choices=("balanced", "even", "halves"), default="even",
+    p.add_argument("--split", choices=("balanced", "even", "halves", "gateup"), default="even",
                    help="stage layer counts: even = counts differing by at most one (BASELINE config 3, the "
                         "default), balanced = min-max of per-stage decode bytes (lm_head priced on the last stage), "
                         "halves = min-max of per-stage decode time with cuts between a layer's attention and MLP "
-                        "halves allowed (pipeline.halves_split)")
+                        "halves allowed (pipeline.halves_split), gateup = the same with boundaries inside a layer's "
+                        "gate/up projection too (pipeline.gateup_split)")
     p.add_argument("--mode", choices=("decode", "prefill", "stages"), default="decode",
                    help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline); "
                         "stages: the per-stage decode projection of the 2/4/8-GPU splits on one GPU")
@@ -252,7 +253,13 @@ def range_bytes(d, r, B: int, ctx_mean: float, lm_head: bool) -> float:
     attn = kb["rmsnorm"] + kb["qkv_gemm"] + kb["qk_norm_rope_kv"] + kb["attention"] + kb["o_gemm"]
     mlp = kb["rmsnorm"] + kb["gateup_gemm"] + kb["down_gemm"]
     n_attn = sum(1 for u in range(r.first_unit, r.first_unit + r.n_units) if u % 2 == 0)
-    return n_attn * attn + (r.n_units - n_attn) * mlp + (kb["lm_head_argmax"] if lm_head else 0)
+    nb = n_attn * attn + (r.n_units - n_attn) * mlp + (kb["lm_head_argmax"] if lm_head else 0)
+    # gate/up boundaries (StageRange.first_col / last_col): the gate/up columns move between
+    # the two stages (weights in proportion; the act rows are counted once, by the receiver)
+    gu_w = kb["gateup_gemm"] - B * d.intermediate * 2
+    nb -= gu_w * r.first_col / d.intermediate
+    nb += gu_w * r.last_col / d.intermediate
+    return nb
 
 
 def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: int = 3, reps: int = 20) -> dict:
@@ -277,7 +284,7 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
             span = SpanRuntime(d, r.first_layer, r.n_layers, has_embed=first, has_lm_head=last,
                                kv_pages=B * ((ctx + warmup + reps) // 64 + 2) + 4, max_tokens=chunk * ctx,
                                max_seqs=B, max_positions=ctx + warmup + reps + 64, device=dev,
-                               skip_first_attn=r.skip_first_attn, skip_last_mlp=r.skip_last_mlp)
+                               **r.span_kwargs())
             span.init_synthetic(seed)
             sess = [("proj", b) for b in range(B)]
             for c in range(0, B, chunk):
@@ -290,7 +297,11 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
                     span.forward(reqs, x=x, want_hidden=False, want_next_ids=last)
             ids = torch.zeros(B, dtype=torch.int32, device=dev) if first else None
             x = None if first else (torch.randn(B, d.hidden, generator=g) * 0.5).to(torch.bfloat16).to(dev)
-            hout = None if last else torch.empty(B, d.hidden, dtype=torch.bfloat16, device=dev)
+            if r.first_col:      # a gate/up-boundary record: h1, then the packed act
+                x = torch.cat([x.reshape(-1), torch.zeros(record_elems(d, B) - B * d.hidden, dtype=torch.bfloat16,
+                                                          device=dev)])
+            hout = None if last else torch.empty(record_elems(d, B) if r.last_col else B * d.hidden,
+                                                 dtype=torch.bfloat16, device=dev)
             nid = torch.empty(B, dtype=torch.int32, device=dev) if last else None
             graph = DecodeGraph(span, sess, warmup + reps, ids=ids, x=x, hidden_out=hout, next_ids=nid)
             for _ in range(warmup):
@@ -322,7 +333,7 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
 def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
     """The splits stage_projection measures: BASELINE config 3's even splits, the layer-granular
     byte-balanced split and the half-layer time-balanced split at each stage count."""
-    from inferd_amd.pipeline import StageRange, halves_split
+    from inferd_amd.pipeline import StageRange, gateup_split, halves_split
     out = {}
     for n in sizes:
         if n > d.layers:
@@ -331,9 +342,9 @@ def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
         bal = [StageRange.layers(f, k) for f, k in stage_split(d, n, B, ctx, "balanced")]
         if bal != out[f"even{n}"]:
             out[f"balanced{n}"] = bal
-        hv = halves_split(d.layers, n)
-        if all(hv != v for v in out.values()):
-            out[f"halves{n}"] = hv
+        for name, sp in (("halves", halves_split(d.layers, n)), ("gateup", gateup_split(d.layers, n, d.intermediate))):
+            if all(sp != v for v in out.values()):
+                out[f"{name}{n}"] = sp
     return out
 
 
@@ -485,6 +496,8 @@ def main():
             f"--spans {args.spans}: need {world} stages, {d.layers} layers"
     elif args.split == "halves":
         ranges = P.halves_split(d.layers, world)
+    elif args.split == "gateup":
+        ranges = P.gateup_split(d.layers, world, d.intermediate)
     else:
         ranges = [P.StageRange.layers(f, k) for f, k in stage_split(d, world, B, ctx, args.split)]
     rg = ranges[rank]
@@ -495,8 +508,7 @@ def main():
     n_mb = world                                   # microbatches in flight
     st = P.PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=args.seed,
                          n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + args.profile_steps + 64,
-                         prefill_chunk=args.prefill_chunk, skip_first_attn=rg.skip_first_attn,
-                         skip_last_mlp=rg.skip_last_mlp)
+                         prefill_chunk=args.prefill_chunk, **rg.span_kwargs())
     # ---- prefill (untimed): every microbatch's sequences get `ctx` real tokens
     g = torch.Generator().manual_seed(args.seed + 17)
     prompts = [torch.randint(0, d.vocab, (B, ctx), generator=g) for _ in range(n_mb)]
@@ -581,7 +593,8 @@ def main():
             "config": {"workload": f"{args.model} greedy decode, batch {B} per microbatch at {ctx} context "
                                    f"(prefilled), {n_mb} microbatch(es) in flight",
                        "global_batch": B * n_mb, "seq_len": ctx, "parallelism": f"pp{world}",
-                       "spans": [r.n_units / 2 for r in ranges], "stage_ranges": [r.label() for r in ranges]},
+                       "spans": [r.n_units / 2 + (r.last_col - r.first_col) / d.intermediate / 2 for r in ranges],
+                       "stage_ranges": [r.label() for r in ranges]},
             "roofline": roof,
             "roofline_step": {"bound": "hbm", "alg_bytes_per_step": int(sb),
                               "achieved": round(sb / (ms_per_step * 1e-3) / 1e9 / world, 1),

@@ -71,6 +71,17 @@ typedef struct InferdSpanConfig {
    * the same bf16 [n_tokens][hidden] tensor a layer boundary hands over. */
   int32_t skip_first_attn; /* the span begins at its first layer's MLP half (input: h1; no embed) */
   int32_t skip_last_mlp;   /* the span ends after its last layer's attention half (output: h1; no lm_head) */
+  /* A finer boundary inside the gate/up projection, decode calls (<= 64 rows) only: the span
+   * before the boundary also computes gate/up columns [0, c) of that layer's SwiGLU product
+   * `act`, the span after it the columns [c, intermediate) and the down projection.  In a
+   * decode call the hand-off is then a RECORD: h1 bf16 [n_tokens][hidden] row-major, followed
+   * by act bf16 [ceil(n_tokens/16)*16][intermediate] fragment-packed (columns [0, c) filled;
+   * the receiving span completes the other columns in place).  Prefill calls hand over h1 only
+   * and the receiving span computes the whole MLP.  Values and rounding points are those of
+   * one span: act columns are independent, down runs whole on one side.  c: 0 = none, else a
+   * multiple of 128 below intermediate. */
+  int32_t gateup_split_first; /* with skip_first_attn: columns [0, c) arrive in x_in's record */
+  int32_t gateup_split_last;  /* with skip_last_mlp: columns [0, c) are computed into x_out's record */
 } InferdSpanConfig;
 
 /* One forward call's batch: n_seqs sequences, their new tokens concatenated

@@ -78,6 +78,10 @@ struct DecodeArgs {
   // GEMM_PACK_A / GEMM_PACK_C (launch_gemm `pack`): A read / EPI_SILU output written
   // fragment-packed (packed_index); decode path only
   int pack;
+  // EPI_SILU over a column range of the [gate; up] weight (a pipeline stage boundary inside a
+  // layer's gate/up projection): 16-column tiles from a gate tile to its up tile (0: n_tiles,
+  // the whole projection)
+  int up_tiles;
 };
 
 
@@ -153,7 +157,8 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   // free (padding their short streams to whole passes cost 10-25 %: o 8.8 -> 10.1 us,
   // lm_head 232 -> 287 us), and there the merged waits cost less than the padding.
   const bf16x8* w0 = (const bf16x8*)(g.Wp + ((int64_t)nt * g.KT + kt0) * 512) + lane;
-  const bf16x8* w1 = (const bf16x8*)(g.Wp + ((int64_t)(nt + g.n_tiles) * g.KT + kt0) * 512) + lane;
+  const int up_dist = g.up_tiles ? g.up_tiles : g.n_tiles;  // [gate; up]: 16-column tiles from gate to up
+  const bf16x8* w1 = (const bf16x8*)(g.Wp + ((int64_t)(nt + up_dist) * g.KT + kt0) * 512) + lane;
   const u16* a[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -165,7 +170,7 @@ __global__ __launch_bounds__((decode_threads<NW, NORM>())) void gemm_decode_kern
   const __amdgpu_buffer_rsrc_t w0r = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.Wp + ((int64_t)nt * g.KT + kt0) * 512), 0, KT * 1024, 0x00020000);
   const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.Wp + ((int64_t)(nt + g.n_tiles) * g.KT + kt0) * 512), 0, KT * 1024, 0x00020000);
+      (void*)(g.Wp + ((int64_t)(nt + up_dist) * g.KT + kt0) * 512), 0, KT * 1024, 0x00020000);
   const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.A + kt0 * (APK ? 512 : 32)), 0,
       APK ? (int)(((int64_t)(MT - 1) * g.KT + KT) * 1024) : (int)(((int64_t)(M - 1) * g.lda + KT * 32) * 2),
@@ -1539,10 +1544,11 @@ bool gemm_uses_tiled(int M, int N, int K, int epi) {
 
 bool launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s, const GemmWs* ws,
-                 const DecodeNorm* dn, unsigned long long* ssq_out, int pack) {
+                 const DecodeNorm* dn, unsigned long long* ssq_out, int pack, int up_tiles) {
   const int KT = K / 32;
   const int n_tiles = N / 16;  // output tiles of 16 columns
   const bool tiled = gemm_uses_tiled(M, N, K, epi);
+  if (up_tiles && (tiled || epi != EPI_SILU)) return false;  // column ranges: decode SwiGLU only
   if (tiled && use_w4(M, N, K, epi)) {
     const int ncols = (epi == EPI_SILU) ? 128 : 256;
     const int gm = (M + 255) / 256, gn = N / ncols;
@@ -1611,6 +1617,7 @@ bool launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, 
     a.eps = dn ? dn->eps : 0.f;
     a.ssq_out = (epi == EPI_RESID) ? ssq_out : nullptr;
     a.pack = pack;
+    a.up_tiles = up_tiles;
     if (mode == DN_EXACT) {
       a.ssq_in = dn->ssq;
       a.norm_w = dn->w;

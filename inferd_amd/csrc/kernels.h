@@ -105,10 +105,13 @@ void gemm_ws_free(GemmWs* w);
 // the stored outputs -- the DecodeNorm input of the next normed GEMV.  Returns false, launching
 // nothing, for a combination no body implements (DN_EXACT or ssq_out with M > 64, DN_EXACT with
 // EPI_RESID): the caller must fail rather than let a consumer read an unfilled SSQ slot.
+// up_tiles (decode EPI_SILU only, else refused): the [gate; up] weight is a column range of a
+// wider projection -- Wp points at its first gate tile and its up tiles sit up_tiles 16-column
+// tiles after the gate tiles (the whole projection's gate width); 0 = N / 16
 bool launch_gemm(const u16* A, int64_t lda, const u16* Wp, int M, int N, int K, u16* C, int64_t ldc,
                  const u16* R, int64_t ldr, int epi, unsigned long long* keys, hipStream_t s,
                  const GemmWs* ws = nullptr, const DecodeNorm* dn = nullptr, unsigned long long* ssq_out = nullptr,
-                 int pack = 0);
+                 int pack = 0, int up_tiles = 0);
 // launch_gemm `pack` bits (decode path, M <= 64 only; common.h packed_index): A is read
 // fragment-packed / the EPI_SILU or EPI_RESID output C is written so / the EPI_RESID residual
 // R is read so

@@ -152,6 +152,8 @@ struct InferdSpan {
   // skip_last_mlp); only layers with an attention half own a KV pool layer
   bool has_attn(int l) const { return !(l == 0 && cfg.skip_first_attn); }
   bool has_mlp(int l) const { return !(l == cfg.n_layers - 1 && cfg.skip_last_mlp); }
+  // the last layer of a span that ends inside the layer's gate/up projection computes part of it
+  bool has_gateup(int l) const { return has_mlp(l) || (l == cfg.n_layers - 1 && cfg.gateup_split_last); }
   int kv_layers() const { return cfg.n_layers - (cfg.skip_first_attn ? 1 : 0); }
   u16* kv_of(int l) const { return kv_pool + kv_layer_elems * (l - (cfg.skip_first_attn ? 1 : 0)); }
 };
@@ -185,6 +187,11 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
     return fail(INFERD_ERR_ARG, "a half-layer boundary needs n_layers >= 1");
   if (c.skip_first_attn && c.skip_last_mlp && c.n_layers == 1)
     return fail(INFERD_ERR_ARG, "a one-layer span cannot skip both of its halves");
+  for (int32_t col : {c.gateup_split_first, c.gateup_split_last})
+    if (col < 0 || col % 128 || (col && col >= c.intermediate))
+      return fail(INFERD_ERR_ARG, "gate/up split columns: 0, or a multiple of 128 below intermediate");
+  if ((c.gateup_split_first && !c.skip_first_attn) || (c.gateup_split_last && !c.skip_last_mlp))
+    return fail(INFERD_ERR_ARG, "a gate/up split refines a half-layer boundary (skip_first_attn / skip_last_mlp)");
   InferdSpan* s = new InferdSpan();
   s->cfg = c;
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
@@ -208,11 +215,11 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
       SALLOC(L.q_norm, HEAD_DIM * 2);
       SALLOC(L.k_norm, HEAD_DIM * 2);
     }
-    if (s->has_mlp(l)) {
+    if (s->has_gateup(l)) {  // a gate/up boundary's sender owns gate/up too
       SALLOC(L.gateup, (size_t)2 * I * h * 2);
-      SALLOC(L.down, (size_t)h * I * 2);
       SALLOC(L.post_ln, (size_t)h * 2);
     }
+    if (s->has_mlp(l)) SALLOC(L.down, (size_t)h * I * 2);
   }
   if (c.has_embed) SALLOC(s->embed, (size_t)c.vocab * h * 2);
   if (c.has_lm_head) {
@@ -327,9 +334,10 @@ int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t) {
 
 // 1 if span-local layer `layer` runs the half that weight `name` belongs to
 bool owns_weight(const InferdSpan* s, int layer, const char* name) {
-  const bool mlp = !strcmp(name, "gate_proj") || !strcmp(name, "up_proj") || !strcmp(name, "down_proj") ||
-                   !strcmp(name, "post_attention_layernorm");
-  return mlp ? s->has_mlp(layer) : s->has_attn(layer);
+  if (!strcmp(name, "down_proj")) return s->has_mlp(layer);
+  if (!strcmp(name, "gate_proj") || !strcmp(name, "up_proj") || !strcmp(name, "post_attention_layernorm"))
+    return s->has_gateup(layer);
+  return s->has_attn(layer);
 }
 // packed sub-blocks start at an n-tile boundary: offset rows*K elements == (rows/16)*KT*512
 }  // namespace
@@ -445,6 +453,8 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pro = s->adv;
     s->adv_pending = false;
   }
+  if (M <= 64 && c.gateup_split_first && !x_in)
+    return fail(INFERD_ERR_ARG, "a span starting inside a gate/up projection needs x_in (the hand-off record)");
   if (c.has_embed) {
     if (!ids) return fail(INFERD_ERR_ARG, "first span needs token ids");
     if (c.n_layers > 0) {
@@ -491,12 +501,17 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       const DecodeNorm dm = {DN_NONE, c.rms_eps, nullptr, nullptr};
       const int pk =
           (gemv && !gemm_uses_tiled(M, I, h, EPI_SILU) && !gemm_uses_tiled(M, h, I, EPI_RESID)) ? 1 : 0;
+      // a gate/up boundary (decode): columns [0, c0) of act arrived in x_in's record behind h1;
+      // this span completes the record's act in place and runs the whole down projection on it
+      const int c0 = gemv ? c.gateup_split_first : 0;
+      u16* actb = c0 ? (u16*)x_in + (size_t)M * h : s->act;
       pe = s->prof_begin(PROF_GATEUP, st);
-      GEMM_TRY(launch_gemm(s->xn, h, W.gateup, M, I, h, s->act, I, nullptr, 0, EPI_SILU, nullptr, st, &s->gws, &dm,
-                           nullptr, pk ? GEMM_PACK_C : 0));
+      GEMM_TRY(launch_gemm(s->xn, h, W.gateup + (size_t)(c0 / 16) * (h / 32) * 512, M, I - c0, h,
+                           actb + (size_t)(c0 / 32) * 512, I, nullptr, 0, EPI_SILU, nullptr, st, &s->gws, &dm, nullptr,
+                           pk ? GEMM_PACK_C : 0, c0 ? I / 16 : 0));
       s->prof_end(pe, st);
       pe = s->prof_begin(PROF_DOWN, st);
-      GEMM_TRY(launch_gemm(s->act, I, W.down, M, h, I, out, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
+      GEMM_TRY(launch_gemm(actb, I, W.down, M, h, I, out, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
                            (gemv && l + 1 < c.n_layers) ? slot(2 * l + 1) : nullptr,
                            (pk ? GEMM_PACK_A : 0) | (out_packed ? GEMM_PACK_C : 0)));
       s->prof_end(pe, st);
@@ -580,6 +595,8 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       // a packed x
       h1 = x_out ? (u16*)x_out : s->xn;
       h1_packed = false;
+      if (gemv && c.gateup_split_last && !x_out)
+        return fail(INFERD_ERR_ARG, "a span ending inside a gate/up projection needs x_out (the hand-off record)");
     }
     pe = s->prof_begin(PROF_O, st);
     GEMM_TRY(launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
@@ -587,6 +604,17 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
                 (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (h1_packed ? GEMM_PACK_C : 0)));
     s->prof_end(pe, st);
     if (!s->has_mlp(l)) {
+      const int c1 = gemv ? c.gateup_split_last : 0;
+      if (c1) {
+        // a gate/up boundary (decode): act columns [0, c1) go into x_out's record behind h1,
+        // normed from the SSQ slot this layer's o GEMV just filled (the record's act is
+        // fragment-packed with the whole projection's row length, as the receiver reads it)
+        const DecodeNorm dm = {DN_EXACT, c.rms_eps, slot(2 * l), W.post_ln};
+        pe = s->prof_begin(PROF_GATEUP, st);
+        GEMM_TRY(launch_gemm(h1, h, W.gateup, M, c1, h, h1 + (size_t)M * h, I, nullptr, 0, EPI_SILU, nullptr, st,
+                             &s->gws, &dm, nullptr, GEMM_PACK_C, I / 16));
+        s->prof_end(pe, st);
+      }
       x = h1;
       x_packed = false;
       if (layer_out)

@@ -34,6 +34,23 @@ import torch
 from .runtime import KV_PAGE, DecodeGraph, ModelDims, SpanRuntime
 
 
+def record_elems(dims, rows: int) -> int:
+    """bf16 elements of a gate/up-boundary hand-off record of `rows` token rows: h1 [rows][hidden]
+    then the SwiGLU product fragment-packed [rows rounded to 16][intermediate]
+    (include/inferd_span.h InferdSpanConfig gateup_split_*)."""
+    return rows * dims.hidden + (rows + 15) // 16 * 16 * dims.intermediate
+
+
+def handoff_elems(dims, rows: int, col: int) -> int:
+    """Elements of a decode hand-off that carry data: h1 alone (col = 0, a layer or half-layer
+    boundary), else h1 plus the act columns [0, col) -- for <= 16 rows those are one contiguous
+    prefix of the packed act (a 16-row tile's columns [0, col) are its first 16 * col elements),
+    for more rows the whole record."""
+    if not col:
+        return rows * dims.hidden
+    return rows * dims.hidden + 16 * col if rows <= 16 else record_elems(dims, rows)
+
+
 def even_split(n_layers: int, n: int):
     """[(first layer, layer count)] per stage, counts differing by at most one."""
     base, extra = divmod(n_layers, n)
@@ -81,12 +98,19 @@ class StageRange:
     (input_layernorm .. o_proj + residual), unit 2*l + 1 its MLP half (post_attention_layernorm
     .. down_proj + residual), qwen3_server_module.py:179-206.  The reference cuts spans at
     layer boundaries only (split_model.py:92-108); a cut between the halves hands over the
-    residual stream h1, a bf16 [tokens, hidden] tensor like a layer boundary's."""
-    __slots__ = ("first_unit", "n_units")
+    residual stream h1, a bf16 [tokens, hidden] tensor like a layer boundary's.
+    first_col / last_col refine a half boundary into the layer's gate/up projection (decode
+    calls; InferdSpanConfig gateup_split_*): the stage before it also computes gate/up columns
+    [0, col), the stage after it the rest and the down projection, and the hand-off is h1 plus
+    the packed SwiGLU product (a record)."""
+    __slots__ = ("first_unit", "n_units", "first_col", "last_col")
 
-    def __init__(self, first_unit: int, n_units: int):
+    def __init__(self, first_unit: int, n_units: int, first_col: int = 0, last_col: int = 0):
         assert first_unit >= 0 and n_units >= 1
         self.first_unit, self.n_units = first_unit, n_units
+        self.first_col, self.last_col = first_col, last_col
+        assert not first_col or self.skip_first_attn, "first_col refines a stage that starts at an MLP half"
+        assert not last_col or self.skip_last_mlp, "last_col refines a stage that ends after an attention half"
 
     @classmethod
     def layers(cls, first_layer: int, n_layers: int) -> "StageRange":
@@ -99,16 +123,23 @@ class StageRange:
     skip_last_mlp = property(lambda self: (self.first_unit + self.n_units) % 2 == 1)
 
     def label(self) -> str:
-        """e.g. '4m..8' = layer 4's MLP half through layer 8; '9..13a' ends with 13's attention half"""
-        a = f"{self.first_layer}{'m' if self.skip_first_attn else ''}"
-        b = f"{self.last_layer}{'a' if self.skip_last_mlp else ''}"
+        """e.g. '4m..8' = layer 4's MLP half through layer 8; '9..13a' ends with 13's attention
+        half; '13m@6144..' / '..13a+6144': a gate/up boundary at column 6144 of layer 13"""
+        a = f"{self.first_layer}{'m' if self.skip_first_attn else ''}{f'@{self.first_col}' if self.first_col else ''}"
+        b = f"{self.last_layer}{'a' if self.skip_last_mlp else ''}{f'+{self.last_col}' if self.last_col else ''}"
         return f"{a}..{b}"
 
+    def span_kwargs(self) -> dict:
+        """The SpanRuntime / PipelineStage keyword arguments of this range's boundaries."""
+        return {"skip_first_attn": self.skip_first_attn, "skip_last_mlp": self.skip_last_mlp,
+                "gateup_split_first": self.first_col, "gateup_split_last": self.last_col}
+
     def __eq__(self, o):
-        return isinstance(o, StageRange) and (o.first_unit, o.n_units) == (self.first_unit, self.n_units)
+        return isinstance(o, StageRange) and (o.first_unit, o.n_units, o.first_col, o.last_col) == \
+            (self.first_unit, self.n_units, self.first_col, self.last_col)
 
     def __repr__(self):
-        return f"StageRange({self.first_unit}, {self.n_units})"
+        return f"StageRange({self.first_unit}, {self.n_units}, {self.first_col}, {self.last_col})"
 
 
 def ranges_from_sizes(sizes) -> list:
@@ -166,6 +197,105 @@ def halves_split(n_layers: int, n: int, costs: dict = DECODE_US_8B):
     return balanced_units(units, n, costs["head"], costs["stage_norm"])
 
 
+# the gate/up share of the MLP half's decode time (profiles/r04/decode_kernel_trace.json:
+# gate/up 33.57 us, down 19.99 us) -- what a column of the gate/up boundary costs
+DECODE_US_8B_GATEUP = 33.57
+
+
+# algorithmic decode bytes per unit at Qwen3-8B, B = 16, ctx 2k (bench.py kernel_bytes), MB: the
+# attention half (norm, q/k/v, attention, o), the gate/up projection, the down projection, the
+# last stage's final norm + lm_head
+DECODE_MB_8B = {"attn_half": 221.6, "gateup": 202.2, "down": 101.6, "head": 1245.0}
+
+
+def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_US_8B, step: int = 256,
+                 gateup_us: float = DECODE_US_8B_GATEUP, mb: dict = DECODE_MB_8B):
+    """Stages cut anywhere in the layer timeline a boundary may sit -- a layer start, or inside
+    a layer's MLP before gate/up column c (c = 0: the half boundary; 0 < c < intermediate, a
+    multiple of `step`: a gate/up boundary) -- so that the lowest stage's HBM fraction at the
+    pipeline's tick, min_s bytes_s / max_s time_s, is the highest the time / byte model allows
+    (an exact search: for a tick bound T the best split is a DP over the cut points; T on a
+    4-us grid from the ideal total / n, then refined to 0.5 us).  Time model: costs
+    (DECODE_US_8B) with the MLP half split into gate/up (gateup_us, linear in the columns) and
+    down; bytes: mb.  Boundaries cannot sit inside an attention half (its K/V live where it
+    runs), so stage boundaries that fall there move to the nearest MLP."""
+    a, mlp, hd, sn = costs["attn_half"], costs["mlp_half"], costs["head"], costs["stage_norm"]
+    ncol = intermediate // step
+    # cut points in timeline order: (layer, col) with col = -1 (layer start) or 0 .. ncol-1
+    # (inside the MLP before gate/up column col * step); time and bytes up to each cut
+    cuts, times, byts, t, y = [], [], [], 0.0, 0.0
+    for l in range(n_layers):
+        cuts.append((l, -1))
+        times.append(t)
+        byts.append(y)
+        t += a
+        y += mb["attn_half"]
+        for k in range(ncol):
+            cuts.append((l, k))
+            times.append(t + gateup_us * k / ncol)
+            byts.append(y + mb["gateup"] * k / ncol)
+        t += mlp
+        y += mb["gateup"] + mb["down"]
+    cuts.append((n_layers, -1))
+    times.append(t)
+    byts.append(y)
+    P = len(cuts) - 1
+
+    # for a tick bound T: f[l] = the highest min over the stages so far of bytes / T with the
+    # last of them ending at cut l and every stage within T (numpy over the previous cut j)
+    import numpy as np
+    tm, by = np.array(times), np.array(byts)
+
+    def solve(T):
+        """(value, boundary cuts) of the best split with every stage within T"""
+        f = np.full(P + 1, -1.0)
+        f[0] = np.inf
+        arg = []
+        for s in range(n):
+            last = s == n - 1
+            extra = sn + (hd if last else 0.0)
+            g = np.full(P + 1, -1.0)
+            gi = np.zeros(P + 1, dtype=np.int64)
+            ends = [P] if last else range(s + 1, P - (n - 1 - s) + 1)
+            for l in ends:
+                j0 = max(int(np.searchsorted(tm, tm[l] - (T - extra), side="left")), s)
+                if j0 >= l:
+                    continue
+                js = np.arange(j0, l)
+                fj = f[j0:l]
+                v = np.where(fj >= 0, np.minimum(fj, (by[l] - by[j0:l] + (mb["head"] if last else 0.0)) / T), -1.0)
+                k = int(v.argmax())
+                g[l], gi[l] = v[k], js[k]
+            arg.append(gi)
+            f = g
+        if f[P] < 0:
+            return -1.0, None
+        b, l = [P], P
+        for s in range(n - 1, -1, -1):
+            l = int(arg[s][l])
+            b.append(l)
+        return float(f[P]), b[::-1]
+    # the tick: coarse grid from the ideal (total / n), then refined around the best
+    lo_t = (times[P] + n * sn + hd) / n
+    best_val, best_b, best_T = -1.0, None, lo_t
+    for T in np.arange(lo_t, lo_t * 1.12, 4.0):
+        v, bb = solve(T)
+        if v > best_val:
+            best_val, best_b, best_T = v, bb, T
+    for T in np.arange(best_T - 4.0, best_T + 4.0, 0.5):
+        v, bb = solve(T)
+        if v > best_val:
+            best_val, best_b = v, bb
+    b = best_b
+    out = []
+    for s in range(n):
+        (l0, c0), (l1, c1) = cuts[b[s]], cuts[b[s + 1]]
+        first_unit = 2 * l0 + (0 if c0 < 0 else 1)
+        end_unit = 2 * l1 + (0 if c1 < 0 else 1)     # exclusive, in half units
+        out.append(StageRange(first_unit, end_unit - first_unit, max(c0, 0) * step, max(c1, 0) * step))
+    return out
+
+
 class SpanExecutor:
     """Runs one span's compute for pipeline items on this rank's GPU."""
 
@@ -183,7 +313,7 @@ class SpanExecutor:
                                 want_hidden=not want_ids, want_next_ids=want_ids, want_logits=want_logits)
         if want_ids:
             return (out["next_ids"], out["logits"]) if want_logits else out["next_ids"]
-        return out["hidden"]
+        return out.get("record", out["hidden"])   # a decode-sized call across a gate/up boundary
 
     def prepare_decode(self, microbatches, n_steps, bufs):
         """Capture one decode graph per microbatch over its fixed buffers
@@ -218,11 +348,14 @@ class PipelineStage:
     def __init__(self, dims: ModelDims, rank: int, world: int, first_layer: int, n_layers: int, *,
                  device, seed: int, n_microbatches: int, batch: int, max_ctx: int, prefill_chunk: int = 2,
                  executor=None, group=None, profile: str = "random", want_logits: bool = False,
-                 skip_first_attn: bool = False, skip_last_mlp: bool = False):
+                 skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
+                 gateup_split_last: int = 0):
         """profile: the synthetic weight profile (runtime.SpanRuntime.init_synthetic: "peaked"
         for token-exact parity runs).  want_logits (last stage): every decode step's and the
         prefill's last-row logits are kept, for parity checks against the oracle's.
-        skip_first_attn / skip_last_mlp: a half-layer stage boundary (StageRange)."""
+        skip_first_attn / skip_last_mlp / gateup_split_*: the stage's sub-layer boundaries
+        (StageRange.span_kwargs()); across a gate/up boundary a decode-sized hand-off is a record
+        (h1 + the packed SwiGLU product, handoff_elems)."""
         assert n_microbatches == world, "the ring schedule keeps exactly one microbatch per stage in flight"
         self.dims, self.rank, self.world = dims, rank, world
         self.S = world
@@ -236,7 +369,8 @@ class PipelineStage:
                                kv_pages=n_microbatches * batch * pages_per_seq + 4,
                                max_tokens=max(prefill_chunk * max_ctx, batch), max_seqs=max(batch, prefill_chunk),
                                max_positions=max_ctx, device=self.device, skip_first_attn=skip_first_attn,
-                               skip_last_mlp=skip_last_mlp)
+                               skip_last_mlp=skip_last_mlp, gateup_split_first=gateup_split_first,
+                               gateup_split_last=gateup_split_last)
             span.init_synthetic(seed, profile)
             executor = SpanExecutor(span)
         self.ex = executor
@@ -245,9 +379,12 @@ class PipelineStage:
         h = dims.hidden
         dev = self.device
         mb = range(n_microbatches)
+        self.col_in, self.col_out = gateup_split_first, gateup_split_last
         self.ids = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
-        self.h_in = [torch.zeros(batch, h, dtype=torch.bfloat16, device=dev) for _ in mb]
-        self.h_out = [torch.zeros(batch, h, dtype=torch.bfloat16, device=dev) for _ in mb]
+        self.h_in = [torch.zeros(record_elems(dims, batch) if self.col_in else (batch, h), dtype=torch.bfloat16,
+                                 device=dev) for _ in mb]
+        self.h_out = [torch.zeros(record_elems(dims, batch) if self.col_out else (batch, h), dtype=torch.bfloat16,
+                                  device=dev) for _ in mb]
         self.ids_out = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
         self.want_logits = want_logits and rank == world - 1
         self.logits = [torch.zeros(batch, dims.vocab, dtype=torch.bfloat16, device=dev) for _ in mb] \
@@ -353,11 +490,21 @@ class PipelineStage:
             send = recv = None
             if not self.last and 0 <= i_send < len(items):
                 send = bufs_out.pop(i_send)
+                m, c = items[i_send]
+                rows = min(self.prefill_chunk, self.B - c) * T
+                if self.col_out and rows <= 64:           # a decode-sized call: record hand-off
+                    send = send[:handoff_elems(self.dims, rows, self.col_out)]
             if not self.first and 0 <= i_cur < len(items):
                 m, c = items[i_cur]
                 nseq = min(self.prefill_chunk, self.B - c)
-                recv = torch.empty(nseq * T, h, dtype=torch.bfloat16, device=self.device)
-                bufs_in[i_cur] = recv
+                rows = nseq * T
+                if self.col_in and rows <= 64:
+                    recv = torch.zeros(record_elems(self.dims, rows), dtype=torch.bfloat16, device=self.device)
+                    bufs_in[i_cur] = recv
+                    recv = recv[:handoff_elems(self.dims, rows, self.col_in)]
+                else:
+                    recv = torch.empty(rows, h, dtype=torch.bfloat16, device=self.device)
+                    bufs_in[i_cur] = recv
             if S > 1:
                 self._exchange(send, (self.rank + 1) % S, recv, (self.rank - 1) % S)
             if 0 <= i_cur < len(items):
@@ -377,8 +524,8 @@ class PipelineStage:
                     ids_parts[(m, c)] = out
                 else:
                     bufs_out[i_cur] = out
-                    if capture is not None and i_cur == 0:
-                        capture["hidden"] = out.cpu()
+                    if capture is not None and i_cur == 0:     # h1 rows (the head of a record)
+                        capture["hidden"] = out.reshape(-1)[:len(sess) * T * h].reshape(len(sess) * T, h).cpu()
         if self.last:
             for m in range(self.n_mb):
                 first_ids[m] = torch.cat([ids_parts[(m, c)] for c in range(0, self.B, self.prefill_chunk)])
@@ -441,12 +588,16 @@ class PipelineStage:
             if 0 <= i_prev < n_items:                      # output of last tick
                 mp = i_prev % self.n_mb
                 send = self.ids_out[mp] if self.last else self.h_out[mp]
+                if self.col_out and not self.last:         # a record: h1 + the act columns it carries
+                    send = send[:handoff_elems(self.dims, self.B, self.col_out)]
             if self.first:
                 j = t - S                                  # ids of item j feed item j + S
                 if 0 <= j < n_items:
                     recv = self.ids[j % self.n_mb]
             elif 0 <= i_cur < n_items:
                 recv = self.h_in[i_cur % self.n_mb]
+                if self.col_in:
+                    recv = recv[:handoff_elems(self.dims, self.B, self.col_in)]
             tx = time.perf_counter()
             self._exchange(send, (self.rank + 1) % S, recv, (self.rank - 1) % S)
             t_x += time.perf_counter() - tx

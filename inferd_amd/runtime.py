@@ -203,14 +203,19 @@ class SpanRuntime:
     def __init__(self, dims: ModelDims, first_layer: int, n_layers: int, *, has_embed: bool,
                  has_lm_head: bool, kv_pages: int = 256, max_tokens: int = 4096, max_seqs: int = 64,
                  max_positions: int | None = None, device: str | torch.device = "cuda",
-                 skip_first_attn: bool = False, skip_last_mlp: bool = False):
+                 skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
+                 gateup_split_last: int = 0):
         """skip_first_attn / skip_last_mlp: sub-layer stage boundaries (InferdSpanConfig): the
         span starts at its first layer's MLP half (x = that layer's post-attention residual)
-        and/or ends after its last layer's attention half (hidden out = that residual)."""
+        and/or ends after its last layer's attention half (hidden out = that residual).
+        gateup_split_first / _last: the boundary sits inside that layer's gate/up projection at
+        this column; decode calls then hand over a record (h1, then the packed SwiGLU product,
+        record_elems()) instead of h1 alone."""
         self.dims = dims
         self.first_layer, self.n_layers = first_layer, n_layers
         self.has_embed, self.has_lm_head = has_embed, has_lm_head
         self.skip_first_attn, self.skip_last_mlp = bool(skip_first_attn), bool(skip_last_mlp)
+        self.gateup_split_first, self.gateup_split_last = int(gateup_split_first), int(gateup_split_last)
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -218,7 +223,7 @@ class SpanRuntime:
         self.max_positions = max_positions or dims.max_positions
         cfg = [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
                n_layers, int(has_embed), int(has_lm_head), self.max_positions, kv_pages, max_tokens, max_seqs,
-               int(skip_first_attn), int(skip_last_mlp)]
+               int(skip_first_attn), int(skip_last_mlp), int(gateup_split_first), int(gateup_split_last)]
         self.handle = None
         self.handle = T.span_create(cfg, dims.eps, dims.rope_theta, self.device)
         self.kv = KvTable(kv_pages)
@@ -230,6 +235,12 @@ class SpanRuntime:
         if h:
             T.span_destroy(h)
             self.handle = None
+
+    def record_elems(self, rows: int) -> int:
+        """bf16 elements of a decode hand-off record at a gate/up boundary: h1 [rows][hidden]
+        then the packed SwiGLU product [rows rounded to 16][intermediate]
+        (include/inferd_span.h, InferdSpanConfig gateup_split_*)."""
+        return rows * self.dims.hidden + (rows + 15) // 16 * 16 * self.dims.intermediate
 
     # ----------------------------------------------------------------- weights
     def _stream(self):
@@ -394,7 +405,15 @@ class SpanRuntime:
             else:
                 if x is None:
                     raise ValueError("span needs hidden states x")
-                x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(total, d.hidden).contiguous()
+                if self.gateup_split_first and total <= 64:   # a decode hand-off record (h1 | act)
+                    x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(-1).contiguous()
+                    if x_d.numel() < self.record_elems(total):
+                        raise ValueError(f"x: a gate/up-boundary record of {self.record_elems(total)} elements "
+                                         f"expected for {total} rows, got {x_d.numel()}")
+                else:
+                    x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(total, d.hidden).contiguous()
+            rec_in = x_d is not None and x_d.dim() == 1
+            rec_out = bool(self.gateup_split_last) and total <= 64 and want_hidden
             temp = []
             states = []
             for sid, _ in requests:
@@ -411,6 +430,10 @@ class SpanRuntime:
                 B = len(requests)
                 lm = self.has_lm_head
                 hid = torch.empty((total, d.hidden), dtype=torch.bfloat16, device=dev) if want_hidden else None
+                rec = None
+                if rec_out:      # h1 then the packed act columns this span computes
+                    rec = torch.empty(self.record_elems(total), dtype=torch.bfloat16, device=dev)
+                    hid = rec[:total * d.hidden].view(total, d.hidden)
                 nid = torch.empty((B,), dtype=torch.int32, device=dev) if (want_next_ids and lm) else None
                 lg = torch.empty((B, d.vocab), dtype=torch.bfloat16, device=dev) if (want_logits and lm) else None
                 lay = torch.empty((self.n_layers, total, d.hidden), dtype=torch.bfloat16, device=dev) \
@@ -419,6 +442,11 @@ class SpanRuntime:
                 for _, n in requests:
                     row0.append(row0[-1] + n)
                 calls = self._plan(requests)
+                if (self.gateup_split_first or self.gateup_split_last) and \
+                        ((rec_in or rec_out) and len(calls) > 1 or
+                         total > 64 and any(sum(t for _, _, t in c) <= 64 for c in calls)):
+                    raise ValueError("across a gate/up boundary a call is either one decode-sized engine call "
+                                     "(<= 64 rows, record hand-off) or only prefill-sized ones (> 64 rows)")
                 keep = []
                 for call in calls:
                     r0 = row0[call[0][0]] + call[0][1]
@@ -434,9 +462,9 @@ class SpanRuntime:
                     c_lay = lay if single else (torch.empty((self.n_layers, m, d.hidden), dtype=torch.bfloat16,
                                                             device=dev) if lay is not None else None)
                     self.run(batch, ids=None if ids_d is None else ids_d[r0:r0 + m],
-                             x=None if x_d is None else x_d[r0:r0 + m],
-                             hidden=None if hid is None else hid[r0:r0 + m], next_ids=c_nid, logits=c_lg,
-                             layers=c_lay)
+                             x=None if x_d is None else (x_d if rec_in else x_d[r0:r0 + m]),
+                             hidden=None if hid is None else (rec if rec is not None else hid[r0:r0 + m]),
+                             next_ids=c_nid, logits=c_lg, layers=c_lay)
                     for i, _, t in call:
                         self.kv.advance(states[i].seq, t)
                     advanced = True
@@ -461,6 +489,8 @@ class SpanRuntime:
         out = {}
         if hid is not None:
             out["hidden"] = hid
+        if rec_out:
+            out["record"] = rec
         if nid is not None:
             out["next_ids"] = nid
         if lg is not None:

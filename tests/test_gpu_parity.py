@@ -380,6 +380,20 @@ def _free_port():
     return p
 
 
+def _ranges(sizes):
+    """StageRanges of a test split: stage sizes in layers (multiples of 0.5: half-layer
+    boundaries), or "gateup8" -- bench.py --split gateup at 8 stages (boundaries inside gate/up
+    projections, record hand-offs)"""
+    from inferd_amd.pipeline import gateup_split, ranges_from_sizes
+    if sizes == "gateup8":
+        return gateup_split(36, 8, 12288)
+    return ranges_from_sizes(sizes)
+
+
+def _tag(sizes):
+    return sizes if isinstance(sizes, str) else "-".join(map(str, sizes))
+
+
 B8, T8, STEPS8 = 16, 2048, 4
 # the 8-stage half-layer split bench.py --split halves runs (pipeline.halves_split: cuts between a
 # layer's attention and MLP halves; stage sizes in layers)
@@ -401,11 +415,9 @@ def _pipe_worker(rank, world, port, sizes, out_dir):
     d = MODELS["qwen3-8b"]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    from inferd_amd.pipeline import ranges_from_sizes
-    rg = ranges_from_sizes(sizes)[rank]
+    rg = _ranges(sizes)[rank]
     st = PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=SEED, n_microbatches=world,
-                       batch=B8, max_ctx=T8 + STEPS8 + 8, prefill_chunk=2, want_logits=True,
-                       skip_first_attn=rg.skip_first_attn, skip_last_mlp=rg.skip_last_mlp)
+                       batch=B8, max_ctx=T8 + STEPS8 + 8, prefill_chunk=2, want_logits=True, **rg.span_kwargs())
     cap = {} if rank in (0, world - 1) else None
     st.prefill(_prompts(world), capture=cap)
     st.prepare_decode(STEPS8)
@@ -477,9 +489,9 @@ def q8b_prefill_logits_oracle():
 
 @pytest.mark.timeout(1200)
 @pytest.mark.parametrize("sizes", [[18, 18], [9, 9, 9, 9], [5, 5, 5, 5, 4, 4, 4, 4], [5, 27, 4], [6, 12, 12, 6],
-                                   [2, 3, 5, 6, 6, 6, 5, 3], HALVES8],
+                                   [2, 3, 5, 6, 6, 6, 5, 3], HALVES8, "gateup8"],
                          ids=["config3_even2", "config3_even4", "config3_even8", "config4_uneven3", "config4_uneven4",
-                              "config4_uneven8", "halves8"])
+                              "config4_uneven8", "halves8", "gateup8"])
 def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_logits_oracle):
     """BASELINE configs 3 (Qwen3-8B, the even splits [18,18], [9,9,9,9], [5,5,5,5,4,4,4,4]) and 4
     (SURVEY §8(d)'s uneven splits [5, 27, 4], [6, 12, 12, 6], [2, 3, 5, 6, 6, 6, 5, 3]) at full
@@ -491,7 +503,7 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     recorded); the first stage boundary's hidden state of sequence 0 is no further from an fp32
     oracle than the bf16 oracle is, and (boundaries up to 9 layers deep, sequences 0 and 1) is
     within the span tolerance of the bf16 oracle.  Checked against a single 36-layer HIP span: the greedy ids fed back to stage 0."""
-    world = len(sizes)
+    world = len(_ranges(sizes))
     port = _free_port()
     _spawn(_pipe_worker, [(r, world, port, sizes, str(tmp_path)) for r in range(world)])
     _spawn(_single_worker, [(_free_port(), world, str(tmp_path))])
@@ -503,8 +515,7 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     assert got == one
     d = R.CONFIGS["qwen3-8b"]
     ids = _prompts(world)[0][:2]
-    from inferd_amd.pipeline import ranges_from_sizes
-    r0 = ranges_from_sizes(sizes)[0]
+    r0 = _ranges(sizes)[0]
     ref = R.RefSpan(d, SEED, 0, r0.last_layer, True, False, torch.bfloat16, "sdpa",
                     skip_last_mlp=r0.skip_last_mlp).forward(ids)
     h = pipe["hidden"].reshape(2, T8, -1)
@@ -521,7 +532,7 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     # the span tolerance (TOL_SPAN / TOL_SPAN_RMS) holds for the shallow boundaries (<= 9 layers);
     # 18 layers deep the engine is 3.6 % (rms) from the bf16 oracle, as far as the bf16 oracle
     # itself is from fp32 arithmetic there, so deeper than 9 layers the noise floor above decides
-    if sizes[0] <= 9:
+    if r0.n_units <= 18:
         assert all(span_ok(x) for x in e)
     lg = torch.load(os.path.join(tmp_path, "logits0.pt"), weights_only=True)
     o16, o32 = q8b_prefill_logits_oracle["bf16"], q8b_prefill_logits_oracle["fp32"]
@@ -533,7 +544,7 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     # after 36 random-weight layers the bf16 oracle itself is ~6 % (rms) from fp32 arithmetic on
     # these logits (CPU measurement), so the assertion is the noise-floor rule, not a span tolerance
     assert lratio <= NOISE_RATIO, lnoise
-    record(f"q8b_pipeline_{'-'.join(map(str, sizes))}", ids_identical=True, decode_steps=STEPS8,
+    record(f"q8b_pipeline_{_tag(sizes)}", ids_identical=True, decode_steps=STEPS8,
            microbatches=world, boundary_err=e, noise_floor=noise, last_stage_prefill_logits=el,
            last_stage_logits_noise=lnoise, last_stage_logits_noise_ratio=lratio)
 
@@ -617,11 +628,10 @@ def _pipe_exact_worker(rank, world, port, sizes, out_dir, profile="peaked_deep",
     d = MODELS["qwen3-8b"]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    from inferd_amd.pipeline import ranges_from_sizes
-    rg = ranges_from_sizes(sizes)[rank]
+    rg = _ranges(sizes)[rank]
     st = PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=SEED, n_microbatches=world,
                        batch=b, max_ctx=T8X + steps + 8, prefill_chunk=2, profile=profile, want_logits=True,
-                       skip_first_attn=rg.skip_first_attn, skip_last_mlp=rg.skip_last_mlp)
+                       **rg.span_kwargs())
     force = None
     fp = os.path.join(out_dir, "force.pt")
     if os.path.exists(fp):
@@ -646,9 +656,9 @@ def _pipe_exact_worker(rank, world, port, sizes, out_dir, profile="peaked_deep",
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("sizes", [[18, 18], [9, 9, 9, 9], [5, 5, 5, 5, 4, 4, 4, 4], [4, 5, 5, 5, 5, 5, 5, 2],
-                                   [5, 27, 4], HALVES8],
+                                   [5, 27, 4], HALVES8, "gateup8"],
                          ids=["config3_even2", "config3_even4", "config3_even8", "balanced8", "config4_uneven3",
-                              "halves8"])
+                              "halves8", "gateup8"])
 def test_q8b_pipeline_token_exact_vs_oracle(tmp_path, sizes, q8b_oracle_greedy):
     """Qwen3-8B through the span pipeline against the CPU oracle ("peaked_deep" profile, see the
     section comment for what each check proves):
@@ -662,7 +672,7 @@ def test_q8b_pipeline_token_exact_vs_oracle(tmp_path, sizes, q8b_oracle_greedy):
         steps (layer arithmetic)."""
     ref_ids, ref_lg, ref32 = q8b_oracle_greedy
     prompts = _q8b_exact_prompts()
-    world = len(sizes)
+    world = len(_ranges(sizes))
     port = _free_port()
     _spawn(_pipe_exact_worker, [(r, world, port, sizes, str(tmp_path)) for r in range(world)])
     fed = torch.load(os.path.join(tmp_path, "ids.pt"), weights_only=True)
@@ -710,7 +720,7 @@ def test_q8b_pipeline_token_exact_vs_oracle(tmp_path, sizes, q8b_oracle_greedy):
           f"microbatches x {B8X}); smallest margin {min(x['margin'] for x in steps):.2f}, worst logit error "
           f"{worst:.3f}; fp32 noise ratio max {max(ratios):.2f}; masked argmax identical on {len(masked)} "
           f"checked steps; host {last['tick']}")
-    record(f"q8b_pipeline_token_exact_{'-'.join(map(str, sizes))}", spans=sizes, microbatches=world, batch=B8X,
+    record(f"q8b_pipeline_token_exact_{_tag(sizes)}", spans=[r.label() for r in _ranges(sizes)], microbatches=world, batch=B8X,
            prompt_len=T8X, decode_steps=STEPS8X, ids_checked=len(chosen) * B8X + len(fed) * B8X, identical=True,
            noise_ratio_max=max(ratios), noise_ratios=ratios, masked_checked=len(masked),
            masked_checked_steps=masked, tick=last["tick"], steps=steps)

@@ -271,6 +271,59 @@ def test_half_layer_stage_chain_bit_exact():
         s.check_errors()
 
 
+@pytest.mark.parametrize("T", [70, 9], ids=["prefill_h1", "prefill_record"])
+def test_gateup_boundary_chain_bit_exact(T):
+    """Stage boundaries inside a layer's gate/up projection (InferdSpanConfig gateup_split_*):
+    Qwen3-0.6B layers 0..3 as [0..1a+1024] (embed), [1m@1024..2a+2048], [2m@2048..3] (lm_head)
+    give bit-identical logits to one span: a prefill of 3 sequences (T = 70: 210 rows, h1
+    hand-offs, the receiver runs the whole MLP; T = 9: 27 rows, decode-sized calls with record
+    hand-offs), then 5 decode-graph steps whose hand-offs are records (h1, then act columns
+    [0, c) fragment-packed, completed in place by the receiver)."""
+    from inferd_amd.pipeline import StageRange, handoff_elems, record_elems
+    from inferd_amd.runtime import DecodeGraph
+    d = R.CONFIGS["qwen3-0.6b"]
+    B, STEPS = 3, 5
+    gen = torch.Generator().manual_seed(41)
+    prompts = torch.randint(0, d.vocab, (B, T), generator=gen)
+    forced = torch.randint(0, d.vocab, (STEPS, B), generator=gen)
+    ranges = [StageRange(0, 3, 0, 1024), StageRange(3, 2, 1024, 2048), StageRange(5, 3, 2048, 0)]
+    chain = [span("qwen3-0.6b", r.first_layer, r.n_layers, i == 0, i == 2, kv_pages=16, max_tokens=B * T + 64,
+                  max_seqs=B, max_positions=1024, **r.span_kwargs()) for i, r in enumerate(ranges)]
+    one = span("qwen3-0.6b", 0, 4, True, True, kv_pages=16, max_tokens=B * T + 64, max_seqs=B, max_positions=1024)
+    sess = [f"g{b}" for b in range(B)]
+    reqs = [(sid, T) for sid in sess]
+    o0 = chain[0].forward(reqs, ids=prompts.reshape(-1))
+    h0 = o0.get("record", o0["hidden"])
+    o1 = chain[1].forward(reqs, x=h0)
+    h1 = o1.get("record", o1["hidden"])
+    assert ("record" in o0) == (B * T <= 64)
+    lc = chain[2].forward(reqs, x=h1, want_logits=True, want_hidden=False)["logits"]
+    lo = one.forward(reqs, ids=prompts.reshape(-1), want_logits=True, want_hidden=False)["logits"]
+    assert torch.equal(lc, lo), (lc.float() - lo.float()).abs().max()
+    ids_c = torch.zeros(B, dtype=torch.int32, device=DEV)
+    ids_o = torch.zeros(B, dtype=torch.int32, device=DEV)
+    recs = [torch.zeros(record_elems(d, B), dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+    lg_c = torch.zeros(B, d.vocab, dtype=torch.bfloat16, device=DEV)
+    lg_o = torch.zeros(B, d.vocab, dtype=torch.bfloat16, device=DEV)
+    nid_c = torch.zeros(B, dtype=torch.int32, device=DEV)
+    nid_o = torch.zeros(B, dtype=torch.int32, device=DEV)
+    graphs = [DecodeGraph(chain[0], sess, STEPS, ids=ids_c, hidden_out=recs[0]),
+              DecodeGraph(chain[1], sess, STEPS, x=recs[0], hidden_out=recs[1]),
+              DecodeGraph(chain[2], sess, STEPS, x=recs[1], next_ids=nid_c, logits=lg_c)]
+    g1 = DecodeGraph(one, sess, STEPS, ids=ids_o, next_ids=nid_o, logits=lg_o)
+    assert handoff_elems(d, B, 1024) == B * d.hidden + 16 * 1024
+    for k in range(STEPS):
+        ids_c.copy_(forced[k])
+        ids_o.copy_(forced[k])
+        for g in graphs:
+            g.launch()
+        g1.launch()
+        assert torch.equal(lg_c, lg_o), (k, (lg_c.float() - lg_o.float()).abs().max())
+        assert torch.equal(nid_c, nid_o), k
+    for s in chain + [one]:
+        s.check_errors()
+
+
 def test_half_layer_span_rejects_bad_configs():
     """A span with the embedding cannot start at a MLP half, one with lm_head cannot end at an
     attention half, a one-layer span cannot skip both halves, and a layer's absent half has no

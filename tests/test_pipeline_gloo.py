@@ -27,19 +27,29 @@ class OracleExecutor:
         self.device = torch.device("cpu")
         self.has_embed, self.has_lm_head = first_span, last_span
         self.dims = d
+        self.r = r
 
     def _run(self, sessions, n, ids=None, x=None, want_ids=False):
+        """Decode-sized hand-offs across a gate/up boundary are records (h1 first, then the packed
+        SwiGLU product): the oracle reads and writes the h1 part and recomputes the whole MLP."""
         outs = []
+        rows, h = len(sessions) * n, self.dims.hidden
         for i, sid in enumerate(sessions):
             if ids is not None:
                 inp = ids.reshape(len(sessions), n)[i:i + 1].long()
                 o = self.sp.forward_cached(sid, inp)
             else:
-                o = self.sp.forward_cached(sid, x.reshape(len(sessions), n, -1)[i:i + 1])
+                o = self.sp.forward_cached(sid, x.reshape(-1)[:rows * h].reshape(len(sessions), n, -1)[i:i + 1])
             outs.append(o)
         if self.sp.last:
             return torch.stack([torch.argmax(o[0, -1]) for o in outs]).to(torch.int32)
-        return torch.cat([o[0] for o in outs]).to(torch.bfloat16)
+        h1 = torch.cat([o[0] for o in outs]).to(torch.bfloat16)
+        if self.r.last_col and rows <= 64:
+            from inferd_amd.pipeline import record_elems
+            rec = torch.zeros(record_elems(self.dims, rows), dtype=torch.bfloat16)
+            rec[:rows * h] = h1.reshape(-1)
+            return rec
+        return h1
 
     def prefill(self, sessions, n_tokens, ids=None, x=None, want_ids=False):
         return self._run(sessions, n_tokens, ids=ids, x=x)
@@ -51,7 +61,7 @@ class OracleExecutor:
         b = self.bufs[m]
         out = self._run(self.mbs[m], 1, ids=b["ids"], x=b["x"])
         dst = b["next_ids"] if self.sp.last else b["hidden_out"]
-        dst.copy_(out.reshape(dst.shape))
+        dst.reshape(-1)[:out.numel()].copy_(out.reshape(-1))
 
 
 def _free_port():
@@ -65,8 +75,11 @@ def _free_port():
 def _split(d, world, sizes):
     """StageRanges per stage: even (bench.even_split) or the given sizes in layers (BASELINE
     config 4's uneven, balance.py-like split; multiples of 0.5 cut between a layer's attention
-    and MLP halves; bench.py --spans)"""
+    and MLP halves; bench.py --spans), or "gateup": gate/up boundaries inside layers 1 and 2
+    (tiny: intermediate 512, columns 256 and 128)."""
     from inferd_amd.pipeline import StageRange, even_split, ranges_from_sizes
+    if sizes == "gateup":
+        return [StageRange(0, 3, 0, 256), StageRange(3, 2, 256, 128), StageRange(5, 3, 128, 0)][:world]
     if not sizes:
         return [StageRange.layers(f, n) for f, n in even_split(d.layers, world)]
     return ranges_from_sizes(sizes)
@@ -89,8 +102,7 @@ def _worker(rank, world, port, n_steps, q, sizes=None, force=False):
     ex = OracleExecutor(d, rg, rank == 0, rank == world - 1)
     B = 3
     st = PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device="cpu", seed=SEED, n_microbatches=world,
-                       batch=B, max_ctx=64, prefill_chunk=2, executor=ex, skip_first_attn=rg.skip_first_attn,
-                       skip_last_mlp=rg.skip_last_mlp)
+                       batch=B, max_ctx=64, prefill_chunk=2, executor=ex, **rg.span_kwargs())
     g = torch.Generator().manual_seed(3)
     prompts = [torch.randint(0, d.vocab, (B, 9), generator=g) for _ in range(world)]
     st.prefill(prompts)
@@ -143,7 +155,7 @@ def _reference(world, n_steps, sizes=None, force=False):
 
 
 @pytest.mark.parametrize("world,sizes", [(2, None), (3, None), (3, [1, 2, 1]), (2, [3, 1]),
-                                         (2, [1.5, 2.5]), (3, [0.5, 2, 1.5])])
+                                         (2, [1.5, 2.5]), (3, [0.5, 2, 1.5]), (3, "gateup")])
 def test_pipeline_matches_single_process(world, sizes):
     n_steps = 4
     ctx = mp.get_context("spawn")
