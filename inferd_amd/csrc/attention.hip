@@ -57,7 +57,8 @@ __device__ __forceinline__ float exp2_raw(float x) { return __builtin_amdgcn_exp
 // Guideline 16 (write-through form): sc1 partial stores -> every wave s_waitcnt vmcnt(0) ->
 // barrier -> lane 0 relaxed agent fetch_add; the last arriver: agent acquire fence +
 // vmcnt(0) + barrier -> plain loads, all issued in parallel (no load inside a serial loop).
-// Shape (NW, nc): tools/attn_lab.hip sweeps -- few long-running workgroups win; the launcher
+// Shape (NW, nc): the round-3 sweeps (tools/archive/attn_lab_r03.hip, archived: it includes kernels
+// no longer in the tree) -- few long-running workgroups win; the launcher
 // aims at ~2048 waves in total with >= 4 pages per workgroup.
 // Workspace: [DECODE_COUNTER_BYTES of u32 counters | partials, PART_STRIDE f32 per head].
 #define PART_STRIDE (HEAD_DIM + 4)
@@ -227,7 +228,7 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
 }
 
 // (the ATTN_PROBE timing builds -- no q prologue / K fragments as the P*V operand -- live in
-// the round-2 tree, git 6a90f3d, with tools/attn_lab.hip)
+// the round-2 tree, git 6a90f3d, with tools/archive/attn_lab_r03.hip)
 
 template <int NW, bool FUSED>
 __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16* __restrict__ kv, const AttnBatch& b,
@@ -590,8 +591,8 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_kernel(const u16* __restr
                               blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-// (waves per workgroup, chunks per (seq, kv head)) for a decode batch (tools/attn_shape_sweep.sh
-// measured the alternatives with lab builds)
+// (waves per workgroup, chunks per (seq, kv head)) for a decode batch (the round-3 shape sweep measured
+// the alternatives with lab builds)
 static void decode_shape(int B, int KV, int max_ctx, int* nw, int* nc) {
   const int np = (max_ctx + KV_PAGE - 1) / KV_PAGE;
   const int S = B * KV;

@@ -1010,6 +1010,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(
     __syncthreads();
     const unsigned ticket = ticket_lds[0];
     if (ticket + 1 < (unsigned)nsl) {
+      // Hand-off form (MI355X_MICROARCH.md, "Valid forms besides Guideline 16's R1/R2", the
+      // producer's write-through variant): every partial is an sc1 (write-through) store, every
+      // storing wave waits vmcnt(0), a barrier, then a relaxed agent-scope add; the combiner
+      // polls relaxed, then one agent acquire fence before its loads.  A C++ __ATOMIC_RELEASE add
+      // would compile to an extra buffer_wbl2 sc1 (~1.7 us, nothing is dirty: the stores are
+      // write-through) and an __ATOMIC_ACQUIRE poll to a buffer_inv per iteration on gfx950 (hipcc
+      // -S, round 5), so the guide's form is kept; the inline-asm wait is not visible to the
+      // compiler's waitcnt pass, so nothing can drop it (the guide's "Compiler hazard").
       split_publish(acc, part, slice);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();

@@ -48,6 +48,32 @@ for tick in range(3):
     del send
     torch.cuda.synchronize()
     ok &= torch.equal(recv, ref) and st._inflight is not None
+# prefill ticks with NO synchronisation in between (ADVICE r04): each tick's send tensor is freed
+# right after its exchange and a same-size tensor is allocated and overwritten at once -- the
+# caching allocator may hand it the freed block; the one-tick lifetime (_inflight) and the
+# stream wait must keep the in-flight send intact.  One synchronisation at the end.
+refs, recvs = [], []
+for tick in range(4):
+    send = torch.randn(2 * 2048, 4096, device=dev, generator=g).to(torch.bfloat16)
+    refs.append(send.clone())
+    recvs.append(torch.empty_like(send))
+    PipelineStage._exchange(st, send, 0, recvs[-1], 0)
+    del send
+    junk = torch.empty(2 * 2048, 4096, device=dev, dtype=torch.bfloat16)
+    junk.fill_(7.0)
+    del junk
+torch.cuda.synchronize()
+ok &= all(torch.equal(a, b) for a, b in zip(recvs, refs))
+# a gate/up-boundary record: only its head travels (pipeline.handoff_elems), as a view
+from inferd_amd.pipeline import handoff_elems, record_elems
+from inferd_amd.runtime import MODELS
+d = MODELS["qwen3-8b"]
+rec_out = torch.randn(record_elems(d, 16), device=dev, generator=g).to(torch.bfloat16)
+rec_in = torch.zeros_like(rec_out)
+n = handoff_elems(d, 16, 4096)
+PipelineStage._exchange(st, rec_out[:n], 0, rec_in[:n], 0)
+torch.cuda.synchronize()
+ok &= torch.equal(rec_in[:n], rec_out[:n]) and int(rec_in[n:].abs().sum()) == 0
 dist.destroy_process_group()
 print("RCCL_EXCHANGE_OK" if ok else "RCCL_EXCHANGE_MISMATCH", flush=True)
 '''

@@ -1,3 +1,6 @@
+// ARCHIVED (round 5): this lab no longer builds against the tree -- it includes
+// ../inferd_amd/csrc/attn_prefill.hip and calls launch_attn_decode_shape, both removed in round 4.
+// Kept as the record of the round-3 decode-attention shape sweeps.
 // Decode-attention design lab: the engine's kernel (attention.hip, included) at its default
 // shape and every (waves per workgroup, chunks) shape, on B sequences x ctx tokens x KV heads
 // with the paged KV pool rotated over > 1 GB (no Infinity-Cache reuse across launches, as in
