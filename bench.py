@@ -37,7 +37,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-from inferd_amd.pipeline import balanced_split, even_split, record_elems  # noqa: E402  (host logic only)
+from inferd_amd.pipeline import balanced_split, buffer_elems, even_split  # noqa: E402  (host logic only)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_BF16_PEAK_TFLOPS = 2500.0
@@ -116,12 +116,13 @@ def parse():
                                                 "balance.py-like split, e.g. 5,27,4; multiples of 0.5 cut between a "
                                                 "layer's attention and MLP halves, e.g. 4.5,4.5,5,...); overrides "
                                                 "--split")
-    p.add_argument("--split", choices=("balanced", "even", "halves", "gateup"), default="even",
+    p.add_argument("--split", choices=("balanced", "even", "halves", "gateup", "sublayer"), default="even",
                    help="stage layer counts: even = counts differing by at most one (BASELINE config 3, the "
                         "default), balanced = min-max of per-stage decode bytes (lm_head priced on the last stage), "
                         "halves = min-max of per-stage decode time with cuts between a layer's attention and MLP "
                         "halves allowed (pipeline.halves_split), gateup = the same with boundaries inside a layer's "
-                        "gate/up projection too (pipeline.gateup_split)")
+                        "gate/up projection too (pipeline.gateup_split), sublayer = also between a layer's "
+                        "attention and its o projection (pipeline.sublayer_split)")
     p.add_argument("--mode", choices=("decode", "prefill", "stages"), default="decode",
                    help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline); "
                         "stages: the per-stage decode projection of the 2/4/8-GPU splits on one GPU")
@@ -259,6 +260,12 @@ def range_bytes(d, r, B: int, ctx_mean: float, lm_head: bool) -> float:
     gu_w = kb["gateup_gemm"] - B * d.intermediate * 2
     nb -= gu_w * r.first_col / d.intermediate
     nb += gu_w * r.last_col / d.intermediate
+    # attention|o boundaries (StageRange.first_o / last_o): the shared attention unit's o GEMV
+    # runs in the stage after the cut, the rest of it (norm, q/k/v, attention) in the one before
+    if r.first_o:
+        nb -= attn - kb["o_gemm"]
+    if r.last_o:
+        nb -= kb["o_gemm"]
     return nb
 
 
@@ -292,16 +299,18 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
                 if first:
                     ids = torch.randint(0, d.vocab, (len(reqs) * ctx,), generator=g, dtype=torch.int32)
                     span.forward(reqs, ids=ids, want_hidden=False, want_next_ids=last)
-                else:
-                    x = (torch.randn(len(reqs) * ctx, d.hidden, generator=g) * 0.5).to(torch.bfloat16)
-                    span.forward(reqs, x=x, want_hidden=False, want_next_ids=last)
+                else:     # (a record x | attention output at an attention|o boundary)
+                    n_in = buffer_elems(d, len(reqs) * ctx, 0, r.first_o, False)
+                    x = (torch.randn(n_in, generator=g) * 0.5).to(torch.bfloat16)
+                    span.forward(reqs, x=x, want_hidden=r.last_o, want_next_ids=last)
             ids = torch.zeros(B, dtype=torch.int32, device=dev) if first else None
             x = None if first else (torch.randn(B, d.hidden, generator=g) * 0.5).to(torch.bfloat16).to(dev)
-            if r.first_col:      # a gate/up-boundary record: h1, then the packed act
-                x = torch.cat([x.reshape(-1), torch.zeros(record_elems(d, B) - B * d.hidden, dtype=torch.bfloat16,
-                                                          device=dev)])
-            hout = None if last else torch.empty(record_elems(d, B) if r.last_col else B * d.hidden,
-                                                 dtype=torch.bfloat16, device=dev)
+            if r.first_col or r.first_o:      # a record: h1 + the packed act, or x + the attention output
+                n_in = buffer_elems(d, B, r.first_col, r.first_o)
+                x = torch.cat([x.reshape(-1), (torch.randn(n_in - B * d.hidden, generator=g) * 0.5 if r.first_o else
+                                               torch.zeros(n_in - B * d.hidden)).to(torch.bfloat16).to(dev)])
+            hout = None if last else torch.empty(buffer_elems(d, B, r.last_col, r.last_o), dtype=torch.bfloat16,
+                                                 device=dev)
             nid = torch.empty(B, dtype=torch.int32, device=dev) if last else None
             graph = DecodeGraph(span, sess, warmup + reps, ids=ids, x=x, hidden_out=hout, next_ids=nid)
             for _ in range(warmup):
@@ -333,7 +342,7 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
 def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
     """The splits stage_projection measures: BASELINE config 3's even splits, the layer-granular
     byte-balanced split and the half-layer time-balanced split at each stage count."""
-    from inferd_amd.pipeline import StageRange, gateup_split, halves_split
+    from inferd_amd.pipeline import StageRange, gateup_split, halves_split, sublayer_split
     out = {}
     for n in sizes:
         if n > d.layers:
@@ -342,7 +351,8 @@ def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
         bal = [StageRange.layers(f, k) for f, k in stage_split(d, n, B, ctx, "balanced")]
         if bal != out[f"even{n}"]:
             out[f"balanced{n}"] = bal
-        for name, sp in (("halves", halves_split(d.layers, n)), ("gateup", gateup_split(d.layers, n, d.intermediate))):
+        for name, sp in (("halves", halves_split(d.layers, n)), ("gateup", gateup_split(d.layers, n, d.intermediate)),
+                         ("sublayer", sublayer_split(d.layers, n, d.intermediate))):
             if all(sp != v for v in out.values()):
                 out[f"{name}{n}"] = sp
     return out
@@ -498,6 +508,8 @@ def main():
         ranges = P.halves_split(d.layers, world)
     elif args.split == "gateup":
         ranges = P.gateup_split(d.layers, world, d.intermediate)
+    elif args.split == "sublayer":
+        ranges = P.sublayer_split(d.layers, world, d.intermediate)
     else:
         ranges = [P.StageRange.layers(f, k) for f, k in stage_split(d, world, B, ctx, args.split)]
     rg = ranges[rank]
@@ -593,7 +605,9 @@ def main():
             "config": {"workload": f"{args.model} greedy decode, batch {B} per microbatch at {ctx} context "
                                    f"(prefilled), {n_mb} microbatch(es) in flight",
                        "global_batch": B * n_mb, "seq_len": ctx, "parallelism": f"pp{world}",
-                       "spans": [r.n_units / 2 + (r.last_col - r.first_col) / d.intermediate / 2 for r in ranges],
+                       # layers per stage (a shared attention unit counts a quarter layer on each side)
+                       "spans": [r.n_units / 2 + (r.last_col - r.first_col) / d.intermediate / 2 -
+                                 0.25 * (r.first_o + r.last_o) for r in ranges],
                        "stage_ranges": [r.label() for r in ranges]},
             "roofline": roof,
             "roofline_step": {"bound": "hbm", "alg_bytes_per_step": int(sb),

@@ -82,6 +82,14 @@ typedef struct InferdSpanConfig {
    * multiple of 128 below intermediate. */
   int32_t gateup_split_first; /* with skip_first_attn: columns [0, c) arrive in x_in's record */
   int32_t gateup_split_last;  /* with skip_last_mlp: columns [0, c) are computed into x_out's record */
+  /* A boundary between a layer's attention kernel and its o projection: the span before it
+   * runs input_layernorm, q/k/v and the attention of that layer (its K/V pages live there),
+   * the span after it starts with o_proj + residual.  The hand-off is a RECORD: the layer's
+   * input residual x bf16 [n_tokens][hidden] row-major, followed by the attention output bf16
+   * [rows][heads * 128] -- fragment-packed over ceil(n_tokens/16)*16 rows in a pure decode call
+   * (every sequence one new token), row-major over n_tokens rows otherwise.  0 or 1. */
+  int32_t o_split_first; /* the span starts at its first layer's o projection (x_in: the record) */
+  int32_t o_split_last;  /* the span ends before its last layer's o projection (x_out: the record) */
 } InferdSpanConfig;
 
 /* One forward call's batch: n_seqs sequences, their new tokens concatenated

@@ -30,7 +30,8 @@ class SpanConfig(C.Structure):
                                      "first_layer", "n_layers", "has_embed", "has_lm_head")] + \
                [("rms_eps", c_f), ("rope_theta", c_f)] + \
                [(n, c_i32) for n in ("max_positions", "kv_pages", "max_tokens", "max_seqs", "skip_first_attn",
-                                     "skip_last_mlp", "gateup_split_first", "gateup_split_last")]
+                                     "skip_last_mlp", "gateup_split_first", "gateup_split_last", "o_split_first",
+                                     "o_split_last")]
 
 
 class Batch(C.Structure):

@@ -102,6 +102,26 @@ __device__ __forceinline__ void decode_advance_one(int32_t* positions, int32_t* 
   }
 }
 
+// A decode step's prologue where the span's first launch is not an RMSNorm (a span starting at
+// an o projection): workgroup 0 runs the graph's scheduler step (NormPrologue positions), and
+// workgroup r < M zeroes row r's words of the SSQ slots the span's decode GEMVs will fill.
+__global__ __launch_bounds__(64) void step_prologue_kernel(unsigned long long* __restrict__ zero_slots,
+                                                           int n_slots, NormPrologue pro) {
+  const int row = blockIdx.x;
+  if (pro.positions && row == 0)
+    for (int b = threadIdx.x; b < pro.B; b += 64) decode_advance_one(pro.positions, pro.slots, pro.ctx_lens,
+                                                                      pro.block_table, pro.max_pages, b, pro.err);
+  for (int i = threadIdx.x; i < n_slots * SSQ_SHARDS * 2; i += 64) zero_slots[(int64_t)i * 64 + row] = 0ull;
+}
+
+void launch_step_prologue(unsigned long long* zero_slots, int n_slots, int M, const NormPrologue* pro_in,
+                          hipStream_t s) {
+  if (!zero_slots || M > 64) n_slots = 0;
+  const NormPrologue pro = pro_in ? *pro_in : NormPrologue{};
+  hipLaunchKernelGGL(step_prologue_kernel, dim3(M < 1 ? 1 : (M > 64 ? 1 : M)), dim3(64), 0, s, zero_slots, n_slots,
+                     pro);
+}
+
 // ------------------------------------------------------------------ RMSNorm
 // y = w * bf16(x * 1/sqrt(mean(x^2) + eps))     (qwen3_server_module.py:19-25)
 // One 256-thread block per row; each thread keeps <= CH 8-element chunks in registers.

@@ -52,6 +52,10 @@ struct NormPrologue {
   const int32_t* block_table = nullptr;
   int max_pages = 0, B = 0;
 };
+// the same prologue work (scheduler step, SSQ slot zeroing for rows < M <= 64) as a launch of its
+// own, for a span whose first launch is not an RMSNorm
+void launch_step_prologue(unsigned long long* zero_slots, int n_slots, int M, const NormPrologue* pro,
+                          hipStream_t s);
 // zero_slots: rows < M of n_slots SSQ slots (kernels.h DecodeNorm) are zeroed too, or null
 void launch_rmsnorm(const u16* x, int64_t ldx, const int32_t* row_index, int row_sub, const u16* w,
                     u16* y, int64_t ldy, int M, int N, float eps, hipStream_t s, bool pack_out = false,

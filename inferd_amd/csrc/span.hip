@@ -150,12 +150,15 @@ struct InferdSpan {
   int qkv_rows() const { return (cfg.heads + 2 * cfg.kv_heads) * HEAD_DIM; }
   // the halves of span-local layer l this span runs (InferdSpanConfig skip_first_attn /
   // skip_last_mlp); only layers with an attention half own a KV pool layer
-  bool has_attn(int l) const { return !(l == 0 && cfg.skip_first_attn); }
-  bool has_mlp(int l) const { return !(l == cfg.n_layers - 1 && cfg.skip_last_mlp); }
+  // has_attn: input_layernorm, q/k/v and the attention kernel; has_o: o_proj + residual
+  bool first_no_attn() const { return cfg.skip_first_attn || cfg.o_split_first; }
+  bool has_attn(int l) const { return !(l == 0 && first_no_attn()); }
+  bool has_o(int l) const { return !(l == 0 && cfg.skip_first_attn) && !(l == cfg.n_layers - 1 && cfg.o_split_last); }
+  bool has_mlp(int l) const { return !(l == cfg.n_layers - 1 && (cfg.skip_last_mlp || cfg.o_split_last)); }
   // the last layer of a span that ends inside the layer's gate/up projection computes part of it
   bool has_gateup(int l) const { return has_mlp(l) || (l == cfg.n_layers - 1 && cfg.gateup_split_last); }
-  int kv_layers() const { return cfg.n_layers - (cfg.skip_first_attn ? 1 : 0); }
-  u16* kv_of(int l) const { return kv_pool + kv_layer_elems * (l - (cfg.skip_first_attn ? 1 : 0)); }
+  int kv_layers() const { return cfg.n_layers - (first_no_attn() ? 1 : 0); }
+  u16* kv_of(int l) const { return kv_pool + kv_layer_elems * (l - (first_no_attn() ? 1 : 0)); }
 };
 
 #define ALLOC(ptr, bytes)                                   \
@@ -192,6 +195,15 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
       return fail(INFERD_ERR_ARG, "gate/up split columns: 0, or a multiple of 128 below intermediate");
   if ((c.gateup_split_first && !c.skip_first_attn) || (c.gateup_split_last && !c.skip_last_mlp))
     return fail(INFERD_ERR_ARG, "a gate/up split refines a half-layer boundary (skip_first_attn / skip_last_mlp)");
+  if ((c.o_split_first | c.o_split_last) & ~1) return fail(INFERD_ERR_ARG, "o_split_first / o_split_last are 0 or 1");
+  if ((c.o_split_first && (c.skip_first_attn || c.has_embed)) || (c.o_split_last && (c.skip_last_mlp || c.has_lm_head)))
+    return fail(INFERD_ERR_ARG, "an attention|o boundary excludes a half-layer boundary at the same end, the "
+                                "embedding (first) and lm_head (last)");
+  if ((c.o_split_first || c.o_split_last) && c.n_layers < 1)
+    return fail(INFERD_ERR_ARG, "an attention|o boundary needs n_layers >= 1");
+  if (c.n_layers == 1 && ((c.o_split_first && (c.o_split_last || c.skip_last_mlp)) ||
+                          (c.o_split_last && c.skip_first_attn)))
+    return fail(INFERD_ERR_ARG, "a one-layer span cannot end before the part it starts at");
   InferdSpan* s = new InferdSpan();
   s->cfg = c;
   const int h = c.hidden, I = c.intermediate, H = c.heads, KV = c.kv_heads;
@@ -210,11 +222,11 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
     LayerW& L = s->layers[l];
     if (s->has_attn(l)) {
       SALLOC(L.qkv, (size_t)s->qkv_rows() * h * 2);
-      SALLOC(L.o, (size_t)h * H * HEAD_DIM * 2);
       SALLOC(L.in_ln, (size_t)h * 2);
       SALLOC(L.q_norm, HEAD_DIM * 2);
       SALLOC(L.k_norm, HEAD_DIM * 2);
     }
+    if (s->has_o(l)) SALLOC(L.o, (size_t)h * H * HEAD_DIM * 2);
     if (s->has_gateup(l)) {  // a gate/up boundary's sender owns gate/up too
       SALLOC(L.gateup, (size_t)2 * I * h * 2);
       SALLOC(L.post_ln, (size_t)h * 2);
@@ -309,7 +321,7 @@ int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
   if (resolve_layer(s, layer, name, t)) return INFERD_ERR_ARG;
   if (!t->dst)
     return fail(INFERD_ERR_ARG, std::string(name) + ": layer " + std::to_string(layer) +
-                                    " of this span runs only its other half (skip_first_attn / skip_last_mlp)");
+                                    " of this span runs only its other half / part (skip_first_attn, skip_last_mlp, o_split_*)");
   return 0;
 }
 
@@ -335,6 +347,7 @@ int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t) {
 // 1 if span-local layer `layer` runs the half that weight `name` belongs to
 bool owns_weight(const InferdSpan* s, int layer, const char* name) {
   if (!strcmp(name, "down_proj")) return s->has_mlp(layer);
+  if (!strcmp(name, "o_proj")) return s->has_o(layer);
   if (!strcmp(name, "gate_proj") || !strcmp(name, "up_proj") || !strcmp(name, "post_attention_layernorm"))
     return s->has_gateup(layer);
   return s->has_attn(layer);
@@ -455,6 +468,8 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   }
   if (M <= 64 && c.gateup_split_first && !x_in)
     return fail(INFERD_ERR_ARG, "a span starting inside a gate/up projection needs x_in (the hand-off record)");
+  if (c.o_split_last && !x_out)
+    return fail(INFERD_ERR_ARG, "a span ending before an o projection needs x_out (the hand-off record)");
   if (c.has_embed) {
     if (!ids) return fail(INFERD_ERR_ARG, "first span needs token ids");
     if (c.n_layers > 0) {
@@ -485,12 +500,27 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   const bool pkx = gemv && !layer_out && h % 128 == 0 && I % 128 == 0;
   bool x_packed = false;  // x (this layer's input) is fragment-packed
   long pe = -1;
+  // decode: the attention output goes to the o projection's GEMV fragment-packed (also the
+  // layout of an attention|o boundary record's second part)
+  const bool pk_o = b->decode && gemv && !gemm_uses_tiled(M, h, H * HEAD_DIM, EPI_RESID);
+  if (c.o_split_first && c.n_layers > 0 && (gemv || pro.positions)) {
+    // a span starting at an o projection has no first RMSNorm launch to carry the graph's
+    // scheduler step and the SSQ slot zeroing: a small launch of its own
+    launch_step_prologue(gemv ? s->ssq : nullptr, 2 * c.n_layers, M, &pro, st);
+    pro = NormPrologue{};
+  }
   for (int l = 0; l < c.n_layers; ++l) {
     const LayerW& W = s->layers[l];
-    // the residual written by this layer's last half: x_out after the span's last layer
+    // the residual written by this layer's last half: x_out after the span's last layer, and
+    // (row-major) the input of a last layer that ends before its o projection -- the first part
+    // of the hand-off record
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
-    const bool out_packed = pkx && l < c.n_layers - 1;
-    if (!s->has_attn(l)) {
+    bool out_packed = pkx && l < c.n_layers - 1;
+    if (c.o_split_last && l == c.n_layers - 2) {
+      out = (u16*)x_out;
+      out_packed = false;
+    }
+    if (l == 0 && c.skip_first_attn) {
       // ---- a span starting at this layer's MLP half: x is h1 (row-major, the caller's), so
       // post_attention_layernorm runs as the span's first RMSNorm launch (slot zeroing and
       // the graph prologue included, like layer 0's input norm)
@@ -523,9 +553,21 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
       LAUNCH_CHECK();
       continue;
     }
+    // the attention output the o projection reads: this layer's, or (a span starting at an o
+    // projection) the record's second part
+    const u16* attn_src = s->attn;
+    if (!s->has_attn(l)) {  // o_split_first, layer 0: x is the record's residual part
+      attn_src = (const u16*)x_in + (size_t)M * h;
+      goto o_proj;
+    }
+    {
     u16* kv_l = s->kv_of(l);
     // decode: QK-norm + RoPE + the cache write run inside the attention
     const bool fused = b->decode;
+    // a span ending before this layer's o projection: the attention writes the record's second
+    // part, behind the layer's input residual (row-major; copied there when it is the span's input)
+    u16* attn_dst = s->attn;
+    if (!s->has_o(l)) attn_dst = (u16*)x_out + (size_t)M * h;
     // decode q/k/v K-slices (reduced inside the fused attention): M <= 16 and K/32 divisible
     // by 4 * slices
     int ksl = (fused && M <= 16) ? QKV_KSL : 1;
@@ -560,16 +602,14 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
                     nullptr, (x_packed && a_in == x) ? GEMM_PACK_A : 0));
     }
     s->prof_end(pe, st);
-    // decode: the attention output goes to the o projection's GEMV fragment-packed
-    const bool pk_o = fused && gemv && !gemm_uses_tiled(M, h, H * HEAD_DIM, EPI_RESID);
     if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
       if (ksl > 1)
         launch_attn_decode_fused(nullptr, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
-                                 scale, s->attn, s->attn_ws, st, s->qkv_part, ksl, pk_o);
+                                 scale, attn_dst, s->attn_ws, st, s->qkv_part, ksl, pk_o);
       else
         launch_attn_decode_fused(s->qkv, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
-                                 scale, s->attn, s->attn_ws, st, nullptr, 0, pk_o);
+                                 scale, attn_dst, s->attn_ws, st, nullptr, 0, pk_o);
       s->prof_end(pe, st);
     } else {
       if (!qkv_done) {
@@ -579,9 +619,17 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
         s->prof_end(pe, st);
       }
       pe = s->prof_begin(PROF_ATTN, st);
-      launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, s->attn, st);
+      launch_attn_prefill(s->q, kv_l, ab, H, KV, scale, attn_dst, st);
       s->prof_end(pe, st);
     }
+    if (!s->has_o(l)) {  // the record: x (first part; the span's input copied there), attention output
+      if (c.n_layers == 1 && x != (const u16*)x_out)
+        HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
+      LAUNCH_CHECK();
+      continue;
+    }
+    }
+  o_proj:
     // ---- h1 = x + o_proj(attn)   (in place when x == s->h: same-element read-then-write)
     // h1 is packed iff pkx.  An in-place epilogue needs one layout on both sides, so h1 goes
     // to s->xn (free after the q/k/v projection) where s->h holds a row-major x (the first
@@ -599,7 +647,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
         return fail(INFERD_ERR_ARG, "a span ending inside a gate/up projection needs x_out (the hand-off record)");
     }
     pe = s->prof_begin(PROF_O, st);
-    GEMM_TRY(launch_gemm(s->attn, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
+    GEMM_TRY(launch_gemm(attn_src, H * HEAD_DIM, W.o, M, h, H * HEAD_DIM, h1, h, x, h, EPI_RESID, nullptr, st, &s->gws, nullptr,
                 gemv ? slot(2 * l) : nullptr,
                 (pk_o ? GEMM_PACK_A : 0) | (x_packed ? GEMM_PACK_R : 0) | (h1_packed ? GEMM_PACK_C : 0)));
     s->prof_end(pe, st);

@@ -41,14 +41,50 @@ def record_elems(dims, rows: int) -> int:
     return rows * dims.hidden + (rows + 15) // 16 * 16 * dims.intermediate
 
 
-def handoff_elems(dims, rows: int, col: int) -> int:
-    """Elements of a decode hand-off that carry data: h1 alone (col = 0, a layer or half-layer
-    boundary), else h1 plus the act columns [0, col) -- for <= 16 rows those are one contiguous
-    prefix of the packed act (a 16-row tile's columns [0, col) are its first 16 * col elements),
-    for more rows the whole record."""
-    if not col:
+def handoff_elems(dims, rows: int, col: int, o: bool = False, packed: bool = True) -> int:
+    """Elements of a hand-off that carry data: at an attention|o boundary (o) the whole record
+    (o_record_elems; packed: a pure decode call); else h1 alone (col = 0, a layer or half-layer
+    boundary, or a call of more than 64 rows), else h1 plus the act columns [0, col) -- for <= 16
+    rows those are one contiguous prefix of the packed act (a 16-row tile's columns [0, col) are
+    its first 16 * col elements), for more rows the whole record."""
+    if o:
+        return o_record_elems(dims, rows, packed)
+    if not col or rows > 64:
         return rows * dims.hidden
     return rows * dims.hidden + 16 * col if rows <= 16 else record_elems(dims, rows)
+
+
+def buffer_elems(dims, rows: int, col: int, o: bool = False, packed: bool = True) -> int:
+    """Elements of the buffer a stage boundary's hand-off lands in (the whole record, of which
+    handoff_elems carries data; rows * hidden at a layer or half-layer boundary)."""
+    if o:
+        return o_record_elems(dims, rows, packed)
+    return record_elems(dims, rows) if col and rows <= 64 else rows * dims.hidden
+
+
+def o_record_elems(dims, rows: int, packed: bool) -> int:
+    """bf16 elements of an attention|o-boundary hand-off record of `rows` token rows: the layer's
+    input residual x [rows][hidden], then the attention output [rows, or rows rounded to 16 when
+    fragment-packed (a pure decode call)][heads * head_dim] (InferdSpanConfig o_split_*)."""
+    return rows * dims.hidden + ((rows + 15) // 16 * 16 if packed else rows) * dims.heads * dims.head_dim
+
+
+def pack_rows(t: torch.Tensor) -> torch.Tensor:
+    """[rows, K] -> the fragment-packed layout of decode hand-offs (common.h packed_index: the
+    16-row, 32-column tile (mt, kt) is 512 elements at (mt * K/32 + kt) * 512, element (r, c) of it
+    at (c % 32 // 8) * 128 + r * 8 + c % 8), rows zero-padded to a multiple of 16.  Host side of
+    the records' packed parts, for tests and CPU executors."""
+    rows, K = t.shape
+    R = (rows + 15) // 16 * 16
+    p = torch.zeros(R, K, dtype=t.dtype, device=t.device)
+    p[:rows] = t
+    return p.view(R // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1)
+
+
+def unpack_rows(flat: torch.Tensor, rows: int, K: int) -> torch.Tensor:
+    """Inverse of pack_rows: the first `rows` rows [rows, K]."""
+    R = (rows + 15) // 16 * 16
+    return flat[:R * K].view(R // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(R, K)[:rows]
 
 
 def even_split(n_layers: int, n: int):
@@ -102,15 +138,25 @@ class StageRange:
     first_col / last_col refine a half boundary into the layer's gate/up projection (decode
     calls; InferdSpanConfig gateup_split_*): the stage before it also computes gate/up columns
     [0, col), the stage after it the rest and the down projection, and the hand-off is h1 plus
-    the packed SwiGLU product (a record)."""
-    __slots__ = ("first_unit", "n_units", "first_col", "last_col")
+    the packed SwiGLU product (a record).
+    first_o / last_o: a boundary between layer l's attention and its o projection
+    (InferdSpanConfig o_split_*): unit 2l then belongs to both stages -- the one before runs its
+    norm, q/k/v and attention (its K/V live there), the one after its o projection -- and the
+    hand-off is the record (x, attention output).  A first_o stage starts at unit 2l, a last_o
+    stage ends after unit 2l."""
+    __slots__ = ("first_unit", "n_units", "first_col", "last_col", "first_o", "last_o")
 
-    def __init__(self, first_unit: int, n_units: int, first_col: int = 0, last_col: int = 0):
+    def __init__(self, first_unit: int, n_units: int, first_col: int = 0, last_col: int = 0,
+                 first_o: bool = False, last_o: bool = False):
         assert first_unit >= 0 and n_units >= 1
         self.first_unit, self.n_units = first_unit, n_units
         self.first_col, self.last_col = first_col, last_col
+        self.first_o, self.last_o = bool(first_o), bool(last_o)
         assert not first_col or self.skip_first_attn, "first_col refines a stage that starts at an MLP half"
         assert not last_col or self.skip_last_mlp, "last_col refines a stage that ends after an attention half"
+        assert not first_o or first_unit % 2 == 0, "first_o: the stage starts in an attention unit"
+        assert not last_o or (first_unit + n_units) % 2 == 1, "last_o: the stage ends in an attention unit"
+        assert not (first_o and last_o and n_units == 1), "a stage of one attention unit's o alone and its core"
 
     @classmethod
     def layers(cls, first_layer: int, n_layers: int) -> "StageRange":
@@ -120,26 +166,34 @@ class StageRange:
     last_layer = property(lambda self: (self.first_unit + self.n_units - 1) // 2)
     n_layers = property(lambda self: self.last_layer - self.first_layer + 1)
     skip_first_attn = property(lambda self: self.first_unit % 2 == 1)
-    skip_last_mlp = property(lambda self: (self.first_unit + self.n_units) % 2 == 1)
+    skip_last_mlp = property(lambda self: (self.first_unit + self.n_units) % 2 == 1 and not self.last_o)
+    # the next stage's first_unit (a last_o stage shares its last unit with the next stage)
+    end_unit = property(lambda self: self.first_unit + self.n_units - (1 if self.last_o else 0))
 
     def label(self) -> str:
         """e.g. '4m..8' = layer 4's MLP half through layer 8; '9..13a' ends with 13's attention
-        half; '13m@6144..' / '..13a+6144': a gate/up boundary at column 6144 of layer 13"""
-        a = f"{self.first_layer}{'m' if self.skip_first_attn else ''}{f'@{self.first_col}' if self.first_col else ''}"
-        b = f"{self.last_layer}{'a' if self.skip_last_mlp else ''}{f'+{self.last_col}' if self.last_col else ''}"
+        half; '13m@6144..' / '..13a+6144': a gate/up boundary at column 6144 of layer 13;
+        '13o..' / '..13q': an attention|o boundary in layer 13"""
+        a = (f"{self.first_layer}{'m' if self.skip_first_attn else ''}{'o' if self.first_o else ''}"
+             f"{f'@{self.first_col}' if self.first_col else ''}")
+        b = (f"{self.last_layer}{'a' if self.skip_last_mlp else ''}{'q' if self.last_o else ''}"
+             f"{f'+{self.last_col}' if self.last_col else ''}")
         return f"{a}..{b}"
 
     def span_kwargs(self) -> dict:
         """The SpanRuntime / PipelineStage keyword arguments of this range's boundaries."""
         return {"skip_first_attn": self.skip_first_attn, "skip_last_mlp": self.skip_last_mlp,
-                "gateup_split_first": self.first_col, "gateup_split_last": self.last_col}
+                "gateup_split_first": self.first_col, "gateup_split_last": self.last_col,
+                "o_split_first": self.first_o, "o_split_last": self.last_o}
+
+    def _key(self):
+        return (self.first_unit, self.n_units, self.first_col, self.last_col, self.first_o, self.last_o)
 
     def __eq__(self, o):
-        return isinstance(o, StageRange) and (o.first_unit, o.n_units, o.first_col, o.last_col) == \
-            (self.first_unit, self.n_units, self.first_col, self.last_col)
+        return isinstance(o, StageRange) and o._key() == self._key()
 
     def __repr__(self):
-        return f"StageRange({self.first_unit}, {self.n_units}, {self.first_col}, {self.last_col})"
+        return "StageRange({}, {}, {}, {}, {}, {})".format(*self._key())
 
 
 def ranges_from_sizes(sizes) -> list:
@@ -205,38 +259,47 @@ DECODE_US_8B_GATEUP = 33.57
 # algorithmic decode bytes per unit at Qwen3-8B, B = 16, ctx 2k (bench.py kernel_bytes), MB: the
 # attention half (norm, q/k/v, attention, o), the gate/up projection, the down projection, the
 # last stage's final norm + lm_head
-DECODE_MB_8B = {"attn_half": 221.6, "gateup": 202.2, "down": 101.6, "head": 1245.0}
+DECODE_MB_8B = {"attn_half": 221.6, "gateup": 202.2, "down": 101.6, "head": 1245.0, "o": 33.9}
+# the o GEMV's share of the attention half (profiles/r04/decode_kernel_trace.json), us
+DECODE_US_8B_O = 8.73
 
 
 def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_US_8B, step: int = 256,
-                 gateup_us: float = DECODE_US_8B_GATEUP, mb: dict = DECODE_MB_8B):
+                 gateup_us: float = DECODE_US_8B_GATEUP, mb: dict = DECODE_MB_8B, o_cuts: bool = False,
+                 o_us: float = DECODE_US_8B_O):
     """Stages cut anywhere in the layer timeline a boundary may sit -- a layer start, or inside
     a layer's MLP before gate/up column c (c = 0: the half boundary; 0 < c < intermediate, a
-    multiple of `step`: a gate/up boundary) -- so that the lowest stage's HBM fraction at the
-    pipeline's tick, min_s bytes_s / max_s time_s, is the highest the time / byte model allows
-    (an exact search: for a tick bound T the best split is a DP over the cut points; T on a
-    4-us grid from the ideal total / n, then refined to 0.5 us).  Time model: costs
-    (DECODE_US_8B) with the MLP half split into gate/up (gateup_us, linear in the columns) and
-    down; bytes: mb.  Boundaries cannot sit inside an attention half (its K/V live where it
-    runs), so stage boundaries that fall there move to the nearest MLP."""
+    multiple of `step`: a gate/up boundary), and with o_cuts also between a layer's attention
+    and its o projection -- so that the lowest stage's HBM fraction at the pipeline's tick,
+    min_s bytes_s / max_s time_s, is the highest the time / byte model allows (an exact search:
+    for a tick bound T the best split is a DP over the cut points; T on a 4-us grid from the
+    ideal total / n, then refined to 0.5 us).  Time model: costs (DECODE_US_8B) with the MLP
+    half split into gate/up (gateup_us, linear in the columns) and down, and the attention half
+    into its core and the o GEMV (o_us); bytes: mb.  Boundaries cannot sit inside the attention
+    itself (its K/V live where it runs)."""
     a, mlp, hd, sn = costs["attn_half"], costs["mlp_half"], costs["head"], costs["stage_norm"]
     ncol = intermediate // step
-    # cut points in timeline order: (layer, col) with col = -1 (layer start) or 0 .. ncol-1
-    # (inside the MLP before gate/up column col * step); time and bytes up to each cut
+    # cut points in timeline order: (layer, kind, col) -- kind "L" a layer start, "O" before the
+    # layer's o projection, "G" inside its MLP before gate/up column col * step; time and bytes
+    # up to each cut
     cuts, times, byts, t, y = [], [], [], 0.0, 0.0
     for l in range(n_layers):
-        cuts.append((l, -1))
+        cuts.append((l, "L", 0))
         times.append(t)
         byts.append(y)
+        if o_cuts:
+            cuts.append((l, "O", 0))
+            times.append(t + a - o_us)
+            byts.append(y + mb["attn_half"] - mb["o"])
         t += a
         y += mb["attn_half"]
         for k in range(ncol):
-            cuts.append((l, k))
+            cuts.append((l, "G", k))
             times.append(t + gateup_us * k / ncol)
             byts.append(y + mb["gateup"] * k / ncol)
         t += mlp
         y += mb["gateup"] + mb["down"]
-    cuts.append((n_layers, -1))
+    cuts.append((n_layers, "L", 0))
     times.append(t)
     byts.append(y)
     P = len(cuts) - 1
@@ -289,11 +352,17 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
     b = best_b
     out = []
     for s in range(n):
-        (l0, c0), (l1, c1) = cuts[b[s]], cuts[b[s + 1]]
-        first_unit = 2 * l0 + (0 if c0 < 0 else 1)
-        end_unit = 2 * l1 + (0 if c1 < 0 else 1)     # exclusive, in half units
-        out.append(StageRange(first_unit, end_unit - first_unit, max(c0, 0) * step, max(c1, 0) * step))
+        (l0, k0, c0), (l1, k1, c1) = cuts[b[s]], cuts[b[s + 1]]
+        first_unit = 2 * l0 + (1 if k0 == "G" else 0)
+        end_unit = 2 * l1 + (0 if k1 == "L" else 1)     # exclusive, in half units
+        out.append(StageRange(first_unit, end_unit - first_unit, c0 * step if k0 == "G" else 0,
+                              c1 * step if k1 == "G" else 0, k0 == "O", k1 == "O"))
     return out
+
+
+def sublayer_split(n_layers: int, n: int, intermediate: int, **kw):
+    """gateup_split with attention|o boundaries as cut points too."""
+    return gateup_split(n_layers, n, intermediate, o_cuts=True, **kw)
 
 
 class SpanExecutor:
@@ -349,13 +418,14 @@ class PipelineStage:
                  device, seed: int, n_microbatches: int, batch: int, max_ctx: int, prefill_chunk: int = 2,
                  executor=None, group=None, profile: str = "random", want_logits: bool = False,
                  skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
-                 gateup_split_last: int = 0):
+                 gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False):
         """profile: the synthetic weight profile (runtime.SpanRuntime.init_synthetic: "peaked"
         for token-exact parity runs).  want_logits (last stage): every decode step's and the
         prefill's last-row logits are kept, for parity checks against the oracle's.
         skip_first_attn / skip_last_mlp / gateup_split_*: the stage's sub-layer boundaries
         (StageRange.span_kwargs()); across a gate/up boundary a decode-sized hand-off is a record
-        (h1 + the packed SwiGLU product, handoff_elems)."""
+        (h1 + the packed SwiGLU product, handoff_elems), across an attention|o boundary (o_split_*)
+        every hand-off is one (x + the attention output)."""
         assert n_microbatches == world, "the ring schedule keeps exactly one microbatch per stage in flight"
         self.dims, self.rank, self.world = dims, rank, world
         self.S = world
@@ -370,7 +440,8 @@ class PipelineStage:
                                max_tokens=max(prefill_chunk * max_ctx, batch), max_seqs=max(batch, prefill_chunk),
                                max_positions=max_ctx, device=self.device, skip_first_attn=skip_first_attn,
                                skip_last_mlp=skip_last_mlp, gateup_split_first=gateup_split_first,
-                               gateup_split_last=gateup_split_last)
+                               gateup_split_last=gateup_split_last, o_split_first=o_split_first,
+                               o_split_last=o_split_last)
             span.init_synthetic(seed, profile)
             executor = SpanExecutor(span)
         self.ex = executor
@@ -380,11 +451,15 @@ class PipelineStage:
         dev = self.device
         mb = range(n_microbatches)
         self.col_in, self.col_out = gateup_split_first, gateup_split_last
+        self.o_in, self.o_out = bool(o_split_first), bool(o_split_last)
+
+        def buf(col, o):     # a decode hand-off buffer: a record (1-D) or [batch, hidden]
+            if col or o:
+                return torch.zeros(buffer_elems(dims, batch, col, o), dtype=torch.bfloat16, device=dev)
+            return torch.zeros(batch, h, dtype=torch.bfloat16, device=dev)
         self.ids = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
-        self.h_in = [torch.zeros(record_elems(dims, batch) if self.col_in else (batch, h), dtype=torch.bfloat16,
-                                 device=dev) for _ in mb]
-        self.h_out = [torch.zeros(record_elems(dims, batch) if self.col_out else (batch, h), dtype=torch.bfloat16,
-                                  device=dev) for _ in mb]
+        self.h_in = [buf(self.col_in, self.o_in) for _ in mb]
+        self.h_out = [buf(self.col_out, self.o_out) for _ in mb]
         self.ids_out = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
         self.want_logits = want_logits and rank == world - 1
         self.logits = [torch.zeros(batch, dims.vocab, dtype=torch.bfloat16, device=dev) for _ in mb] \
@@ -492,16 +567,17 @@ class PipelineStage:
                 send = bufs_out.pop(i_send)
                 m, c = items[i_send]
                 rows = min(self.prefill_chunk, self.B - c) * T
-                if self.col_out and rows <= 64:           # a decode-sized call: record hand-off
-                    send = send[:handoff_elems(self.dims, rows, self.col_out)]
+                if (self.col_out and rows <= 64) or self.o_out:     # a record hand-off
+                    send = send.reshape(-1)[:handoff_elems(self.dims, rows, self.col_out, self.o_out, T == 1)]
             if not self.first and 0 <= i_cur < len(items):
                 m, c = items[i_cur]
                 nseq = min(self.prefill_chunk, self.B - c)
                 rows = nseq * T
-                if self.col_in and rows <= 64:
-                    recv = torch.zeros(record_elems(self.dims, rows), dtype=torch.bfloat16, device=self.device)
+                if (self.col_in and rows <= 64) or self.o_in:
+                    recv = torch.zeros(buffer_elems(self.dims, rows, self.col_in, self.o_in, T == 1),
+                                       dtype=torch.bfloat16, device=self.device)
                     bufs_in[i_cur] = recv
-                    recv = recv[:handoff_elems(self.dims, rows, self.col_in)]
+                    recv = recv[:handoff_elems(self.dims, rows, self.col_in, self.o_in, T == 1)]
                 else:
                     recv = torch.empty(rows, h, dtype=torch.bfloat16, device=self.device)
                     bufs_in[i_cur] = recv
@@ -588,16 +664,16 @@ class PipelineStage:
             if 0 <= i_prev < n_items:                      # output of last tick
                 mp = i_prev % self.n_mb
                 send = self.ids_out[mp] if self.last else self.h_out[mp]
-                if self.col_out and not self.last:         # a record: h1 + the act columns it carries
-                    send = send[:handoff_elems(self.dims, self.B, self.col_out)]
+                if (self.col_out or self.o_out) and not self.last:   # a record (the part carrying data)
+                    send = send[:handoff_elems(self.dims, self.B, self.col_out, self.o_out)]
             if self.first:
                 j = t - S                                  # ids of item j feed item j + S
                 if 0 <= j < n_items:
                     recv = self.ids[j % self.n_mb]
             elif 0 <= i_cur < n_items:
                 recv = self.h_in[i_cur % self.n_mb]
-                if self.col_in:
-                    recv = recv[:handoff_elems(self.dims, self.B, self.col_in)]
+                if self.col_in or self.o_in:
+                    recv = recv[:handoff_elems(self.dims, self.B, self.col_in, self.o_in)]
             tx = time.perf_counter()
             self._exchange(send, (self.rank + 1) % S, recv, (self.rank - 1) % S)
             t_x += time.perf_counter() - tx

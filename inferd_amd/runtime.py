@@ -204,18 +204,21 @@ class SpanRuntime:
                  has_lm_head: bool, kv_pages: int = 256, max_tokens: int = 4096, max_seqs: int = 64,
                  max_positions: int | None = None, device: str | torch.device = "cuda",
                  skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
-                 gateup_split_last: int = 0):
+                 gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False):
         """skip_first_attn / skip_last_mlp: sub-layer stage boundaries (InferdSpanConfig): the
         span starts at its first layer's MLP half (x = that layer's post-attention residual)
         and/or ends after its last layer's attention half (hidden out = that residual).
         gateup_split_first / _last: the boundary sits inside that layer's gate/up projection at
         this column; decode calls then hand over a record (h1, then the packed SwiGLU product,
-        record_elems()) instead of h1 alone."""
+        record_elems()) instead of h1 alone.  o_split_first / _last: the boundary sits between a
+        layer's attention and its o projection; every call hands over a record (the layer's input
+        residual, then the attention output: o_record_elems())."""
         self.dims = dims
         self.first_layer, self.n_layers = first_layer, n_layers
         self.has_embed, self.has_lm_head = has_embed, has_lm_head
         self.skip_first_attn, self.skip_last_mlp = bool(skip_first_attn), bool(skip_last_mlp)
         self.gateup_split_first, self.gateup_split_last = int(gateup_split_first), int(gateup_split_last)
+        self.o_split_first, self.o_split_last = bool(o_split_first), bool(o_split_last)
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -223,7 +226,8 @@ class SpanRuntime:
         self.max_positions = max_positions or dims.max_positions
         cfg = [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
                n_layers, int(has_embed), int(has_lm_head), self.max_positions, kv_pages, max_tokens, max_seqs,
-               int(skip_first_attn), int(skip_last_mlp), int(gateup_split_first), int(gateup_split_last)]
+               int(skip_first_attn), int(skip_last_mlp), int(gateup_split_first), int(gateup_split_last),
+               int(o_split_first), int(o_split_last)]
         self.handle = None
         self.handle = T.span_create(cfg, dims.eps, dims.rope_theta, self.device)
         self.kv = KvTable(kv_pages)
@@ -241,6 +245,13 @@ class SpanRuntime:
         then the packed SwiGLU product [rows rounded to 16][intermediate]
         (include/inferd_span.h, InferdSpanConfig gateup_split_*)."""
         return rows * self.dims.hidden + (rows + 15) // 16 * 16 * self.dims.intermediate
+
+    def o_record_elems(self, rows: int, decode: bool) -> int:
+        """bf16 elements of an attention|o-boundary record: the layer's input residual
+        [rows][hidden], then the attention output [rows, or rows rounded to 16 in a pure decode
+        call (fragment-packed)][heads * 128]."""
+        d = self.dims
+        return rows * d.hidden + ((rows + 15) // 16 * 16 if decode else rows) * d.heads * d.head_dim
 
     # ----------------------------------------------------------------- weights
     def _stream(self):
@@ -391,6 +402,13 @@ class SpanRuntime:
         if len(set(sids)) != len(sids):
             raise ValueError("a session may appear only once per forward call")
         total = sum(n for _, n in requests)
+        # hand-off records (InferdSpanConfig): decode calls at a gate/up boundary, every call at an
+        # attention|o boundary (the attention output fragment-packed in a pure decode call)
+        packed = total <= 64 and all(n == 1 for _, n in requests)
+        in_rec = (self.record_elems(total) if self.gateup_split_first and total <= 64 else
+                  self.o_record_elems(total, packed) if self.o_split_first else 0)
+        out_rec = (self.record_elems(total) if self.gateup_split_last and total <= 64 else
+                   self.o_record_elems(total, packed) if self.o_split_last else 0)
         with torch.cuda.device(dev):
             ids_d = x_d = None
             if self.has_embed:
@@ -405,15 +423,17 @@ class SpanRuntime:
             else:
                 if x is None:
                     raise ValueError("span needs hidden states x")
-                if self.gateup_split_first and total <= 64:   # a decode hand-off record (h1 | act)
+                if in_rec:   # a hand-off record (h1 | act, or x | attention output)
                     x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(-1).contiguous()
-                    if x_d.numel() < self.record_elems(total):
-                        raise ValueError(f"x: a gate/up-boundary record of {self.record_elems(total)} elements "
-                                         f"expected for {total} rows, got {x_d.numel()}")
+                    if x_d.numel() < in_rec:
+                        raise ValueError(f"x: a {in_rec}-element hand-off record expected for {total} rows, "
+                                         f"got {x_d.numel()}")
                 else:
                     x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(total, d.hidden).contiguous()
             rec_in = x_d is not None and x_d.dim() == 1
-            rec_out = bool(self.gateup_split_last) and total <= 64 and want_hidden
+            rec_out = bool(out_rec) and want_hidden
+            if self.o_split_last and not want_hidden:
+                raise ValueError("a span ending before an o projection always hands over its record")
             temp = []
             states = []
             for sid, _ in requests:
@@ -431,8 +451,8 @@ class SpanRuntime:
                 lm = self.has_lm_head
                 hid = torch.empty((total, d.hidden), dtype=torch.bfloat16, device=dev) if want_hidden else None
                 rec = None
-                if rec_out:      # h1 then the packed act columns this span computes
-                    rec = torch.empty(self.record_elems(total), dtype=torch.bfloat16, device=dev)
+                if rec_out:      # h1 then the packed act columns (or x then the attention output)
+                    rec = torch.empty(out_rec, dtype=torch.bfloat16, device=dev)
                     hid = rec[:total * d.hidden].view(total, d.hidden)
                 nid = torch.empty((B,), dtype=torch.int32, device=dev) if (want_next_ids and lm) else None
                 lg = torch.empty((B, d.vocab), dtype=torch.bfloat16, device=dev) if (want_logits and lm) else None
@@ -447,6 +467,9 @@ class SpanRuntime:
                          total > 64 and any(sum(t for _, _, t in c) <= 64 for c in calls)):
                     raise ValueError("across a gate/up boundary a call is either one decode-sized engine call "
                                      "(<= 64 rows, record hand-off) or only prefill-sized ones (> 64 rows)")
+                if (self.o_split_first or self.o_split_last) and len(calls) > 1:
+                    raise ValueError("across an attention|o boundary a forward call is one engine call "
+                                     f"(at most {self.max_tokens} tokens / {self.max_seqs} sequences)")
                 keep = []
                 for call in calls:
                     r0 = row0[call[0][0]] + call[0][1]

@@ -383,10 +383,12 @@ def _free_port():
 def _ranges(sizes):
     """StageRanges of a test split: stage sizes in layers (multiples of 0.5: half-layer
     boundaries), or "gateup8" -- bench.py --split gateup at 8 stages (boundaries inside gate/up
-    projections, record hand-offs)"""
-    from inferd_amd.pipeline import gateup_split, ranges_from_sizes
+    projections, record hand-offs) -- or "sublayer8" (bench.py --split sublayer)"""
+    from inferd_amd.pipeline import gateup_split, ranges_from_sizes, sublayer_split
     if sizes == "gateup8":
         return gateup_split(36, 8, 12288)
+    if sizes == "sublayer8":      # bench.py --split sublayer: attention|o boundaries too
+        return sublayer_split(36, 8, 12288)
     return ranges_from_sizes(sizes)
 
 
@@ -489,9 +491,9 @@ def q8b_prefill_logits_oracle():
 
 @pytest.mark.timeout(1200)
 @pytest.mark.parametrize("sizes", [[18, 18], [9, 9, 9, 9], [5, 5, 5, 5, 4, 4, 4, 4], [5, 27, 4], [6, 12, 12, 6],
-                                   [2, 3, 5, 6, 6, 6, 5, 3], HALVES8, "gateup8"],
+                                   [2, 3, 5, 6, 6, 6, 5, 3], HALVES8, "gateup8", "sublayer8"],
                          ids=["config3_even2", "config3_even4", "config3_even8", "config4_uneven3", "config4_uneven4",
-                              "config4_uneven8", "halves8", "gateup8"])
+                              "config4_uneven8", "halves8", "gateup8", "sublayer8"])
 def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_logits_oracle):
     """BASELINE configs 3 (Qwen3-8B, the even splits [18,18], [9,9,9,9], [5,5,5,5,4,4,4,4]) and 4
     (SURVEY §8(d)'s uneven splits [5, 27, 4], [6, 12, 12, 6], [2, 3, 5, 6, 6, 6, 5, 3]) at full
@@ -516,13 +518,17 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     d = R.CONFIGS["qwen3-8b"]
     ids = _prompts(world)[0][:2]
     r0 = _ranges(sizes)[0]
-    ref = R.RefSpan(d, SEED, 0, r0.last_layer, True, False, torch.bfloat16, "sdpa",
-                    skip_last_mlp=r0.skip_last_mlp).forward(ids)
+    # the captured hidden rows: the stage's output, or (a stage ending before an o projection) the
+    # x part of its record
+    ref = R.RefSpan(d, SEED, 0, r0.last_layer, True, False, torch.bfloat16, "sdpa", skip_last_mlp=r0.skip_last_mlp,
+                    o_split_last=r0.last_o).forward(ids)
+    ref = ref[0] if r0.last_o else ref
     h = pipe["hidden"].reshape(2, T8, -1)
     e = [errs(h[b], ref[b]) for b in range(2)]
     # fp32 oracle on sequence 0: the bf16 noise floor of this boundary, at every depth
-    ref32 = R.RefSpan(d, SEED, 0, r0.last_layer, True, False, torch.float32, "sdpa",
-                      skip_last_mlp=r0.skip_last_mlp).forward(ids[:1])[0]
+    ref32 = R.RefSpan(d, SEED, 0, r0.last_layer, True, False, torch.float32, "sdpa", skip_last_mlp=r0.skip_last_mlp,
+                      o_split_last=r0.last_o).forward(ids[:1])
+    ref32 = (ref32[0] if r0.last_o else ref32)[0]
     noise = {"engine_vs_fp32": errs(h[0], ref32), "bf16_ref_vs_fp32": errs(ref[0], ref32)}
     print(f"noise floor: engine vs fp32 rms {noise['engine_vs_fp32']['rms_rel']:.2e}, "
           f"bf16 reference vs fp32 rms {noise['bf16_ref_vs_fp32']['rms_rel']:.2e}")
@@ -656,9 +662,9 @@ def _pipe_exact_worker(rank, world, port, sizes, out_dir, profile="peaked_deep",
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("sizes", [[18, 18], [9, 9, 9, 9], [5, 5, 5, 5, 4, 4, 4, 4], [4, 5, 5, 5, 5, 5, 5, 2],
-                                   [5, 27, 4], HALVES8, "gateup8"],
+                                   [5, 27, 4], HALVES8, "gateup8", "sublayer8"],
                          ids=["config3_even2", "config3_even4", "config3_even8", "balanced8", "config4_uneven3",
-                              "halves8", "gateup8"])
+                              "halves8", "gateup8", "sublayer8"])
 def test_q8b_pipeline_token_exact_vs_oracle(tmp_path, sizes, q8b_oracle_greedy):
     """Qwen3-8B through the span pipeline against the CPU oracle ("peaked_deep" profile, see the
     section comment for what each check proves):

@@ -324,6 +324,75 @@ def test_gateup_boundary_chain_bit_exact(T):
         s.check_errors()
 
 
+@pytest.mark.parametrize("split,T", [("o", 70), ("o", 9), ("o_gateup", 9)],
+                         ids=["o_prefill_rows", "o_prefill_small", "o_then_gateup"])
+def test_o_boundary_chain_bit_exact(split, T):
+    """Stage boundaries between a layer's attention and its o projection (InferdSpanConfig
+    o_split_*): Qwen3-0.6B layers 0..3 as [0..1q] (embed), [1o..3q], [3o..3] (lm_head) -- or
+    [0..1q], [1o..2a+1024], [2m@1024..3] (an attention|o boundary and a gate/up one) -- give
+    bit-identical logits to one span: a prefill of 3 sequences (the record x | attention output
+    row-major), then 5 decode-graph steps whose records carry the attention output fragment-packed.
+    The first record's attention output (layer 1's, before o_proj) is within the span tolerance of
+    the oracle's."""
+    from inferd_amd.pipeline import StageRange, buffer_elems, o_record_elems, unpack_rows
+    from inferd_amd.runtime import DecodeGraph
+    d = R.CONFIGS["qwen3-0.6b"]
+    B, STEPS = 3, 5
+    Hd = d.heads * d.head_dim
+    gen = torch.Generator().manual_seed(43)
+    prompts = torch.randint(0, d.vocab, (B, T), generator=gen)
+    forced = torch.randint(0, d.vocab, (STEPS, B), generator=gen)
+    if split == "o":
+        ranges = [StageRange(0, 3, last_o=True), StageRange(2, 5, first_o=True, last_o=True),
+                  StageRange(6, 2, first_o=True)]
+    else:
+        ranges = [StageRange(0, 3, last_o=True), StageRange(2, 3, 0, 1024, first_o=True), StageRange(5, 3, 1024, 0)]
+    chain = [span("qwen3-0.6b", r.first_layer, r.n_layers, i == 0, i == 2, kv_pages=16, max_tokens=B * T + 64,
+                  max_seqs=B, max_positions=1024, **r.span_kwargs()) for i, r in enumerate(ranges)]
+    one = span("qwen3-0.6b", 0, 4, True, True, kv_pages=16, max_tokens=B * T + 64, max_seqs=B, max_positions=1024)
+    sess = [f"o{b}" for b in range(B)]
+    reqs = [(sid, T) for sid in sess]
+    o0 = chain[0].forward(reqs, ids=prompts.reshape(-1))
+    rec0 = o0["record"]
+    assert rec0.numel() == o_record_elems(d, B * T, False)
+    o1 = chain[1].forward(reqs, x=rec0)
+    lc = chain[2].forward(reqs, x=o1.get("record", o1["hidden"]), want_logits=True, want_hidden=False)["logits"]
+    lo = one.forward(reqs, ids=prompts.reshape(-1), want_logits=True, want_hidden=False)["logits"]
+    assert torch.equal(lc, lo), (lc.float() - lo.float()).abs().max()
+    xr, ar = R.RefSpan(d, SEED, 0, 1, True, False, o_split_last=True).forward(prompts)
+    ex = rel_err(rec0[:B * T * d.hidden].reshape(B, T, -1), xr)
+    ea = rel_err(rec0[B * T * d.hidden:].reshape(B, T, -1), ar)
+    print(f"attention|o record vs oracle: x rel err {ex:.2e}, attention output rel err {ea:.2e}")
+    assert ex < TOL_REL and ea < TOL_REL
+    ids_c = torch.zeros(B, dtype=torch.int32, device=DEV)
+    ids_o = torch.zeros(B, dtype=torch.int32, device=DEV)
+    r0, r1 = ranges[0], ranges[1]
+    recs = [torch.zeros(buffer_elems(d, B, r.last_col, r.last_o), dtype=torch.bfloat16, device=DEV)
+            for r in (r0, r1)]
+    lg_c = torch.zeros(B, d.vocab, dtype=torch.bfloat16, device=DEV)
+    lg_o = torch.zeros(B, d.vocab, dtype=torch.bfloat16, device=DEV)
+    nid_c = torch.zeros(B, dtype=torch.int32, device=DEV)
+    nid_o = torch.zeros(B, dtype=torch.int32, device=DEV)
+    graphs = [DecodeGraph(chain[0], sess, STEPS, ids=ids_c, hidden_out=recs[0]),
+              DecodeGraph(chain[1], sess, STEPS, x=recs[0], hidden_out=recs[1]),
+              DecodeGraph(chain[2], sess, STEPS, x=recs[1], next_ids=nid_c, logits=lg_c)]
+    g1 = DecodeGraph(one, sess, STEPS, ids=ids_o, next_ids=nid_o, logits=lg_o)
+    assert recs[0].numel() == B * d.hidden + 16 * Hd
+    for k in range(STEPS):
+        ids_c.copy_(forced[k])
+        ids_o.copy_(forced[k])
+        for g in graphs:
+            g.launch()
+        g1.launch()
+        assert torch.equal(lg_c, lg_o), (k, (lg_c.float() - lg_o.float()).abs().max())
+        assert torch.equal(nid_c, nid_o), k
+    # the decode record's attention output is fragment-packed: its padding rows stay zero
+    a = unpack_rows(recs[0][B * d.hidden:], 16, Hd)
+    assert torch.count_nonzero(a[B:]) == 0 and torch.count_nonzero(a[:B]) > 0
+    for s in chain + [one]:
+        s.check_errors()
+
+
 def test_half_layer_span_rejects_bad_configs():
     """A span with the embedding cannot start at a MLP half, one with lm_head cannot end at an
     attention half, a one-layer span cannot skip both halves, and a layer's absent half has no
@@ -337,6 +406,20 @@ def test_half_layer_span_rejects_bad_configs():
     with pytest.raises(RuntimeError, match="both"):
         SpanRuntime(d, 1, 1, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
                     skip_first_attn=True, skip_last_mlp=True)
+    for kw in ({"o_split_first": True, "o_split_last": True}, {"o_split_first": True, "skip_last_mlp": True}):
+        with pytest.raises(RuntimeError, match="cannot end before"):
+            SpanRuntime(d, 1, 1, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64,
+                        max_seqs=2, **kw)
+    for kw in ({"has_embed": True, "o_split_first": True}, {"has_lm_head": True, "o_split_last": True},
+               {"skip_first_attn": True, "o_split_first": True}):
+        with pytest.raises(RuntimeError, match="attention\\|o boundary excludes"):
+            SpanRuntime(d, 1, 2, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
+                        **{"has_embed": False, "has_lm_head": False, **kw})
+    so = SpanRuntime(d, 1, 2, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
+                     o_split_first=True)
+    with pytest.raises(RuntimeError, match="other half"):
+        so.set_weight(0, "k_proj", torch.zeros(d.kv_heads * 128, d.hidden, dtype=torch.bfloat16))
+    so.set_weight(0, "o_proj", torch.zeros(d.hidden, d.heads * 128, dtype=torch.bfloat16))
     s = SpanRuntime(d, 1, 2, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
                     skip_first_attn=True)
     with pytest.raises(RuntimeError, match="other half"):

@@ -23,7 +23,8 @@ class OracleExecutor:
 
     def __init__(self, d, r, first_span, last_span):
         self.sp = R.RefSpan(d, SEED, r.first_layer, r.last_layer, first_span, last_span, torch.bfloat16, "sdpa",
-                            skip_first_attn=r.skip_first_attn, skip_last_mlp=r.skip_last_mlp)
+                            skip_first_attn=r.skip_first_attn, skip_last_mlp=r.skip_last_mlp,
+                            o_split_first=r.first_o, o_split_last=r.last_o)
         self.device = torch.device("cpu")
         self.has_embed, self.has_lm_head = first_span, last_span
         self.dims = d
@@ -31,18 +32,32 @@ class OracleExecutor:
 
     def _run(self, sessions, n, ids=None, x=None, want_ids=False):
         """Decode-sized hand-offs across a gate/up boundary are records (h1 first, then the packed
-        SwiGLU product): the oracle reads and writes the h1 part and recomputes the whole MLP."""
+        SwiGLU product): the oracle reads and writes the h1 part and recomputes the whole MLP.
+        Across an attention|o boundary every hand-off is a record (x, then the attention output,
+        fragment-packed in a pure decode call): the oracle reads / writes both parts."""
+        from inferd_amd.pipeline import pack_rows, unpack_rows
         outs = []
-        rows, h = len(sessions) * n, self.dims.hidden
+        S, rows, h = len(sessions), len(sessions) * n, self.dims.hidden
+        Hd = self.dims.heads * self.dims.head_dim
+        packed = n == 1 and rows <= 64
+        a_in = None
+        if x is not None and self.r.first_o:
+            tail = x.reshape(-1)[rows * h:]
+            a_in = (unpack_rows(tail, rows, Hd) if packed else tail[:rows * Hd].view(rows, Hd)).reshape(S, n, Hd)
         for i, sid in enumerate(sessions):
             if ids is not None:
-                inp = ids.reshape(len(sessions), n)[i:i + 1].long()
+                inp = ids.reshape(S, n)[i:i + 1].long()
                 o = self.sp.forward_cached(sid, inp)
             else:
-                o = self.sp.forward_cached(sid, x.reshape(-1)[:rows * h].reshape(len(sessions), n, -1)[i:i + 1])
+                xi = x.reshape(-1)[:rows * h].reshape(S, n, -1)[i:i + 1]
+                o = self.sp.forward_cached(sid, (xi, a_in[i:i + 1]) if a_in is not None else xi)
             outs.append(o)
         if self.sp.last:
             return torch.stack([torch.argmax(o[0, -1]) for o in outs]).to(torch.int32)
+        if self.r.last_o:
+            xs = torch.cat([o[0][0] for o in outs]).to(torch.bfloat16).reshape(-1)
+            a = torch.cat([o[1][0] for o in outs]).to(torch.bfloat16)
+            return torch.cat([xs, pack_rows(a) if packed else a.reshape(-1)])
         h1 = torch.cat([o[0] for o in outs]).to(torch.bfloat16)
         if self.r.last_col and rows <= 64:
             from inferd_amd.pipeline import record_elems
@@ -80,6 +95,11 @@ def _split(d, world, sizes):
     from inferd_amd.pipeline import StageRange, even_split, ranges_from_sizes
     if sizes == "gateup":
         return [StageRange(0, 3, 0, 256), StageRange(3, 2, 256, 128), StageRange(5, 3, 128, 0)][:world]
+    if sizes == "o":      # attention|o boundaries in layers 1 and 3
+        return [StageRange(0, 3, last_o=True), StageRange(2, 5, first_o=True, last_o=True),
+                StageRange(6, 2, first_o=True)][:world]
+    if sizes == "o_gateup":   # an attention|o boundary, then a gate/up one (the same stage)
+        return [StageRange(0, 3, last_o=True), StageRange(2, 3, 0, 256, first_o=True), StageRange(5, 3, 256, 0)]
     if not sizes:
         return [StageRange.layers(f, n) for f, n in even_split(d.layers, world)]
     return ranges_from_sizes(sizes)
@@ -155,7 +175,8 @@ def _reference(world, n_steps, sizes=None, force=False):
 
 
 @pytest.mark.parametrize("world,sizes", [(2, None), (3, None), (3, [1, 2, 1]), (2, [3, 1]),
-                                         (2, [1.5, 2.5]), (3, [0.5, 2, 1.5]), (3, "gateup")])
+                                         (2, [1.5, 2.5]), (3, [0.5, 2, 1.5]), (3, "gateup"),
+                                         (3, "o"), (3, "o_gateup")])
 def test_pipeline_matches_single_process(world, sizes):
     n_steps = 4
     ctx = mp.get_context("spawn")

@@ -10,27 +10,33 @@ D8 = MODELS["qwen3-8b"]
 
 
 def _cover(ranges, n_layers, intermediate):
-    """every half-layer unit once, in order; a gate/up column boundary continues exactly where
+    """every half-layer unit once, in order (an attention unit cut before its o projection is
+    shared by the two stages around the cut); a gate/up column boundary continues exactly where
     the previous stage stopped"""
     u = 0
-    prev_col = 0
+    prev_col, prev_o = 0, False
     for i, r in enumerate(ranges):
         assert r.first_unit == u, (i, r)
-        assert r.first_col == prev_col, (i, r)
+        assert r.first_col == prev_col and r.first_o == prev_o, (i, r)
         assert r.first_col % 128 == 0 and r.last_col % 128 == 0
         assert 0 <= r.first_col < intermediate and 0 <= r.last_col < intermediate
         if r.first_col:
             assert r.skip_first_attn
         if r.last_col:
             assert r.skip_last_mlp
-        u += r.n_units
-        prev_col = r.last_col
-    assert u == 2 * n_layers and prev_col == 0
+        if r.first_o or r.last_o:      # the engine's constraints (span.hip inferd_span_create)
+            assert not (r.first_o and r.skip_first_attn) and not (r.last_o and r.skip_last_mlp)
+            assert r.n_layers > 1 or not (r.first_o and (r.last_o or r.skip_last_mlp))
+        u = r.end_unit
+        prev_col, prev_o = r.last_col, r.last_o
+    assert u == 2 * n_layers and prev_col == 0 and not prev_o
+    assert not ranges[0].first_o and not ranges[-1].last_o
 
 
 @pytest.mark.parametrize("n", [1, 2, 4, 8])
 def test_splits_cover_the_model(n):
-    for ranges in (P.halves_split(D8.layers, n), P.gateup_split(D8.layers, n, D8.intermediate)):
+    for ranges in (P.halves_split(D8.layers, n), P.gateup_split(D8.layers, n, D8.intermediate),
+                   P.sublayer_split(D8.layers, n, D8.intermediate)):
         assert len(ranges) == n
         _cover(ranges, D8.layers, D8.intermediate)
     assert [r.label() for r in P.ranges_from_sizes([4.5, 4.5, 5, 5, 4.5, 5, 5, 2.5])][:2] == ["0..4a", "4m..8"]
@@ -57,6 +63,29 @@ def test_gateup_split_balances_better_than_halves():
     assert score(P.gateup_split(D8.layers, 8, D8.intermediate)) > score(P.halves_split(D8.layers, 8))
 
 
+def test_sublayer_split_model_score():
+    """With attention|o cut points too the model's lowest per-stage HBM fraction at the tick
+    rises again (bench.range_bytes over the model's stage times)."""
+    import bench
+
+    def model(ranges):
+        c = P.DECODE_US_8B
+        t, b = [], []
+        for i, r in enumerate(ranges):
+            last = i == len(ranges) - 1
+            n_attn = sum(1 for u in range(r.first_unit, r.first_unit + r.n_units) if u % 2 == 0)
+            us = n_attn * c["attn_half"] + (r.n_units - n_attn) * c["mlp_half"] + c["stage_norm"]
+            us += P.DECODE_US_8B_GATEUP * (r.last_col - r.first_col) / D8.intermediate
+            us -= (c["attn_half"] - P.DECODE_US_8B_O) if r.first_o else 0.0
+            us -= P.DECODE_US_8B_O if r.last_o else 0.0
+            t.append(us + (c["head"] if last else 0.0))
+            b.append(bench.range_bytes(D8, r, 16, 2060, last))
+        return min(b) / max(t)
+    sub = P.sublayer_split(D8.layers, 8, D8.intermediate)
+    assert any(r.first_o for r in sub)
+    assert model(sub) > model(P.gateup_split(D8.layers, 8, D8.intermediate))
+
+
 def test_record_sizes():
     assert P.record_elems(D8, 16) == 16 * 4096 + 16 * 12288
     assert P.record_elems(D8, 17) == 17 * 4096 + 32 * 12288
@@ -65,7 +94,28 @@ def test_record_sizes():
     assert P.handoff_elems(D8, 20, 2048) == P.record_elems(D8, 20)     # several: the whole record
     r = P.StageRange(9, 10, 2048, 4096)
     assert r.span_kwargs() == {"skip_first_attn": True, "skip_last_mlp": True, "gateup_split_first": 2048,
-                               "gateup_split_last": 4096}
+                               "gateup_split_last": 4096, "o_split_first": False, "o_split_last": False}
     assert r.label() == "4m@2048..9a+4096"
     with pytest.raises(AssertionError):
         P.StageRange(8, 10, 2048, 0)          # a gate/up boundary refines a half boundary
+    r = P.StageRange(28, 9, first_o=True, last_o=True)
+    assert r.label() == "14o..18q" and r.end_unit == 36 and not r.skip_last_mlp
+    assert r.span_kwargs()["o_split_first"] and r.span_kwargs()["o_split_last"]
+    assert P.o_record_elems(D8, 16, True) == 16 * 4096 + 16 * 4096
+    assert P.o_record_elems(D8, 3, True) == 3 * 4096 + 16 * 4096
+    assert P.o_record_elems(D8, 70, False) == 70 * 4096 * 2
+    assert P.handoff_elems(D8, 3, 0, o=True) == P.buffer_elems(D8, 3, 0, o=True) == P.o_record_elems(D8, 3, True)
+    with pytest.raises(AssertionError):
+        P.StageRange(29, 4, first_o=True)     # an attention|o boundary sits in an attention unit
+
+
+def test_packed_rows_round_trip():
+    """pipeline.pack_rows is common.h packed_index: element (r, c) of a [rows][K] matrix at
+    ((r / 16) * K/32 + c / 32) * 512 + (r % 16) * 8 + (c % 32 / 8) * 128 + c % 8."""
+    import torch
+    t = torch.arange(19 * 96, dtype=torch.float32).view(19, 96)
+    f = P.pack_rows(t)
+    assert f.numel() == 32 * 96
+    for r, c in ((0, 0), (5, 37), (18, 95), (16, 8)):
+        assert f[((r // 16) * 3 + c // 32) * 512 + (r % 16) * 8 + (c % 32 // 8) * 128 + c % 8] == t[r, c]
+    assert torch.equal(P.unpack_rows(f, 19, 96), t)
