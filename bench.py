@@ -269,66 +269,74 @@ def range_bytes(d, r, B: int, ctx_mean: float, lm_head: bool) -> float:
     return nb
 
 
-def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: int = 3, reps: int = 20) -> dict:
-    """Every stage of every split measured alone on this GPU with its real role (embedding on
-    stage 0, final norm + lm_head + argmax on the last): the span is built, B sequences are
-    prefilled with ctx tokens through the real prefill path (stage 0 from random ids, later
-    stages from random hidden states), one microbatch's decode step is captured as the stage's
-    decode graph, and `reps` replays are timed with HIP events on the launch stream outside the
-    graph (after `warmup` replays).  The lockstep pipeline (pipeline.py) ticks at its slowest
-    stage, so per split: tick = max stage ms, each stage's fraction of the HBM roofline at that
-    tick = its algorithmic bytes / (tick x 8 TB/s), bubble = 1 - sum / (S x
-    tick), and the compute-only projected rate S x B / tick (the xGMI hand-off excluded)."""
+def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int, warmup: int = 3,
+             reps: int = 20) -> float:
+    """One stage (StageRange r, with the embedding when first and final norm + lm_head + argmax
+    when last) measured alone on this GPU: the span is built, B sequences are prefilled with
+    ctx tokens through the real prefill path (stage 0 from random ids, later stages from random
+    hidden states / records), one microbatch's decode step is captured as the stage's decode
+    graph, and `reps` replays are timed with HIP events on the launch stream outside the graph
+    (after `warmup` replays).  Returns ms per replay."""
     from inferd_amd.runtime import DecodeGraph, SpanRuntime
+    chunk = 2
+    span = SpanRuntime(d, r.first_layer, r.n_layers, has_embed=first, has_lm_head=last,
+                       kv_pages=B * ((ctx + warmup + reps) // 64 + 2) + 4, max_tokens=chunk * ctx,
+                       max_seqs=B, max_positions=ctx + warmup + reps + 64, device=dev, **r.span_kwargs())
+    span.init_synthetic(seed)
+    sess = [("proj", b) for b in range(B)]
+    for c in range(0, B, chunk):
+        reqs = [(sid, ctx) for sid in sess[c:c + chunk]]
+        if first:
+            ids = torch.randint(0, d.vocab, (len(reqs) * ctx,), generator=g, dtype=torch.int32)
+            span.forward(reqs, ids=ids, want_hidden=False, want_next_ids=last)
+        else:     # (a record x | attention output at an attention|o boundary)
+            n_in = buffer_elems(d, len(reqs) * ctx, 0, r.first_o, False)
+            x = (torch.randn(n_in, generator=g) * 0.5).to(torch.bfloat16)
+            span.forward(reqs, x=x, want_hidden=r.last_o, want_next_ids=last)
+    ids = torch.zeros(B, dtype=torch.int32, device=dev) if first else None
+    x = None if first else (torch.randn(B, d.hidden, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    if r.first_col or r.first_o:      # a record: h1 + the packed act, or x + the attention output
+        n_in = buffer_elems(d, B, r.first_col, r.first_o)
+        x = torch.cat([x.reshape(-1), (torch.randn(n_in - B * d.hidden, generator=g) * 0.5 if r.first_o else
+                                       torch.zeros(n_in - B * d.hidden)).to(torch.bfloat16).to(dev)])
+    hout = None if last else torch.empty(buffer_elems(d, B, r.last_col, r.last_o), dtype=torch.bfloat16,
+                                         device=dev)
+    nid = torch.empty(B, dtype=torch.int32, device=dev) if last else None
+    graph = DecodeGraph(span, sess, warmup + reps, ids=ids, x=x, hidden_out=hout, next_ids=nid)
+    for _ in range(warmup):
+        graph.launch()
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        graph.launch()
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    span.check_errors()
+    del graph, span
+    torch.cuda.synchronize(dev)
+    return ms
+
+
+def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: int = 3, reps: int = 20) -> dict:
+    """Every stage of every split measured alone on this GPU with its real role (stage_ms:
+    embedding on stage 0, final norm + lm_head + argmax on the last).  The lockstep pipeline
+    (pipeline.py) ticks at its slowest stage, so per split: tick = max stage ms, each stage's
+    fraction of the HBM roofline at that tick = its algorithmic bytes / (tick x 8 TB/s) (SURVEY
+    §8(d)), bubble = 1 - sum / (S x tick), and the compute-only projected rate S x B / tick (the
+    xGMI hand-off excluded)."""
     out = {}
     g = torch.Generator(device="cpu").manual_seed(seed + 5)
-    chunk = 2
     for name, ranges in splits.items():
         S = len(ranges)
         stages = []
         for s, r in enumerate(ranges):
-            first, last = s == 0, s == S - 1
-            span = SpanRuntime(d, r.first_layer, r.n_layers, has_embed=first, has_lm_head=last,
-                               kv_pages=B * ((ctx + warmup + reps) // 64 + 2) + 4, max_tokens=chunk * ctx,
-                               max_seqs=B, max_positions=ctx + warmup + reps + 64, device=dev,
-                               **r.span_kwargs())
-            span.init_synthetic(seed)
-            sess = [("proj", b) for b in range(B)]
-            for c in range(0, B, chunk):
-                reqs = [(sid, ctx) for sid in sess[c:c + chunk]]
-                if first:
-                    ids = torch.randint(0, d.vocab, (len(reqs) * ctx,), generator=g, dtype=torch.int32)
-                    span.forward(reqs, ids=ids, want_hidden=False, want_next_ids=last)
-                else:     # (a record x | attention output at an attention|o boundary)
-                    n_in = buffer_elems(d, len(reqs) * ctx, 0, r.first_o, False)
-                    x = (torch.randn(n_in, generator=g) * 0.5).to(torch.bfloat16)
-                    span.forward(reqs, x=x, want_hidden=r.last_o, want_next_ids=last)
-            ids = torch.zeros(B, dtype=torch.int32, device=dev) if first else None
-            x = None if first else (torch.randn(B, d.hidden, generator=g) * 0.5).to(torch.bfloat16).to(dev)
-            if r.first_col or r.first_o:      # a record: h1 + the packed act, or x + the attention output
-                n_in = buffer_elems(d, B, r.first_col, r.first_o)
-                x = torch.cat([x.reshape(-1), (torch.randn(n_in - B * d.hidden, generator=g) * 0.5 if r.first_o else
-                                               torch.zeros(n_in - B * d.hidden)).to(torch.bfloat16).to(dev)])
-            hout = None if last else torch.empty(buffer_elems(d, B, r.last_col, r.last_o), dtype=torch.bfloat16,
-                                                 device=dev)
-            nid = torch.empty(B, dtype=torch.int32, device=dev) if last else None
-            graph = DecodeGraph(span, sess, warmup + reps, ids=ids, x=x, hidden_out=hout, next_ids=nid)
-            for _ in range(warmup):
-                graph.launch()
-            stream = torch.cuda.current_stream(dev)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(reps):
-                graph.launch()
-            e1.record(stream)
-            e1.synchronize()
-            ms = e0.elapsed_time(e1) / reps
-            span.check_errors()
+            last = s == S - 1
+            ms = stage_ms(d, r, s == 0, last, B, ctx, dev, g, seed, warmup, reps)
             nb = range_bytes(d, r, B, ctx + warmup + (reps + 1) / 2.0, last)
             stages.append({"range": r.label(), "units": r.n_units, "ms": round(ms, 4), "alg_bytes": int(nb),
                            "frac_own": round(nb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
-            del graph, span
-            torch.cuda.synchronize(dev)
         tick = max(st["ms"] for st in stages)
         for st in stages:
             st["frac_at_tick"] = round(st["alg_bytes"] / (tick * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
@@ -339,10 +347,22 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
     return out
 
 
+def sub_split(d, n: int, o_cuts: bool):
+    """The sub-layer splits (pipeline.gateup_split: gate/up boundaries; o_cuts: attention|o
+    boundaries too) on the measured boundary-cost table where one exists for the model
+    (pipeline.measured_split, inferd_amd/data/decode_costs_*.json), else on the kernel-mean model."""
+    import os
+    from inferd_amd import pipeline as P
+    name = d.name.replace("-", "_")
+    if os.path.exists(os.path.join(os.path.dirname(P.__file__), "data", f"decode_costs_{name}.json")):
+        return P.measured_split(d.layers, n, d.intermediate, o_cuts=o_cuts, name=name)
+    return P.gateup_split(d.layers, n, d.intermediate, o_cuts=o_cuts)
+
+
 def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
     """The splits stage_projection measures: BASELINE config 3's even splits, the layer-granular
     byte-balanced split and the half-layer time-balanced split at each stage count."""
-    from inferd_amd.pipeline import StageRange, gateup_split, halves_split, sublayer_split
+    from inferd_amd.pipeline import StageRange, halves_split
     out = {}
     for n in sizes:
         if n > d.layers:
@@ -351,8 +371,8 @@ def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
         bal = [StageRange.layers(f, k) for f, k in stage_split(d, n, B, ctx, "balanced")]
         if bal != out[f"even{n}"]:
             out[f"balanced{n}"] = bal
-        for name, sp in (("halves", halves_split(d.layers, n)), ("gateup", gateup_split(d.layers, n, d.intermediate)),
-                         ("sublayer", sublayer_split(d.layers, n, d.intermediate))):
+        for name, sp in (("halves", halves_split(d.layers, n)), ("gateup", sub_split(d, n, False)),
+                         ("sublayer", sub_split(d, n, True))):
             if all(sp != v for v in out.values()):
                 out[f"{name}{n}"] = sp
     return out
@@ -506,10 +526,8 @@ def main():
             f"--spans {args.spans}: need {world} stages, {d.layers} layers"
     elif args.split == "halves":
         ranges = P.halves_split(d.layers, world)
-    elif args.split == "gateup":
-        ranges = P.gateup_split(d.layers, world, d.intermediate)
-    elif args.split == "sublayer":
-        ranges = P.sublayer_split(d.layers, world, d.intermediate)
+    elif args.split in ("gateup", "sublayer"):
+        ranges = sub_split(d, world, args.split == "sublayer")
     else:
         ranges = [P.StageRange.layers(f, k) for f, k in stage_split(d, world, B, ctx, args.split)]
     rg = ranges[rank]

@@ -307,6 +307,7 @@ struct Target {
 };
 
 int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t);
+bool owns_weight(const InferdSpan* s, int layer, const char* name);
 
 int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
   const InferdSpanConfig& c = s->cfg;
@@ -319,7 +320,9 @@ int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
   }
   if (layer >= c.n_layers) return fail(INFERD_ERR_ARG, "layer index out of span");
   if (resolve_layer(s, layer, name, t)) return INFERD_ERR_ARG;
-  if (!t->dst)
+  // by ownership, not by t->dst: a sub-tensor of an absent part (k_proj, up_proj) resolves to
+  // an offset from a null base
+  if (!owns_weight(s, layer, name))
     return fail(INFERD_ERR_ARG, std::string(name) + ": layer " + std::to_string(layer) +
                                     " of this span runs only its other half / part (skip_first_attn, skip_last_mlp, o_split_*)");
   return 0;

@@ -264,50 +264,99 @@ DECODE_MB_8B = {"attn_half": 221.6, "gateup": 202.2, "down": 101.6, "head": 1245
 DECODE_US_8B_O = 8.73
 
 
+def load_decode_costs(name: str = "qwen3_8b") -> dict:
+    """The measured stage-boundary cost table (tools/boundary_costs.py on an MI355X, B = 16, ctx
+    2048; profiles/r05/boundary_costs.json): us per decode-graph replay of small spans -- one
+    layer, an attention half, an MLP half starting at each gate/up column, an attention half
+    plus gate/up columns [0, c), the attention core, o + MLP, the head and the embedding."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", f"decode_costs_{name}.json")) as f:
+        c = json.load(f)
+    for k in ("mlp", "send"):
+        c[k] = {int(col): v for col, v in c[k].items()}
+    # the first stage (embedding, fed token ids) runs its layers ~3.5 % slower than the table's
+    # spans (fed random hidden states): stage 0 / the median of the other stages' measured /
+    # predicted ratio over the 8-stage splits of profiles/r05/stage_projection_sublayer.json
+    # (1.036 sublayer8, 1.044 gateup8, 1.030 balanced8, 1.030 halves8, 1.004 even8)
+    c.setdefault("first_scale", 1.035)
+    return c
+
+
 def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_US_8B, step: int = 256,
                  gateup_us: float = DECODE_US_8B_GATEUP, mb: dict = DECODE_MB_8B, o_cuts: bool = False,
-                 o_us: float = DECODE_US_8B_O):
+                 o_us: float = DECODE_US_8B_O, cal: dict | None = None):
     """Stages cut anywhere in the layer timeline a boundary may sit -- a layer start, or inside
     a layer's MLP before gate/up column c (c = 0: the half boundary; 0 < c < intermediate, a
     multiple of `step`: a gate/up boundary), and with o_cuts also between a layer's attention
     and its o projection -- so that the lowest stage's HBM fraction at the pipeline's tick,
     min_s bytes_s / max_s time_s, is the highest the time / byte model allows (an exact search:
     for a tick bound T the best split is a DP over the cut points; T on a 4-us grid from the
-    ideal total / n, then refined to 0.5 us).  Time model: costs (DECODE_US_8B) with the MLP
+    ideal total / n, then refined to 1 us).  Time model: costs (DECODE_US_8B) with the MLP
     half split into gate/up (gateup_us, linear in the columns) and down, and the attention half
     into its core and the o GEMV (o_us); bytes: mb.  Boundaries cannot sit inside the attention
-    itself (its K/V live where it runs)."""
+    itself (its K/V live where it runs).
+
+    cal (load_decode_costs(): measured stage times of small spans) replaces the time model: a
+    stage costs cal["stage"] + its full layers x cal["layer"] + the part of the layer it starts
+    in (o + MLP: cal["o_mlp"]; the MLP from gate/up column c: cal["mlp"][c]) + the part of the
+    layer it ends in (the attention core: cal["core"]; the attention half + gate/up columns
+    [0, c): cal["send"][c]) + head / embedding -- which prices what a boundary really costs
+    (the partial gate/up GEMV's wave quantisation, the extra launches)."""
     a, mlp, hd, sn = costs["attn_half"], costs["mlp_half"], costs["head"], costs["stage_norm"]
     ncol = intermediate // step
+    emb, fs = 0.0, 1.0
+    if cal is not None:
+        fs = cal.get("first_scale", 1.0)
+        assert all(k * step in cal["mlp"] and k * step in cal["send"] for k in range(ncol)), "cal: column grid"
+        sn, hd, emb, lay = cal["stage"], cal["head"], cal["embed"], cal["layer"]
     # cut points in timeline order: (layer, kind, col) -- kind "L" a layer start, "O" before the
     # layer's o projection, "G" inside its MLP before gate/up column col * step; time and bytes
-    # up to each cut
-    cuts, times, byts, t, y = [], [], [], 0.0, 0.0
+    # up to each cut.  A stage from cut j to cut l costs times[l] - times[j] + sadj[j] (the
+    # receiving side's correction, cal) + sn (+ head, + embedding)
+    cuts, times, byts, sadj, t, y = [], [], [], [], 0.0, 0.0
     for l in range(n_layers):
         cuts.append((l, "L", 0))
         times.append(t)
         byts.append(y)
+        sadj.append(0.0)
         if o_cuts:
             cuts.append((l, "O", 0))
-            times.append(t + a - o_us)
             byts.append(y + mb["attn_half"] - mb["o"])
-        t += a
+            if cal is None:
+                times.append(t + a - o_us)
+                sadj.append(0.0)
+            else:
+                times.append(t + cal["core"] - sn)
+                sadj.append((cal["o_mlp"] - sn) - (lay - (cal["core"] - sn)))
         y += mb["attn_half"]
         for k in range(ncol):
             cuts.append((l, "G", k))
-            times.append(t + gateup_us * k / ncol)
             byts.append(y + mb["gateup"] * k / ncol)
-        t += mlp
+            if cal is None:
+                times.append(t + a + gateup_us * k / ncol)
+                sadj.append(0.0)
+            else:
+                te = cal["send"][k * step] - sn
+                times.append(t + te)
+                sadj.append((cal["mlp"][k * step] - sn) - (lay - te))
+        t += (a + mlp) if cal is None else lay
         y += mb["gateup"] + mb["down"]
     cuts.append((n_layers, "L", 0))
     times.append(t)
     byts.append(y)
+    sadj.append(0.0)
+    # the search below needs cut times in order: measured send[c] is a staircase (wave
+    # quantisation), made non-decreasing here (a flat step costs the same wherever it is cut)
+    for i in range(1, len(times)):
+        times[i] = max(times[i], times[i - 1])
     P = len(cuts) - 1
 
     # for a tick bound T: f[l] = the highest min over the stages so far of bytes / T with the
     # last of them ending at cut l and every stage within T (numpy over the previous cut j)
     import numpy as np
-    tm, by = np.array(times), np.array(byts)
+    tm, by, sa = np.array(times), np.array(byts), np.array(sadj)
+    sa_lo = float(sa.min())
 
     def solve(T):
         """(value, boundary cuts) of the best split with every stage within T"""
@@ -316,16 +365,16 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
         arg = []
         for s in range(n):
             last = s == n - 1
-            extra = sn + (hd if last else 0.0)
+            extra = sn + (hd if last else 0.0) + (emb if s == 0 else 0.0)
             g = np.full(P + 1, -1.0)
             gi = np.zeros(P + 1, dtype=np.int64)
             ends = [P] if last else range(s + 1, P - (n - 1 - s) + 1)
             for l in ends:
-                j0 = max(int(np.searchsorted(tm, tm[l] - (T - extra), side="left")), s)
+                j0 = max(int(np.searchsorted(tm, tm[l] - (T / (fs if s == 0 else 1.0) - extra) + sa_lo, side="left")), s)
                 if j0 >= l:
                     continue
                 js = np.arange(j0, l)
-                fj = f[j0:l]
+                fj = np.where((tm[l] - tm[j0:l] + sa[j0:l] + extra) * (fs if s == 0 else 1.0) <= T, f[j0:l], -1.0)
                 v = np.where(fj >= 0, np.minimum(fj, (by[l] - by[j0:l] + (mb["head"] if last else 0.0)) / T), -1.0)
                 k = int(v.argmax())
                 g[l], gi[l] = v[k], js[k]
@@ -339,13 +388,13 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
             b.append(l)
         return float(f[P]), b[::-1]
     # the tick: coarse grid from the ideal (total / n), then refined around the best
-    lo_t = (times[P] + n * sn + hd) / n
+    lo_t = (times[P] + n * sn + hd + emb) / n
     best_val, best_b, best_T = -1.0, None, lo_t
-    for T in np.arange(lo_t, lo_t * 1.12, 4.0):
+    for T in np.arange(lo_t, lo_t * 1.08, 4.0):
         v, bb = solve(T)
         if v > best_val:
             best_val, best_b, best_T = v, bb, T
-    for T in np.arange(best_T - 4.0, best_T + 4.0, 0.5):
+    for T in np.arange(best_T - 4.0, best_T + 4.0, 1.0):
         v, bb = solve(T)
         if v > best_val:
             best_val, best_b = v, bb
@@ -363,6 +412,30 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
 def sublayer_split(n_layers: int, n: int, intermediate: int, **kw):
     """gateup_split with attention|o boundaries as cut points too."""
     return gateup_split(n_layers, n, intermediate, o_cuts=True, **kw)
+
+
+def predicted_stage_us(r: StageRange, cal: dict, first: bool, last: bool) -> float:
+    """A stage's decode-graph time on the measured cost table (load_decode_costs), us: the stage
+    overhead, its full layers, the layer it starts in part-way (o + MLP, or the MLP from gate/up
+    column first_col) and the one it ends in part-way (the attention core, or the attention half
+    + gate/up columns [0, last_col)), head and embedding."""
+    fs = cal.get("first_scale", 1.0) if first else 1.0
+    t = cal["stage"] + (cal["embed"] if first else 0.0) + (cal["head"] if last else 0.0)
+    l0, l1 = r.first_layer, r.last_layer
+    start = cal["o_mlp"] - cal["stage"] if r.first_o else \
+        (cal["mlp"][r.first_col] - cal["stage"] if r.skip_first_attn else None)
+    end = cal["core"] - cal["stage"] if r.last_o else \
+        (cal["send"][r.last_col] - cal["stage"] if r.skip_last_mlp else None)
+    if l0 == l1 and start is not None and end is not None:
+        # one layer, cut on both sides: its start part less what its end part leaves out
+        return fs * (t + start - (cal["layer"] - end))
+    full = r.n_layers - (start is not None) - (end is not None)
+    return fs * (t + full * cal["layer"] + (start or 0.0) + (end or 0.0))
+
+
+def measured_split(n_layers: int, n: int, intermediate: int, o_cuts: bool = True, name: str = "qwen3_8b", **kw):
+    """sublayer_split (or gateup_split) on the measured stage-boundary costs (load_decode_costs)."""
+    return gateup_split(n_layers, n, intermediate, o_cuts=o_cuts, cal=load_decode_costs(name), **kw)
 
 
 class SpanExecutor:

@@ -384,11 +384,9 @@ def _ranges(sizes):
     """StageRanges of a test split: stage sizes in layers (multiples of 0.5: half-layer
     boundaries), or "gateup8" -- bench.py --split gateup at 8 stages (boundaries inside gate/up
     projections, record hand-offs) -- or "sublayer8" (bench.py --split sublayer)"""
-    from inferd_amd.pipeline import gateup_split, ranges_from_sizes, sublayer_split
-    if sizes == "gateup8":
-        return gateup_split(36, 8, 12288)
-    if sizes == "sublayer8":      # bench.py --split sublayer: attention|o boundaries too
-        return sublayer_split(36, 8, 12288)
+    from inferd_amd.pipeline import measured_split, ranges_from_sizes
+    if sizes in ("gateup8", "sublayer8"):   # bench.py --split gateup / sublayer (bench.sub_split)
+        return measured_split(36, 8, 12288, o_cuts=sizes == "sublayer8")
     return ranges_from_sizes(sizes)
 
 
