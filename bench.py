@@ -266,6 +266,13 @@ def range_bytes(d, r, B: int, ctx_mean: float, lm_head: bool) -> float:
         nb -= attn - kb["o_gemm"]
     if r.last_o:
         nb -= kb["o_gemm"]
+    # q/k/v|attention boundaries (first_q / last_q): the norm and q/k/v GEMV before the cut, the
+    # attention and o after it
+    qkv = kb["rmsnorm"] + kb["qkv_gemm"]
+    if r.first_q:
+        nb -= qkv
+    if r.last_q:
+        nb -= attn - qkv
     return nb
 
 
@@ -290,17 +297,18 @@ def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int,
             ids = torch.randint(0, d.vocab, (len(reqs) * ctx,), generator=g, dtype=torch.int32)
             span.forward(reqs, ids=ids, want_hidden=False, want_next_ids=last)
         else:     # (a record x | attention output at an attention|o boundary)
-            n_in = buffer_elems(d, len(reqs) * ctx, 0, r.first_o, False)
+            n_in = buffer_elems(d, len(reqs) * ctx, 0, r.first_o, False, r.first_q)
             x = (torch.randn(n_in, generator=g) * 0.5).to(torch.bfloat16)
-            span.forward(reqs, x=x, want_hidden=r.last_o, want_next_ids=last)
+            span.forward(reqs, x=x, want_hidden=r.last_o or r.last_q, want_next_ids=last)
     ids = torch.zeros(B, dtype=torch.int32, device=dev) if first else None
     x = None if first else (torch.randn(B, d.hidden, generator=g) * 0.5).to(torch.bfloat16).to(dev)
-    if r.first_col or r.first_o:      # a record: h1 + the packed act, or x + the attention output
-        n_in = buffer_elems(d, B, r.first_col, r.first_o)
-        x = torch.cat([x.reshape(-1), (torch.randn(n_in - B * d.hidden, generator=g) * 0.5 if r.first_o else
-                                       torch.zeros(n_in - B * d.hidden)).to(torch.bfloat16).to(dev)])
-    hout = None if last else torch.empty(buffer_elems(d, B, r.last_col, r.last_o), dtype=torch.bfloat16,
-                                         device=dev)
+    if r.first_col or r.first_o or r.first_q:
+        # a record: h1 + the packed act, x + the attention output, or x + the q/k/v rows
+        n_in = buffer_elems(d, B, r.first_col, r.first_o, True, r.first_q)
+        x = torch.cat([x.reshape(-1), (torch.randn(n_in - B * d.hidden, generator=g) * 0.5 if (r.first_o or r.first_q)
+                                       else torch.zeros(n_in - B * d.hidden)).to(torch.bfloat16).to(dev)])
+    hout = None if last else torch.empty(buffer_elems(d, B, r.last_col, r.last_o, True, r.last_q),
+                                         dtype=torch.bfloat16, device=dev)
     nid = torch.empty(B, dtype=torch.int32, device=dev) if last else None
     graph = DecodeGraph(span, sess, warmup + reps, ids=ids, x=x, hidden_out=hout, next_ids=nid)
     for _ in range(warmup):
@@ -625,7 +633,7 @@ def main():
                        "global_batch": B * n_mb, "seq_len": ctx, "parallelism": f"pp{world}",
                        # layers per stage (a shared attention unit counts a quarter layer on each side)
                        "spans": [r.n_units / 2 + (r.last_col - r.first_col) / d.intermediate / 2 -
-                                 0.25 * (r.first_o + r.last_o) for r in ranges],
+                                 0.25 * (r.first_o + r.last_o + r.first_q + r.last_q) for r in ranges],
                        "stage_ranges": [r.label() for r in ranges]},
             "roofline": roof,
             "roofline_step": {"bound": "hbm", "alg_bytes_per_step": int(sb),

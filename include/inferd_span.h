@@ -63,7 +63,7 @@ typedef struct InferdSpanConfig {
   int32_t kv_pages;       /* KV pool capacity, in INFERD_KV_PAGE_TOKENS-token pages */
   int32_t max_tokens;     /* activation workspace rows (tokens per forward call) */
   int32_t max_seqs;       /* sequences per forward call */
-  /* Sub-layer stage boundaries (ABI 3).  The reference cuts spans at layer boundaries only
+  /* Sub-layer stage boundaries (ABI 3; q/k/v boundaries ABI 4).  The reference cuts spans at layer boundaries only
    * (split_model.py:92-108); a pipeline balanced to the last stage's lm_head needs a finer
    * cut.  A decoder layer (qwen3_server_module.py:179-206) is two halves: attention
    * (input_layernorm .. o_proj + residual) and MLP (post_attention_layernorm .. down_proj +
@@ -90,6 +90,16 @@ typedef struct InferdSpanConfig {
    * (every sequence one new token), row-major over n_tokens rows otherwise.  0 or 1. */
   int32_t o_split_first; /* the span starts at its first layer's o projection (x_in: the record) */
   int32_t o_split_last;  /* the span ends before its last layer's o projection (x_out: the record) */
+  /* A boundary between a layer's q/k/v projection and its attention kernel (ABI 4): the span
+   * before it runs that layer's input_layernorm and q/k/v projection, the span after it the
+   * attention (its K/V pages live there), o_proj and the MLP.  In a pure decode call the
+   * hand-off is a RECORD: the layer's input residual x bf16 [n_tokens][hidden] row-major,
+   * followed by the raw q/k/v projection output bf16 [n_tokens][(heads + 2 kv_heads) * 128]
+   * row-major (before QK-norm and RoPE: the receiver's attention applies them and writes the
+   * cache).  Other calls hand over x only and the receiving span runs the whole layer (it owns
+   * the layer's input_layernorm and q/k/v weights too).  0 or 1. */
+  int32_t qkv_split_first; /* the span starts at its first layer's attention (x_in: the record) */
+  int32_t qkv_split_last;  /* the span ends after its last layer's q/k/v projection (x_out: the record) */
 } InferdSpanConfig;
 
 /* One forward call's batch: n_seqs sequences, their new tokens concatenated

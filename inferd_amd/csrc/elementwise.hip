@@ -352,3 +352,31 @@ __global__ void argmax_decode_kernel(const unsigned long long* __restrict__ keys
 void launch_argmax_decode(const unsigned long long* keys, int B, int32_t* ids, hipStream_t s) {
   hipLaunchKernelGGL(argmax_decode_kernel, dim3((B + 63) / 64), dim3(64), 0, s, keys, B, ids);
 }
+
+// ------------------------------------------------------------------ q/k/v slice reduction
+// The bf16 q/k/v rows of a decode call from the split-K projection's fp32 slices
+// (launch_gemm_decode_partial: [ksl][M][N]), summed exactly as the fused decode attention sums
+// them (attention.hip qkv8: 0 + slice 0 + ... + slice 3, zeros past ksl, rounded once) -- the
+// raw q/k/v part of a q/k/v|attention boundary's record.
+__global__ __launch_bounds__(256) void qkv_reduce_kernel(const float* __restrict__ part, int ksl, int M, int N,
+                                                         u16* __restrict__ out) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const int64_t n = (int64_t)M * N;
+  if (i >= n) return;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+    const f32x4 p = sl < ksl ? *(const f32x4*)(part + (int64_t)sl * n + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += p[j];
+  }
+  u16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = f2bf(acc[j]);
+  *(u16x4*)(out + i) = o;
+}
+
+void launch_qkv_reduce(const float* part, int ksl, int M, int N, u16* out, hipStream_t s) {
+  const int64_t n4 = ((int64_t)M * N + 3) / 4;
+  hipLaunchKernelGGL(qkv_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, part, ksl, M, N, out);
+}

@@ -54,6 +54,9 @@ struct NormPrologue {
 };
 // the same prologue work (scheduler step, SSQ slot zeroing for rows < M <= 64) as a launch of its
 // own, for a span whose first launch is not an RMSNorm
+// bf16 q/k/v rows from decode split-K slices ([ksl][M][N] fp32, M * N % 4 == 0), summed in the
+// fused decode attention's order
+void launch_qkv_reduce(const float* part, int ksl, int M, int N, u16* out, hipStream_t s);
 void launch_step_prologue(unsigned long long* zero_slots, int n_slots, int M, const NormPrologue* pro,
                           hipStream_t s);
 // zero_slots: rows < M of n_slots SSQ slots (kernels.h DecodeNorm) are zeroed too, or null

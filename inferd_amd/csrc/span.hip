@@ -49,7 +49,7 @@ int inferd_fail(int code, const std::string& msg) { return fail(code, msg); }
   } while (0)
 
 extern "C" const char* inferd_last_error(void) { return g_err.c_str(); }
-extern "C" int inferd_abi_version(void) { return 3; }
+extern "C" int inferd_abi_version(void) { return 4; }
 
 namespace {
 
@@ -150,14 +150,21 @@ struct InferdSpan {
   int qkv_rows() const { return (cfg.heads + 2 * cfg.kv_heads) * HEAD_DIM; }
   // the halves of span-local layer l this span runs (InferdSpanConfig skip_first_attn /
   // skip_last_mlp); only layers with an attention half own a KV pool layer
-  // has_attn: input_layernorm, q/k/v and the attention kernel; has_o: o_proj + residual
+  // has_qkv: input_layernorm + q/k/v weights; has_attn: the attention kernel and a KV pool
+  // layer; has_o: o_proj + residual
   bool first_no_attn() const { return cfg.skip_first_attn || cfg.o_split_first; }
-  bool has_attn(int l) const { return !(l == 0 && first_no_attn()); }
-  bool has_o(int l) const { return !(l == 0 && cfg.skip_first_attn) && !(l == cfg.n_layers - 1 && cfg.o_split_last); }
-  bool has_mlp(int l) const { return !(l == cfg.n_layers - 1 && (cfg.skip_last_mlp || cfg.o_split_last)); }
+  bool last_qkv_only(int l) const { return l == cfg.n_layers - 1 && cfg.qkv_split_last; }
+  bool has_qkv(int l) const { return !(l == 0 && first_no_attn()); }
+  bool has_attn(int l) const { return has_qkv(l) && !last_qkv_only(l); }
+  bool has_o(int l) const {
+    return !(l == 0 && cfg.skip_first_attn) && !(l == cfg.n_layers - 1 && cfg.o_split_last) && !last_qkv_only(l);
+  }
+  bool has_mlp(int l) const {
+    return !(l == cfg.n_layers - 1 && (cfg.skip_last_mlp || cfg.o_split_last)) && !last_qkv_only(l);
+  }
   // the last layer of a span that ends inside the layer's gate/up projection computes part of it
   bool has_gateup(int l) const { return has_mlp(l) || (l == cfg.n_layers - 1 && cfg.gateup_split_last); }
-  int kv_layers() const { return cfg.n_layers - (first_no_attn() ? 1 : 0); }
+  int kv_layers() const { return cfg.n_layers - (first_no_attn() ? 1 : 0) - (cfg.qkv_split_last ? 1 : 0); }
   u16* kv_of(int l) const { return kv_pool + kv_layer_elems * (l - (first_no_attn() ? 1 : 0)); }
 };
 
@@ -201,8 +208,17 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
                                 "embedding (first) and lm_head (last)");
   if ((c.o_split_first || c.o_split_last) && c.n_layers < 1)
     return fail(INFERD_ERR_ARG, "an attention|o boundary needs n_layers >= 1");
+  if ((c.qkv_split_first | c.qkv_split_last) & ~1) return fail(INFERD_ERR_ARG, "qkv_split_first / qkv_split_last are 0 or 1");
+  if ((c.qkv_split_first && (c.skip_first_attn || c.o_split_first || c.has_embed)) ||
+      (c.qkv_split_last && (c.skip_last_mlp || c.o_split_last || c.has_lm_head)))
+    return fail(INFERD_ERR_ARG, "a q/k/v|attention boundary excludes another sub-layer boundary at the same end, the "
+                                "embedding (first) and lm_head (last)");
+  if ((c.qkv_split_first || c.qkv_split_last) && c.n_layers < 1)
+    return fail(INFERD_ERR_ARG, "a q/k/v|attention boundary needs n_layers >= 1");
   if (c.n_layers == 1 && ((c.o_split_first && (c.o_split_last || c.skip_last_mlp)) ||
-                          (c.o_split_last && c.skip_first_attn)))
+                          (c.o_split_last && c.skip_first_attn) ||
+                          (c.qkv_split_last && (c.skip_first_attn || c.o_split_first || c.qkv_split_first)) ||
+                          (c.qkv_split_first && c.o_split_last)))
     return fail(INFERD_ERR_ARG, "a one-layer span cannot end before the part it starts at");
   InferdSpan* s = new InferdSpan();
   s->cfg = c;
@@ -220,7 +236,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   } while (0)
   for (int l = 0; l < c.n_layers; ++l) {
     LayerW& L = s->layers[l];
-    if (s->has_attn(l)) {
+    if (s->has_qkv(l)) {
       SALLOC(L.qkv, (size_t)s->qkv_rows() * h * 2);
       SALLOC(L.in_ln, (size_t)h * 2);
       SALLOC(L.q_norm, HEAD_DIM * 2);
@@ -324,7 +340,8 @@ int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
   // an offset from a null base
   if (!owns_weight(s, layer, name))
     return fail(INFERD_ERR_ARG, std::string(name) + ": layer " + std::to_string(layer) +
-                                    " of this span runs only its other half / part (skip_first_attn, skip_last_mlp, o_split_*)");
+                                    " of this span runs only its other half / part (skip_first_attn, skip_last_mlp, o_split_*, "
+                                    "qkv_split_last)");
   return 0;
 }
 
@@ -353,7 +370,7 @@ bool owns_weight(const InferdSpan* s, int layer, const char* name) {
   if (!strcmp(name, "o_proj")) return s->has_o(layer);
   if (!strcmp(name, "gate_proj") || !strcmp(name, "up_proj") || !strcmp(name, "post_attention_layernorm"))
     return s->has_gateup(layer);
-  return s->has_attn(layer);
+  return s->has_qkv(layer);
 }
 // packed sub-blocks start at an n-tile boundary: offset rows*K elements == (rows/16)*KT*512
 }  // namespace
@@ -471,8 +488,8 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   }
   if (M <= 64 && c.gateup_split_first && !x_in)
     return fail(INFERD_ERR_ARG, "a span starting inside a gate/up projection needs x_in (the hand-off record)");
-  if (c.o_split_last && !x_out)
-    return fail(INFERD_ERR_ARG, "a span ending before an o projection needs x_out (the hand-off record)");
+  if ((c.o_split_last || c.qkv_split_last) && !x_out)
+    return fail(INFERD_ERR_ARG, "a span ending before an o projection or an attention needs x_out (the hand-off record)");
   if (c.has_embed) {
     if (!ids) return fail(INFERD_ERR_ARG, "first span needs token ids");
     if (c.n_layers > 0) {
@@ -506,9 +523,14 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
   // decode: the attention output goes to the o projection's GEMV fragment-packed (also the
   // layout of an attention|o boundary record's second part)
   const bool pk_o = b->decode && gemv && !gemm_uses_tiled(M, h, H * HEAD_DIM, EPI_RESID);
-  if (c.o_split_first && c.n_layers > 0 && (gemv || pro.positions)) {
-    // a span starting at an o projection has no first RMSNorm launch to carry the graph's
-    // scheduler step and the SSQ slot zeroing: a small launch of its own
+  // a q/k/v|attention boundary: a pure decode call hands over the raw q/k/v rows behind x
+  // (qkv_split_*); other calls hand over x and the receiver runs the whole layer
+  const bool qrec = b->decode;
+  const bool q_in = c.qkv_split_first && qrec;
+  if ((c.o_split_first || q_in) && c.n_layers > 0 && (gemv || pro.positions)) {
+    // a span starting at an o projection (or, decoding, at an attention) has no first RMSNorm
+    // launch to carry the graph's scheduler step and the SSQ slot zeroing: a small launch of
+    // its own
     launch_step_prologue(gemv ? s->ssq : nullptr, 2 * c.n_layers, M, &pro, st);
     pro = NormPrologue{};
   }
@@ -519,7 +541,7 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // of the hand-off record
     u16* out = (l == c.n_layers - 1 && x_out) ? (u16*)x_out : s->h;
     bool out_packed = pkx && l < c.n_layers - 1;
-    if (c.o_split_last && l == c.n_layers - 2) {
+    if ((c.o_split_last || c.qkv_split_last) && l == c.n_layers - 2) {
       out = (u16*)x_out;
       out_packed = false;
     }
@@ -559,55 +581,78 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     // the attention output the o projection reads: this layer's, or (a span starting at an o
     // projection) the record's second part
     const u16* attn_src = s->attn;
-    if (!s->has_attn(l)) {  // o_split_first, layer 0: x is the record's residual part
+    if (l == 0 && c.o_split_first) {  // x is the record's residual part
       attn_src = (const u16*)x_in + (size_t)M * h;
       goto o_proj;
     }
     {
-    u16* kv_l = s->kv_of(l);
+    // a q/k/v|attention boundary: q_only -- this (last) layer runs its norm and q/k/v
+    // projection only, into the record behind x (pure decode calls; other calls hand over x
+    // alone); q_recv -- this (first) layer's q/k/v rows arrive in x_in's record
+    const bool q_only = s->last_qkv_only(l);
+    const bool q_recv = l == 0 && q_in;
+    u16* kv_l = q_only ? nullptr : s->kv_of(l);
+    u16* q_dst = q_only ? (u16*)x_out + (size_t)M * h : nullptr;
     // decode: QK-norm + RoPE + the cache write run inside the attention
     const bool fused = b->decode;
     // a span ending before this layer's o projection: the attention writes the record's second
     // part, behind the layer's input residual (row-major; copied there when it is the span's input)
     u16* attn_dst = s->attn;
-    if (!s->has_o(l)) attn_dst = (u16*)x_out + (size_t)M * h;
+    if (!s->has_o(l) && !q_only) attn_dst = (u16*)x_out + (size_t)M * h;
     // decode q/k/v K-slices (reduced inside the fused attention): M <= 16 and K/32 divisible
     // by 4 * slices
     int ksl = (fused && M <= 16) ? QKV_KSL : 1;
     if ((h / 32) % (4 * ksl)) ksl = 1;
-    // ---- input_layernorm -> q/k/v projection
+    // ---- input_layernorm -> q/k/v projection (not on a layer whose q/k/v rows arrive in the
+    // record; on a q_only layer of a call that hands over x alone, only the span's first norm
+    // launch when it carries the prologue: the embedding / scheduler step)
     const u16* a_in = x;
-    DecodeNorm dn = {DN_NONE, c.rms_eps, nullptr, nullptr};
-    if (gemv && l > 0) {
-      dn = {DN_EXACT, c.rms_eps, slot(2 * l - 1), W.in_ln};
-    } else {
-      pe = s->prof_begin(PROF_NORM, st);
-      launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st, false, gemv ? s->ssq : nullptr,
-                     2 * c.n_layers, l == 0 ? &pro : nullptr);
-      s->prof_end(pe, st);
-      a_in = s->xn;
-    }
-    pe = s->prof_begin(PROF_QKV, st);
-    // prefill: q/k norm + RoPE and the K/V cache write in the projection's epilogue when
-    // the persistent GEMM runs it (else the separate qk_norm_rope_kv launch below)
     bool qkv_done = false;
-    if (ksl > 1) {
-      launch_gemm_decode_partial(a_in, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, dn, st,
-                                 (x_packed && a_in == x) ? GEMM_PACK_A : 0);
-    } else {
-      if (!b->decode) {
-        const QkvEpilogue qe = {b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t, s->sin_t, s->q, kv_l,
-                                H, KV, c.rms_eps};
-        qkv_done = launch_gemm_qkv_fused(a_in, h, W.qkv, M, qkvN, h, qe, st);
+    if (!q_recv) {
+      DecodeNorm dn = {DN_NONE, c.rms_eps, nullptr, nullptr};
+      if (gemv && l > 0) {
+        dn = {DN_EXACT, c.rms_eps, slot(2 * l - 1), W.in_ln};
+      } else if (!(q_only && !qrec && l > 0)) {
+        pe = s->prof_begin(PROF_NORM, st);
+        launch_rmsnorm(x, h, nullptr, 0, W.in_ln, s->xn, h, M, h, c.rms_eps, st, false, gemv ? s->ssq : nullptr,
+                       2 * c.n_layers, l == 0 ? &pro : nullptr);
+        s->prof_end(pe, st);
+        a_in = s->xn;
       }
-      if (!qkv_done)
-        GEMM_TRY(launch_gemm(a_in, h, W.qkv, M, qkvN, h, s->qkv, qkvN, nullptr, 0, EPI_NONE, nullptr, st, &s->gws, &dn,
-                    nullptr, (x_packed && a_in == x) ? GEMM_PACK_A : 0));
+      if (!(q_only && !qrec)) {
+        pe = s->prof_begin(PROF_QKV, st);
+        // prefill: q/k norm + RoPE and the K/V cache write in the projection's epilogue when
+        // the persistent GEMM runs it (else the separate qk_norm_rope_kv launch below)
+        if (ksl > 1) {
+          launch_gemm_decode_partial(a_in, h, W.qkv, M, qkvN, h, ksl, s->qkv_part, dn, st,
+                                     (x_packed && a_in == x) ? GEMM_PACK_A : 0);
+          // the record's q/k/v rows: the slices summed as the fused attention sums them
+          if (q_only) launch_qkv_reduce(s->qkv_part, ksl, M, qkvN, q_dst, st);
+        } else {
+          if (!b->decode && !q_only) {
+            const QkvEpilogue qe = {b->positions, b->slots, W.q_norm, W.k_norm, s->cos_t, s->sin_t, s->q, kv_l,
+                                    H, KV, c.rms_eps};
+            qkv_done = launch_gemm_qkv_fused(a_in, h, W.qkv, M, qkvN, h, qe, st);
+          }
+          if (!qkv_done)
+            GEMM_TRY(launch_gemm(a_in, h, W.qkv, M, qkvN, h, q_only ? q_dst : s->qkv, qkvN, nullptr, 0, EPI_NONE,
+                                 nullptr, st, &s->gws, &dn, nullptr, (x_packed && a_in == x) ? GEMM_PACK_A : 0));
+        }
+        s->prof_end(pe, st);
+      }
     }
-    s->prof_end(pe, st);
+    if (q_only) {  // the record: x (first part; the span's input copied there), q/k/v rows
+      if (c.n_layers == 1 && x != (const u16*)x_out)
+        HIP_TRY(hipMemcpyAsync(x_out, x, (size_t)M * h * 2, hipMemcpyDeviceToDevice, st));
+      LAUNCH_CHECK();
+      continue;
+    }
     if (fused) {  // QK-norm + RoPE + cache write inside attention
       pe = s->prof_begin(PROF_ATTN, st);
-      if (ksl > 1)
+      if (q_recv)
+        launch_attn_decode_fused((const u16*)x_in + (size_t)M * h, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t,
+                                 c.rms_eps, kv_l, ab, H, KV, scale, attn_dst, s->attn_ws, st, nullptr, 0, pk_o);
+      else if (ksl > 1)
         launch_attn_decode_fused(nullptr, qkvN, W.q_norm, W.k_norm, s->cos_t, s->sin_t, c.rms_eps, kv_l, ab, H, KV,
                                  scale, attn_dst, s->attn_ws, st, s->qkv_part, ksl, pk_o);
       else

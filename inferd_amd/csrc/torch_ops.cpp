@@ -83,8 +83,15 @@ void check_forward_args(const InferdSpanConfig& c, const at::Tensor& words, cons
   check_arg(ids, dev, at::kInt, M, "ids");
   // attention|o boundaries: x then the attention output (16-row tiles in a pure decode call)
   const int64_t orec = (b.decode && dec ? (M + 15) / 16 * 16 : M) * (int64_t)c.heads * c.head_dim;
-  check_arg(x, dev, at::kBFloat16, M * h + (dec && c.gateup_split_first ? rec : 0) + (c.o_split_first ? orec : 0), "x");
-  check_arg(x_out, dev, at::kBFloat16, M * h + (dec && c.gateup_split_last ? rec : 0) + (c.o_split_last ? orec : 0),
+  // q/k/v|attention boundaries: x then the raw q/k/v rows (pure decode calls; else x only)
+  const int64_t qrec = b.decode ? M * (int64_t)(c.heads + 2 * c.kv_heads) * c.head_dim : 0;
+  check_arg(x, dev, at::kBFloat16,
+            M * h + (dec && c.gateup_split_first ? rec : 0) + (c.o_split_first ? orec : 0) +
+                (c.qkv_split_first ? qrec : 0),
+            "x");
+  check_arg(x_out, dev, at::kBFloat16,
+            M * h + (dec && c.gateup_split_last ? rec : 0) + (c.o_split_last ? orec : 0) +
+                (c.qkv_split_last ? qrec : 0),
             "x_out");
   check_arg(next_ids, dev, at::kInt, B, "next_ids");
   check_arg(logits, dev, at::kBFloat16, B * (int64_t)c.vocab, "logits");
@@ -94,18 +101,19 @@ void check_forward_args(const InferdSpanConfig& c, const at::Tensor& words, cons
 // ---- span lifetime ------------------------------------------------------------------------
 // cfg: [hidden, intermediate, heads, kv_heads, head_dim, vocab, first_layer, n_layers, has_embed,
 //       has_lm_head, max_positions, kv_pages, max_tokens, max_seqs, skip_first_attn, skip_last_mlp,
-//       gateup_split_first, gateup_split_last, o_split_first, o_split_last]
+//       gateup_split_first, gateup_split_last, o_split_first, o_split_last, qkv_split_first,
+//       qkv_split_last]
 // (the sub-layer boundary fields may be omitted: 14 ints = whole layers)
 int64_t span_create(at::IntArrayRef cfg, double rms_eps, double rope_theta, at::Device device) {
-  TORCH_CHECK(cfg.size() == 14 || cfg.size() == 16 || cfg.size() == 18 || cfg.size() == 20,
-              "span_create: 14, 16, 18 or 20 config ints");
+  TORCH_CHECK(cfg.size() >= 14 && cfg.size() <= 22 && cfg.size() % 2 == 0, "span_create: 14 .. 22 config ints");
   auto opt = [&](size_t i) { return cfg.size() > i ? (int32_t)cfg[i] : 0; };
   TORCH_CHECK(device.is_cuda(), "span_create: a GPU device");
   c10::hip::HIPGuard g(device.index());
   InferdSpanConfig c{(int32_t)cfg[0], (int32_t)cfg[1], (int32_t)cfg[2], (int32_t)cfg[3], (int32_t)cfg[4],
                      (int32_t)cfg[5], (int32_t)cfg[6], (int32_t)cfg[7], (int32_t)cfg[8], (int32_t)cfg[9],
                      (float)rms_eps, (float)rope_theta, (int32_t)cfg[10], (int32_t)cfg[11], (int32_t)cfg[12],
-                     (int32_t)cfg[13], opt(14), opt(15), opt(16), opt(17), opt(18), opt(19)};
+                     (int32_t)cfg[13], opt(14), opt(15), opt(16), opt(17), opt(18), opt(19), opt(20),
+                     opt(21)};
   InferdSpan* s = nullptr;
   ok(inferd_span_create(&c, &s), "span_create");
   return reinterpret_cast<int64_t>(s);
@@ -118,7 +126,7 @@ std::vector<int64_t> span_config(int64_t span) {
   return {c.hidden, c.intermediate, c.heads, c.kv_heads, c.head_dim, c.vocab, c.first_layer, c.n_layers,
           c.has_embed, c.has_lm_head, c.max_positions, c.kv_pages, c.max_tokens, c.max_seqs,
           c.skip_first_attn, c.skip_last_mlp, c.gateup_split_first, c.gateup_split_last, c.o_split_first,
-          c.o_split_last};
+          c.o_split_last, c.qkv_split_first, c.qkv_split_last};
 }
 
 void span_init_synthetic(int64_t span, int64_t seed, at::Device device) {

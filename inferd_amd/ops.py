@@ -41,9 +41,10 @@ PROF_CLASSES = _lib.PROF_CLASSES    # span_profile_stop's kernel classes (INFERD
 def span_config(dims, first_layer: int, n_layers: int, *, has_embed: bool, has_lm_head: bool, kv_pages: int,
                 max_tokens: int, max_seqs: int, max_positions: int, skip_first_attn: bool = False,
                 skip_last_mlp: bool = False, gateup_split_first: int = 0, gateup_split_last: int = 0,
-                o_split_first: bool = False, o_split_last: bool = False) -> list:
-    """The 20 config ints of span_create (InferdSpanConfig order)."""
+                o_split_first: bool = False, o_split_last: bool = False, qkv_split_first: bool = False,
+                qkv_split_last: bool = False) -> list:
+    """The 22 config ints of span_create (InferdSpanConfig order)."""
     return [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
             n_layers, int(has_embed), int(has_lm_head), max_positions, kv_pages, max_tokens, max_seqs,
             int(skip_first_attn), int(skip_last_mlp), int(gateup_split_first), int(gateup_split_last),
-            int(o_split_first), int(o_split_last)]
+            int(o_split_first), int(o_split_last), int(qkv_split_first), int(qkv_split_last)]

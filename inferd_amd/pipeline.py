@@ -41,24 +41,37 @@ def record_elems(dims, rows: int) -> int:
     return rows * dims.hidden + (rows + 15) // 16 * 16 * dims.intermediate
 
 
-def handoff_elems(dims, rows: int, col: int, o: bool = False, packed: bool = True) -> int:
-    """Elements of a hand-off that carry data: at an attention|o boundary (o) the whole record
-    (o_record_elems; packed: a pure decode call); else h1 alone (col = 0, a layer or half-layer
-    boundary, or a call of more than 64 rows), else h1 plus the act columns [0, col) -- for <= 16
-    rows those are one contiguous prefix of the packed act (a 16-row tile's columns [0, col) are
-    its first 16 * col elements), for more rows the whole record."""
+def q_record_elems(dims, rows: int, pure: bool) -> int:
+    """bf16 elements of a q/k/v|attention-boundary hand-off of `rows` token rows: x
+    [rows][hidden], then -- a pure decode call -- the raw q/k/v rows [rows][(heads + 2 kv_heads)
+    * head_dim] (InferdSpanConfig qkv_split_*)."""
+    return rows * dims.hidden + (rows * (dims.heads + 2 * dims.kv_heads) * dims.head_dim if pure else 0)
+
+
+def handoff_elems(dims, rows: int, col: int, o: bool = False, pure: bool = True, q: bool = False) -> int:
+    """Elements of a hand-off that carry data (pure: a pure decode call, every sequence one new
+    token): at an attention|o boundary (o) the whole record (o_record_elems, packed in a pure
+    decode call of <= 64 rows); at a q/k/v|attention boundary (q) q_record_elems; else h1 alone
+    (col = 0, a layer or half-layer boundary, or a call of more than 64 rows), else h1 plus the
+    act columns [0, col) -- for <= 16 rows those are one contiguous prefix of the packed act (a
+    16-row tile's columns [0, col) are its first 16 * col elements), for more rows the whole
+    record."""
     if o:
-        return o_record_elems(dims, rows, packed)
+        return o_record_elems(dims, rows, pure and rows <= 64)
+    if q:
+        return q_record_elems(dims, rows, pure)
     if not col or rows > 64:
         return rows * dims.hidden
     return rows * dims.hidden + 16 * col if rows <= 16 else record_elems(dims, rows)
 
 
-def buffer_elems(dims, rows: int, col: int, o: bool = False, packed: bool = True) -> int:
+def buffer_elems(dims, rows: int, col: int, o: bool = False, pure: bool = True, q: bool = False) -> int:
     """Elements of the buffer a stage boundary's hand-off lands in (the whole record, of which
     handoff_elems carries data; rows * hidden at a layer or half-layer boundary)."""
     if o:
-        return o_record_elems(dims, rows, packed)
+        return o_record_elems(dims, rows, pure and rows <= 64)
+    if q:
+        return q_record_elems(dims, rows, pure)
     return record_elems(dims, rows) if col and rows <= 64 else rows * dims.hidden
 
 
@@ -143,57 +156,80 @@ class StageRange:
     (InferdSpanConfig o_split_*): unit 2l then belongs to both stages -- the one before runs its
     norm, q/k/v and attention (its K/V live there), the one after its o projection -- and the
     hand-off is the record (x, attention output).  A first_o stage starts at unit 2l, a last_o
-    stage ends after unit 2l."""
-    __slots__ = ("first_unit", "n_units", "first_col", "last_col", "first_o", "last_o")
+    stage ends after unit 2l.
+    first_q / last_q: likewise a boundary between layer l's q/k/v projection and its attention
+    (InferdSpanConfig qkv_split_*): the stage before runs the norm and q/k/v, the one after the
+    attention (its K/V live there), o and the MLP; the hand-off is (x, the raw q/k/v rows) in a
+    pure decode call, x alone otherwise."""
+    __slots__ = ("first_unit", "n_units", "first_col", "last_col", "first_o", "last_o", "first_q", "last_q")
 
     def __init__(self, first_unit: int, n_units: int, first_col: int = 0, last_col: int = 0,
-                 first_o: bool = False, last_o: bool = False):
+                 first_o: bool = False, last_o: bool = False, first_q: bool = False, last_q: bool = False):
         assert first_unit >= 0 and n_units >= 1
         self.first_unit, self.n_units = first_unit, n_units
         self.first_col, self.last_col = first_col, last_col
         self.first_o, self.last_o = bool(first_o), bool(last_o)
+        self.first_q, self.last_q = bool(first_q), bool(last_q)
+        assert not (first_o and first_q) and not (last_o and last_q)
         assert not first_col or self.skip_first_attn, "first_col refines a stage that starts at an MLP half"
         assert not last_col or self.skip_last_mlp, "last_col refines a stage that ends after an attention half"
-        assert not first_o or first_unit % 2 == 0, "first_o: the stage starts in an attention unit"
-        assert not last_o or (first_unit + n_units) % 2 == 1, "last_o: the stage ends in an attention unit"
-        assert not (first_o and last_o and n_units == 1), "a stage of one attention unit's o alone and its core"
+        assert not (first_o or first_q) or first_unit % 2 == 0, "first_o / first_q: the stage starts in an attention unit"
+        assert not (last_o or last_q) or (first_unit + n_units) % 2 == 1, \
+            "last_o / last_q: the stage ends in an attention unit"
+        assert not ((first_o or first_q) and (last_o or last_q) and n_units == 1), \
+            "a stage that starts and ends inside one attention unit"
 
     @classmethod
     def layers(cls, first_layer: int, n_layers: int) -> "StageRange":
         return cls(2 * first_layer, 2 * n_layers)
 
+    @classmethod
+    def from_label(cls, label: str) -> "StageRange":
+        """Inverse of label(): e.g. '4m@12032..9a+4096', '14o..18', '9m@768..14q'."""
+        import re
+        m = re.fullmatch(r"(\d+)(m?)(o?)(k?)(?:@(\d+))?\.\.(\d+)(a?)(q?)(v?)(?:\+(\d+))?", label)
+        if not m:
+            raise ValueError(f"not a stage label: {label}")
+        l0, m0, o0, k0, c0, l1, a1, q1, v1, c1 = m.groups()
+        first = 2 * int(l0) + (1 if m0 else 0)
+        end = 2 * int(l1) + (1 if (a1 or q1 or v1) else 2)
+        return cls(first, end - first, int(c0 or 0), int(c1 or 0), bool(o0), bool(q1), bool(k0), bool(v1))
+
     first_layer = property(lambda self: self.first_unit // 2)
     last_layer = property(lambda self: (self.first_unit + self.n_units - 1) // 2)
     n_layers = property(lambda self: self.last_layer - self.first_layer + 1)
     skip_first_attn = property(lambda self: self.first_unit % 2 == 1)
-    skip_last_mlp = property(lambda self: (self.first_unit + self.n_units) % 2 == 1 and not self.last_o)
-    # the next stage's first_unit (a last_o stage shares its last unit with the next stage)
-    end_unit = property(lambda self: self.first_unit + self.n_units - (1 if self.last_o else 0))
+    skip_last_mlp = property(lambda self: (self.first_unit + self.n_units) % 2 == 1 and not (self.last_o or self.last_q))
+    # the next stage's first_unit (a last_o / last_q stage shares its last unit with the next stage)
+    end_unit = property(lambda self: self.first_unit + self.n_units - (1 if (self.last_o or self.last_q) else 0))
 
     def label(self) -> str:
         """e.g. '4m..8' = layer 4's MLP half through layer 8; '9..13a' ends with 13's attention
         half; '13m@6144..' / '..13a+6144': a gate/up boundary at column 6144 of layer 13;
-        '13o..' / '..13q': an attention|o boundary in layer 13"""
+        '13o..' / '..13q': an attention|o boundary in layer 13; '13k..' / '..13v': a
+        q/k/v|attention boundary"""
         a = (f"{self.first_layer}{'m' if self.skip_first_attn else ''}{'o' if self.first_o else ''}"
-             f"{f'@{self.first_col}' if self.first_col else ''}")
+             f"{'k' if self.first_q else ''}{f'@{self.first_col}' if self.first_col else ''}")
         b = (f"{self.last_layer}{'a' if self.skip_last_mlp else ''}{'q' if self.last_o else ''}"
-             f"{f'+{self.last_col}' if self.last_col else ''}")
+             f"{'v' if self.last_q else ''}{f'+{self.last_col}' if self.last_col else ''}")
         return f"{a}..{b}"
 
     def span_kwargs(self) -> dict:
         """The SpanRuntime / PipelineStage keyword arguments of this range's boundaries."""
         return {"skip_first_attn": self.skip_first_attn, "skip_last_mlp": self.skip_last_mlp,
                 "gateup_split_first": self.first_col, "gateup_split_last": self.last_col,
-                "o_split_first": self.first_o, "o_split_last": self.last_o}
+                "o_split_first": self.first_o, "o_split_last": self.last_o,
+                "qkv_split_first": self.first_q, "qkv_split_last": self.last_q}
 
     def _key(self):
-        return (self.first_unit, self.n_units, self.first_col, self.last_col, self.first_o, self.last_o)
+        return (self.first_unit, self.n_units, self.first_col, self.last_col, self.first_o, self.last_o,
+                self.first_q, self.last_q)
 
     def __eq__(self, o):
         return isinstance(o, StageRange) and o._key() == self._key()
 
     def __repr__(self):
-        return "StageRange({}, {}, {}, {}, {}, {})".format(*self._key())
+        return "StageRange({}, {}, {}, {}, {}, {}, {}, {})".format(*self._key())
 
 
 def ranges_from_sizes(sizes) -> list:
@@ -259,9 +295,11 @@ DECODE_US_8B_GATEUP = 33.57
 # algorithmic decode bytes per unit at Qwen3-8B, B = 16, ctx 2k (bench.py kernel_bytes), MB: the
 # attention half (norm, q/k/v, attention, o), the gate/up projection, the down projection, the
 # last stage's final norm + lm_head
-DECODE_MB_8B = {"attn_half": 221.6, "gateup": 202.2, "down": 101.6, "head": 1245.0, "o": 33.9}
-# the o GEMV's share of the attention half (profiles/r04/decode_kernel_trace.json), us
+DECODE_MB_8B = {"attn_half": 221.6, "gateup": 202.2, "down": 101.6, "head": 1245.0, "o": 33.9, "qkv": 52.7}
+# the o GEMV's and the (norm +) q/k/v GEMV's shares of the attention half
+# (profiles/r04/decode_kernel_trace.json), us
 DECODE_US_8B_O = 8.73
+DECODE_US_8B_QKV = 12.70
 
 
 def load_decode_costs(name: str = "qwen3_8b") -> dict:
@@ -273,24 +311,42 @@ def load_decode_costs(name: str = "qwen3_8b") -> dict:
     import os
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", f"decode_costs_{name}.json")) as f:
         c = json.load(f)
+    return apply_cost_fit(c)
+
+
+def apply_cost_fit(c: dict) -> dict:
+    """The cost table with its "projection_fit" (tools/fit_decode_costs.py: a least-squares fit
+    of whole-stage measurements, bench.py --mode stages) applied: every table entry is a stage
+    overhead plus content, content x content_scale, the overhead -> the fitted stage cost, the
+    head x head_scale, and first_scale for the first stage (embedding, fed token ids)."""
+    c = dict(c)
     for k in ("mlp", "send"):
         c[k] = {int(col): v for col, v in c[k].items()}
-    # the first stage (embedding, fed token ids) runs its layers ~3.5 % slower than the table's
-    # spans (fed random hidden states): stage 0 / the median of the other stages' measured /
-    # predicted ratio over the 8-stage splits of profiles/r05/stage_projection_sublayer.json
-    # (1.036 sublayer8, 1.044 gateup8, 1.030 balanced8, 1.030 halves8, 1.004 even8)
-    c.setdefault("first_scale", 1.035)
+    fit = c.get("projection_fit")
+    if fit:
+        a, st0, st = fit["content_scale"], c["stage"], fit["stage"]
+        for k in ("mlp", "send"):
+            c[k] = {col: a * (v - st0) + st for col, v in c[k].items()}
+        for k in ("attn", "core", "o_mlp", "one_layer", "q_send", "q_recv"):
+            if k in c:
+                c[k] = a * (c[k] - st0) + st
+        c["layer"] *= a
+        c["stage"] = st
+        c["head"] *= fit["head_scale"]
+        c["first_scale"] = fit["first_scale"]
     return c
 
 
 def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_US_8B, step: int = 256,
                  gateup_us: float = DECODE_US_8B_GATEUP, mb: dict = DECODE_MB_8B, o_cuts: bool = False,
-                 o_us: float = DECODE_US_8B_O, cal: dict | None = None):
+                 o_us: float = DECODE_US_8B_O, cal: dict | None = None, q_cuts: bool = False,
+                 q_us: float = DECODE_US_8B_QKV):
     """Stages cut anywhere in the layer timeline a boundary may sit -- a layer start, or inside
     a layer's MLP before gate/up column c (c = 0: the half boundary; 0 < c < intermediate, a
     multiple of `step`: a gate/up boundary), and with o_cuts also between a layer's attention
     and its o projection -- so that the lowest stage's HBM fraction at the pipeline's tick,
-    min_s bytes_s / max_s time_s, is the highest the time / byte model allows (an exact search:
+    min_s bytes_s / max_s time_s, is the highest the time / byte model allows -- with q_cuts also
+    between a layer's q/k/v projection and its attention (an exact search:
     for a tick bound T the best split is a DP over the cut points; T on a 4-us grid from the
     ideal total / n, then refined to 1 us).  Time model: costs (DECODE_US_8B) with the MLP
     half split into gate/up (gateup_us, linear in the columns) and down, and the attention half
@@ -320,6 +376,15 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
         times.append(t)
         byts.append(y)
         sadj.append(0.0)
+        if q_cuts:
+            cuts.append((l, "Q", 0))
+            byts.append(y + mb["qkv"])
+            if cal is None:
+                times.append(t + q_us)
+                sadj.append(0.0)
+            else:
+                times.append(t + cal["q_send"] - sn)
+                sadj.append((cal["q_recv"] - sn) - (lay - (cal["q_send"] - sn)))
         if o_cuts:
             cuts.append((l, "O", 0))
             byts.append(y + mb["attn_half"] - mb["o"])
@@ -405,7 +470,7 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
         first_unit = 2 * l0 + (1 if k0 == "G" else 0)
         end_unit = 2 * l1 + (0 if k1 == "L" else 1)     # exclusive, in half units
         out.append(StageRange(first_unit, end_unit - first_unit, c0 * step if k0 == "G" else 0,
-                              c1 * step if k1 == "G" else 0, k0 == "O", k1 == "O"))
+                              c1 * step if k1 == "G" else 0, k0 == "O", k1 == "O", k0 == "Q", k1 == "Q"))
     return out
 
 
@@ -423,8 +488,10 @@ def predicted_stage_us(r: StageRange, cal: dict, first: bool, last: bool) -> flo
     t = cal["stage"] + (cal["embed"] if first else 0.0) + (cal["head"] if last else 0.0)
     l0, l1 = r.first_layer, r.last_layer
     start = cal["o_mlp"] - cal["stage"] if r.first_o else \
+        cal["q_recv"] - cal["stage"] if r.first_q else \
         (cal["mlp"][r.first_col] - cal["stage"] if r.skip_first_attn else None)
     end = cal["core"] - cal["stage"] if r.last_o else \
+        cal["q_send"] - cal["stage"] if r.last_q else \
         (cal["send"][r.last_col] - cal["stage"] if r.skip_last_mlp else None)
     if l0 == l1 and start is not None and end is not None:
         # one layer, cut on both sides: its start part less what its end part leaves out
@@ -433,9 +500,14 @@ def predicted_stage_us(r: StageRange, cal: dict, first: bool, last: bool) -> flo
     return fs * (t + full * cal["layer"] + (start or 0.0) + (end or 0.0))
 
 
-def measured_split(n_layers: int, n: int, intermediate: int, o_cuts: bool = True, name: str = "qwen3_8b", **kw):
-    """sublayer_split (or gateup_split) on the measured stage-boundary costs (load_decode_costs)."""
-    return gateup_split(n_layers, n, intermediate, o_cuts=o_cuts, cal=load_decode_costs(name), **kw)
+def measured_split(n_layers: int, n: int, intermediate: int, o_cuts: bool = True, name: str = "qwen3_8b",
+                   q_cuts: bool | None = None, **kw):
+    """sublayer_split (or gateup_split) on the measured stage-boundary costs (load_decode_costs);
+    q/k/v|attention cut points too (q_cuts, by default) where the table has their costs."""
+    cal = load_decode_costs(name)
+    if q_cuts is None:
+        q_cuts = o_cuts and "q_send" in cal
+    return gateup_split(n_layers, n, intermediate, o_cuts=o_cuts, cal=cal, q_cuts=q_cuts, **kw)
 
 
 class SpanExecutor:
@@ -491,14 +563,16 @@ class PipelineStage:
                  device, seed: int, n_microbatches: int, batch: int, max_ctx: int, prefill_chunk: int = 2,
                  executor=None, group=None, profile: str = "random", want_logits: bool = False,
                  skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
-                 gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False):
+                 gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False,
+                 qkv_split_first: bool = False, qkv_split_last: bool = False):
         """profile: the synthetic weight profile (runtime.SpanRuntime.init_synthetic: "peaked"
         for token-exact parity runs).  want_logits (last stage): every decode step's and the
         prefill's last-row logits are kept, for parity checks against the oracle's.
         skip_first_attn / skip_last_mlp / gateup_split_*: the stage's sub-layer boundaries
         (StageRange.span_kwargs()); across a gate/up boundary a decode-sized hand-off is a record
         (h1 + the packed SwiGLU product, handoff_elems), across an attention|o boundary (o_split_*)
-        every hand-off is one (x + the attention output)."""
+        every hand-off is one (x + the attention output), across a q/k/v|attention boundary
+        (qkv_split_*) every decode hand-off (x + the raw q/k/v rows)."""
         assert n_microbatches == world, "the ring schedule keeps exactly one microbatch per stage in flight"
         self.dims, self.rank, self.world = dims, rank, world
         self.S = world
@@ -514,7 +588,8 @@ class PipelineStage:
                                max_positions=max_ctx, device=self.device, skip_first_attn=skip_first_attn,
                                skip_last_mlp=skip_last_mlp, gateup_split_first=gateup_split_first,
                                gateup_split_last=gateup_split_last, o_split_first=o_split_first,
-                               o_split_last=o_split_last)
+                               o_split_last=o_split_last, qkv_split_first=qkv_split_first,
+                               qkv_split_last=qkv_split_last)
             span.init_synthetic(seed, profile)
             executor = SpanExecutor(span)
         self.ex = executor
@@ -525,14 +600,15 @@ class PipelineStage:
         mb = range(n_microbatches)
         self.col_in, self.col_out = gateup_split_first, gateup_split_last
         self.o_in, self.o_out = bool(o_split_first), bool(o_split_last)
+        self.q_in, self.q_out = bool(qkv_split_first), bool(qkv_split_last)
 
-        def buf(col, o):     # a decode hand-off buffer: a record (1-D) or [batch, hidden]
-            if col or o:
-                return torch.zeros(buffer_elems(dims, batch, col, o), dtype=torch.bfloat16, device=dev)
+        def buf(col, o, q):     # a decode hand-off buffer: a record (1-D) or [batch, hidden]
+            if col or o or q:
+                return torch.zeros(buffer_elems(dims, batch, col, o, True, q), dtype=torch.bfloat16, device=dev)
             return torch.zeros(batch, h, dtype=torch.bfloat16, device=dev)
         self.ids = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
-        self.h_in = [buf(self.col_in, self.o_in) for _ in mb]
-        self.h_out = [buf(self.col_out, self.o_out) for _ in mb]
+        self.h_in = [buf(self.col_in, self.o_in, self.q_in) for _ in mb]
+        self.h_out = [buf(self.col_out, self.o_out, self.q_out) for _ in mb]
         self.ids_out = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
         self.want_logits = want_logits and rank == world - 1
         self.logits = [torch.zeros(batch, dims.vocab, dtype=torch.bfloat16, device=dev) for _ in mb] \
@@ -640,17 +716,18 @@ class PipelineStage:
                 send = bufs_out.pop(i_send)
                 m, c = items[i_send]
                 rows = min(self.prefill_chunk, self.B - c) * T
-                if (self.col_out and rows <= 64) or self.o_out:     # a record hand-off
-                    send = send.reshape(-1)[:handoff_elems(self.dims, rows, self.col_out, self.o_out, T == 1)]
+                if (self.col_out and rows <= 64) or self.o_out or (self.q_out and T == 1):     # a record hand-off
+                    send = send.reshape(-1)[:handoff_elems(self.dims, rows, self.col_out, self.o_out, T == 1,
+                                                           self.q_out)]
             if not self.first and 0 <= i_cur < len(items):
                 m, c = items[i_cur]
                 nseq = min(self.prefill_chunk, self.B - c)
                 rows = nseq * T
-                if (self.col_in and rows <= 64) or self.o_in:
-                    recv = torch.zeros(buffer_elems(self.dims, rows, self.col_in, self.o_in, T == 1),
+                if (self.col_in and rows <= 64) or self.o_in or (self.q_in and T == 1):
+                    recv = torch.zeros(buffer_elems(self.dims, rows, self.col_in, self.o_in, T == 1, self.q_in),
                                        dtype=torch.bfloat16, device=self.device)
                     bufs_in[i_cur] = recv
-                    recv = recv[:handoff_elems(self.dims, rows, self.col_in, self.o_in, T == 1)]
+                    recv = recv[:handoff_elems(self.dims, rows, self.col_in, self.o_in, T == 1, self.q_in)]
                 else:
                     recv = torch.empty(rows, h, dtype=torch.bfloat16, device=self.device)
                     bufs_in[i_cur] = recv
@@ -737,16 +814,16 @@ class PipelineStage:
             if 0 <= i_prev < n_items:                      # output of last tick
                 mp = i_prev % self.n_mb
                 send = self.ids_out[mp] if self.last else self.h_out[mp]
-                if (self.col_out or self.o_out) and not self.last:   # a record (the part carrying data)
-                    send = send[:handoff_elems(self.dims, self.B, self.col_out, self.o_out)]
+                if (self.col_out or self.o_out or self.q_out) and not self.last:   # a record (the part carrying data)
+                    send = send[:handoff_elems(self.dims, self.B, self.col_out, self.o_out, True, self.q_out)]
             if self.first:
                 j = t - S                                  # ids of item j feed item j + S
                 if 0 <= j < n_items:
                     recv = self.ids[j % self.n_mb]
             elif 0 <= i_cur < n_items:
                 recv = self.h_in[i_cur % self.n_mb]
-                if self.col_in or self.o_in:
-                    recv = recv[:handoff_elems(self.dims, self.B, self.col_in, self.o_in)]
+                if self.col_in or self.o_in or self.q_in:
+                    recv = recv[:handoff_elems(self.dims, self.B, self.col_in, self.o_in, True, self.q_in)]
             tx = time.perf_counter()
             self._exchange(send, (self.rank + 1) % S, recv, (self.rank - 1) % S)
             t_x += time.perf_counter() - tx

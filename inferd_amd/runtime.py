@@ -204,7 +204,8 @@ class SpanRuntime:
                  has_lm_head: bool, kv_pages: int = 256, max_tokens: int = 4096, max_seqs: int = 64,
                  max_positions: int | None = None, device: str | torch.device = "cuda",
                  skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
-                 gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False):
+                 gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False,
+                 qkv_split_first: bool = False, qkv_split_last: bool = False):
         """skip_first_attn / skip_last_mlp: sub-layer stage boundaries (InferdSpanConfig): the
         span starts at its first layer's MLP half (x = that layer's post-attention residual)
         and/or ends after its last layer's attention half (hidden out = that residual).
@@ -212,13 +213,17 @@ class SpanRuntime:
         this column; decode calls then hand over a record (h1, then the packed SwiGLU product,
         record_elems()) instead of h1 alone.  o_split_first / _last: the boundary sits between a
         layer's attention and its o projection; every call hands over a record (the layer's input
-        residual, then the attention output: o_record_elems())."""
+        residual, then the attention output: o_record_elems()).  qkv_split_first / _last: the
+        boundary sits between a layer's q/k/v projection and its attention; a pure decode call
+        hands over a record (x, then the raw q/k/v rows: q_record_elems()), other calls x alone
+        (the receiver runs the whole layer)."""
         self.dims = dims
         self.first_layer, self.n_layers = first_layer, n_layers
         self.has_embed, self.has_lm_head = has_embed, has_lm_head
         self.skip_first_attn, self.skip_last_mlp = bool(skip_first_attn), bool(skip_last_mlp)
         self.gateup_split_first, self.gateup_split_last = int(gateup_split_first), int(gateup_split_last)
         self.o_split_first, self.o_split_last = bool(o_split_first), bool(o_split_last)
+        self.qkv_split_first, self.qkv_split_last = bool(qkv_split_first), bool(qkv_split_last)
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -227,7 +232,7 @@ class SpanRuntime:
         cfg = [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
                n_layers, int(has_embed), int(has_lm_head), self.max_positions, kv_pages, max_tokens, max_seqs,
                int(skip_first_attn), int(skip_last_mlp), int(gateup_split_first), int(gateup_split_last),
-               int(o_split_first), int(o_split_last)]
+               int(o_split_first), int(o_split_last), int(qkv_split_first), int(qkv_split_last)]
         self.handle = None
         self.handle = T.span_create(cfg, dims.eps, dims.rope_theta, self.device)
         self.kv = KvTable(kv_pages)
@@ -252,6 +257,12 @@ class SpanRuntime:
         call (fragment-packed)][heads * 128]."""
         d = self.dims
         return rows * d.hidden + ((rows + 15) // 16 * 16 if decode else rows) * d.heads * d.head_dim
+
+    def q_record_elems(self, rows: int, decode: bool) -> int:
+        """bf16 elements of a q/k/v|attention-boundary hand-off: x [rows][hidden], then (a pure
+        decode call) the raw q/k/v rows [rows][(heads + 2 kv_heads) * head_dim]."""
+        d = self.dims
+        return rows * d.hidden + (rows * (d.heads + 2 * d.kv_heads) * d.head_dim if decode else 0)
 
     # ----------------------------------------------------------------- weights
     def _stream(self):
@@ -404,11 +415,14 @@ class SpanRuntime:
         total = sum(n for _, n in requests)
         # hand-off records (InferdSpanConfig): decode calls at a gate/up boundary, every call at an
         # attention|o boundary (the attention output fragment-packed in a pure decode call)
-        packed = total <= 64 and all(n == 1 for _, n in requests)
+        pure = all(n == 1 for _, n in requests)
+        packed = total <= 64 and pure
         in_rec = (self.record_elems(total) if self.gateup_split_first and total <= 64 else
-                  self.o_record_elems(total, packed) if self.o_split_first else 0)
+                  self.o_record_elems(total, packed) if self.o_split_first else
+                  self.q_record_elems(total, True) if self.qkv_split_first and pure else 0)
         out_rec = (self.record_elems(total) if self.gateup_split_last and total <= 64 else
-                   self.o_record_elems(total, packed) if self.o_split_last else 0)
+                   self.o_record_elems(total, packed) if self.o_split_last else
+                   self.q_record_elems(total, True) if self.qkv_split_last and pure else 0)
         with torch.cuda.device(dev):
             ids_d = x_d = None
             if self.has_embed:
@@ -432,8 +446,8 @@ class SpanRuntime:
                     x_d = x.to(device=dev, dtype=torch.bfloat16).reshape(total, d.hidden).contiguous()
             rec_in = x_d is not None and x_d.dim() == 1
             rec_out = bool(out_rec) and want_hidden
-            if self.o_split_last and not want_hidden:
-                raise ValueError("a span ending before an o projection always hands over its record")
+            if (self.o_split_last or self.qkv_split_last) and not want_hidden:
+                raise ValueError("a span ending before an o projection or an attention always hands over its record")
             temp = []
             states = []
             for sid, _ in requests:
@@ -462,11 +476,17 @@ class SpanRuntime:
                 for _, n in requests:
                     row0.append(row0[-1] + n)
                 calls = self._plan(requests)
+                if (rec_in or rec_out) and len(calls) > 1:
+                    raise ValueError("a call handing over a record is one engine call "
+                                     f"(at most {self.max_tokens} tokens / {self.max_seqs} sequences)")
                 if (self.gateup_split_first or self.gateup_split_last) and \
-                        ((rec_in or rec_out) and len(calls) > 1 or
-                         total > 64 and any(sum(t for _, _, t in c) <= 64 for c in calls)):
+                        total > 64 and any(sum(t for _, _, t in c) <= 64 for c in calls):
                     raise ValueError("across a gate/up boundary a call is either one decode-sized engine call "
                                      "(<= 64 rows, record hand-off) or only prefill-sized ones (> 64 rows)")
+                if (self.qkv_split_first or self.qkv_split_last) and not pure and \
+                        any(all(t == 1 for _, _, t in c) for c in calls):
+                    raise ValueError("across a q/k/v|attention boundary an engine call of one-token pieces is a "
+                                     "decode call (record hand-off): split such a request differently")
                 if (self.o_split_first or self.o_split_last) and len(calls) > 1:
                     raise ValueError("across an attention|o boundary a forward call is one engine call "
                                      f"(at most {self.max_tokens} tokens / {self.max_seqs} sequences)")

@@ -324,8 +324,9 @@ def test_gateup_boundary_chain_bit_exact(T):
         s.check_errors()
 
 
-@pytest.mark.parametrize("split,T", [("o", 70), ("o", 9), ("o_gateup", 9)],
-                         ids=["o_prefill_rows", "o_prefill_small", "o_then_gateup"])
+@pytest.mark.parametrize("split,T", [("o", 70), ("o", 9), ("o_gateup", 9), ("q", 70), ("q", 9), ("q_o", 9)],
+                         ids=["o_prefill_rows", "o_prefill_small", "o_then_gateup", "q_prefill_rows", "q_prefill_small",
+                              "q_then_o"])
 def test_o_boundary_chain_bit_exact(split, T):
     """Stage boundaries between a layer's attention and its o projection (InferdSpanConfig
     o_split_*): Qwen3-0.6B layers 0..3 as [0..1q] (embed), [1o..3q], [3o..3] (lm_head) -- or
@@ -333,7 +334,10 @@ def test_o_boundary_chain_bit_exact(split, T):
     bit-identical logits to one span: a prefill of 3 sequences (the record x | attention output
     row-major), then 5 decode-graph steps whose records carry the attention output fragment-packed.
     The first record's attention output (layer 1's, before o_proj) is within the span tolerance of
-    the oracle's."""
+    the oracle's.  "q" / "q_o": q/k/v|attention boundaries (InferdSpanConfig qkv_split_*) in
+    place of the first (and second) ones -- prefill hands over x alone and the receiver runs the
+    whole layer; decode records carry x and the raw q/k/v rows (split-K slices summed by the
+    sender as the fused attention sums them)."""
     from inferd_amd.pipeline import StageRange, buffer_elems, o_record_elems, unpack_rows
     from inferd_amd.runtime import DecodeGraph
     d = R.CONFIGS["qwen3-0.6b"]
@@ -345,6 +349,12 @@ def test_o_boundary_chain_bit_exact(split, T):
     if split == "o":
         ranges = [StageRange(0, 3, last_o=True), StageRange(2, 5, first_o=True, last_o=True),
                   StageRange(6, 2, first_o=True)]
+    elif split == "q":
+        ranges = [StageRange(0, 3, last_q=True), StageRange(2, 5, first_q=True, last_q=True),
+                  StageRange(6, 2, first_q=True)]
+    elif split == "q_o":
+        ranges = [StageRange(0, 3, last_q=True), StageRange(2, 5, first_q=True, last_o=True),
+                  StageRange(6, 2, first_o=True)]
     else:
         ranges = [StageRange(0, 3, last_o=True), StageRange(2, 3, 0, 1024, first_o=True), StageRange(5, 3, 1024, 0)]
     chain = [span("qwen3-0.6b", r.first_layer, r.n_layers, i == 0, i == 2, kv_pages=16, max_tokens=B * T + 64,
@@ -353,21 +363,22 @@ def test_o_boundary_chain_bit_exact(split, T):
     sess = [f"o{b}" for b in range(B)]
     reqs = [(sid, T) for sid in sess]
     o0 = chain[0].forward(reqs, ids=prompts.reshape(-1))
-    rec0 = o0["record"]
-    assert rec0.numel() == o_record_elems(d, B * T, False)
+    qsplit = split.startswith("q")
+    rec0 = o0["hidden"].reshape(-1) if qsplit else o0["record"]
+    assert rec0.numel() == (B * T * d.hidden if qsplit else o_record_elems(d, B * T, False))
     o1 = chain[1].forward(reqs, x=rec0)
     lc = chain[2].forward(reqs, x=o1.get("record", o1["hidden"]), want_logits=True, want_hidden=False)["logits"]
     lo = one.forward(reqs, ids=prompts.reshape(-1), want_logits=True, want_hidden=False)["logits"]
     assert torch.equal(lc, lo), (lc.float() - lo.float()).abs().max()
-    xr, ar = R.RefSpan(d, SEED, 0, 1, True, False, o_split_last=True).forward(prompts)
+    xr, ar = R.RefSpan(d, SEED, 0, 1, True, False, o_split_last=not qsplit, qkv_split_last=qsplit).forward(prompts)
     ex = rel_err(rec0[:B * T * d.hidden].reshape(B, T, -1), xr)
-    ea = rel_err(rec0[B * T * d.hidden:].reshape(B, T, -1), ar)
-    print(f"attention|o record vs oracle: x rel err {ex:.2e}, attention output rel err {ea:.2e}")
+    ea = 0.0 if qsplit else rel_err(rec0[B * T * d.hidden:].reshape(B, T, -1), ar)
+    print(f"{split} record vs oracle: x rel err {ex:.2e}, attention output rel err {ea:.2e}")
     assert ex < TOL_REL and ea < TOL_REL
     ids_c = torch.zeros(B, dtype=torch.int32, device=DEV)
     ids_o = torch.zeros(B, dtype=torch.int32, device=DEV)
     r0, r1 = ranges[0], ranges[1]
-    recs = [torch.zeros(buffer_elems(d, B, r.last_col, r.last_o), dtype=torch.bfloat16, device=DEV)
+    recs = [torch.zeros(buffer_elems(d, B, r.last_col, r.last_o, True, r.last_q), dtype=torch.bfloat16, device=DEV)
             for r in (r0, r1)]
     lg_c = torch.zeros(B, d.vocab, dtype=torch.bfloat16, device=DEV)
     lg_o = torch.zeros(B, d.vocab, dtype=torch.bfloat16, device=DEV)
@@ -377,7 +388,8 @@ def test_o_boundary_chain_bit_exact(split, T):
               DecodeGraph(chain[1], sess, STEPS, x=recs[0], hidden_out=recs[1]),
               DecodeGraph(chain[2], sess, STEPS, x=recs[1], next_ids=nid_c, logits=lg_c)]
     g1 = DecodeGraph(one, sess, STEPS, ids=ids_o, next_ids=nid_o, logits=lg_o)
-    assert recs[0].numel() == B * d.hidden + 16 * Hd
+    Nq = (d.heads + 2 * d.kv_heads) * d.head_dim
+    assert recs[0].numel() == B * d.hidden + (B * Nq if qsplit else 16 * Hd)
     for k in range(STEPS):
         ids_c.copy_(forced[k])
         ids_o.copy_(forced[k])
@@ -386,9 +398,15 @@ def test_o_boundary_chain_bit_exact(split, T):
         g1.launch()
         assert torch.equal(lg_c, lg_o), (k, (lg_c.float() - lg_o.float()).abs().max())
         assert torch.equal(nid_c, nid_o), k
-    # the decode record's attention output is fragment-packed: its padding rows stay zero
-    a = unpack_rows(recs[0][B * d.hidden:], 16, Hd)
-    assert torch.count_nonzero(a[B:]) == 0 and torch.count_nonzero(a[:B]) > 0
+    if qsplit:   # the decode record's q/k/v rows: the oracle's projection of the record's x
+        xq = recs[0][:B * d.hidden].view(B, 1, d.hidden).cpu()
+        qr = R.qkv_proj(xq, R.RefSpan(d, SEED, 1, 1, False, False).layers[0], d)
+        eq = rel_err(recs[0][B * d.hidden:].view(B, 1, Nq), qr)
+        print(f"q/k/v record rows vs oracle: rel err {eq:.2e}")
+        assert eq < TOL_REL
+    else:        # the decode record's attention output is fragment-packed: its padding rows stay zero
+        a = unpack_rows(recs[0][B * d.hidden:], 16, Hd)
+        assert torch.count_nonzero(a[B:]) == 0 and torch.count_nonzero(a[:B]) > 0
     for s in chain + [one]:
         s.check_errors()
 
@@ -415,6 +433,19 @@ def test_half_layer_span_rejects_bad_configs():
         with pytest.raises(RuntimeError, match="attention\\|o boundary excludes"):
             SpanRuntime(d, 1, 2, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
                         **{"has_embed": False, "has_lm_head": False, **kw})
+    for kw in ({"has_embed": True, "qkv_split_first": True}, {"has_lm_head": True, "qkv_split_last": True},
+               {"o_split_first": True, "qkv_split_first": True}, {"skip_last_mlp": True, "qkv_split_last": True}):
+        with pytest.raises(RuntimeError, match="attention boundary excludes"):
+            SpanRuntime(d, 1, 2, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
+                        **{"has_embed": False, "has_lm_head": False, **kw})
+    with pytest.raises(RuntimeError, match="cannot end before"):
+        SpanRuntime(d, 1, 1, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
+                    qkv_split_first=True, qkv_split_last=True)
+    sq = SpanRuntime(d, 1, 2, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
+                     qkv_split_last=True)
+    sq.set_weight(1, "k_proj", torch.zeros(d.kv_heads * 128, d.hidden, dtype=torch.bfloat16))
+    with pytest.raises(RuntimeError, match="other half"):
+        sq.set_weight(1, "o_proj", torch.zeros(d.hidden, d.heads * 128, dtype=torch.bfloat16))
     so = SpanRuntime(d, 1, 2, has_embed=False, has_lm_head=False, device=DEV, kv_pages=8, max_tokens=64, max_seqs=2,
                      o_split_first=True)
     with pytest.raises(RuntimeError, match="other half"):

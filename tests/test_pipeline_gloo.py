@@ -24,7 +24,8 @@ class OracleExecutor:
     def __init__(self, d, r, first_span, last_span):
         self.sp = R.RefSpan(d, SEED, r.first_layer, r.last_layer, first_span, last_span, torch.bfloat16, "sdpa",
                             skip_first_attn=r.skip_first_attn, skip_last_mlp=r.skip_last_mlp,
-                            o_split_first=r.first_o, o_split_last=r.last_o)
+                            o_split_first=r.first_o, o_split_last=r.last_o, qkv_split_first=r.first_q,
+                            qkv_split_last=r.last_q)
         self.device = torch.device("cpu")
         self.has_embed, self.has_lm_head = first_span, last_span
         self.dims = d
@@ -34,23 +35,31 @@ class OracleExecutor:
         """Decode-sized hand-offs across a gate/up boundary are records (h1 first, then the packed
         SwiGLU product): the oracle reads and writes the h1 part and recomputes the whole MLP.
         Across an attention|o boundary every hand-off is a record (x, then the attention output,
-        fragment-packed in a pure decode call): the oracle reads / writes both parts."""
+        fragment-packed in a pure decode call): the oracle reads / writes both parts.  Across a
+        q/k/v|attention boundary a pure decode call's hand-off is (x, raw q/k/v rows), others x."""
         from inferd_amd.pipeline import pack_rows, unpack_rows
         outs = []
         S, rows, h = len(sessions), len(sessions) * n, self.dims.hidden
         Hd = self.dims.heads * self.dims.head_dim
         packed = n == 1 and rows <= 64
-        a_in = None
+        Nq = (self.dims.heads + 2 * self.dims.kv_heads) * self.dims.head_dim
+        a_in = q_in = None
         if x is not None and self.r.first_o:
             tail = x.reshape(-1)[rows * h:]
             a_in = (unpack_rows(tail, rows, Hd) if packed else tail[:rows * Hd].view(rows, Hd)).reshape(S, n, Hd)
+        if x is not None and self.r.first_q and n == 1:
+            q_in = x.reshape(-1)[rows * h:rows * (h + Nq)].view(S, n, Nq)
         for i, sid in enumerate(sessions):
             if ids is not None:
                 inp = ids.reshape(S, n)[i:i + 1].long()
                 o = self.sp.forward_cached(sid, inp)
             else:
                 xi = x.reshape(-1)[:rows * h].reshape(S, n, -1)[i:i + 1]
-                o = self.sp.forward_cached(sid, (xi, a_in[i:i + 1]) if a_in is not None else xi)
+                if self.r.first_o:
+                    xi = (xi, a_in[i:i + 1])
+                elif self.r.first_q:
+                    xi = (xi, None if q_in is None else q_in[i:i + 1])
+                o = self.sp.forward_cached(sid, xi)
             outs.append(o)
         if self.sp.last:
             return torch.stack([torch.argmax(o[0, -1]) for o in outs]).to(torch.int32)
@@ -58,6 +67,11 @@ class OracleExecutor:
             xs = torch.cat([o[0][0] for o in outs]).to(torch.bfloat16).reshape(-1)
             a = torch.cat([o[1][0] for o in outs]).to(torch.bfloat16)
             return torch.cat([xs, pack_rows(a) if packed else a.reshape(-1)])
+        if self.r.last_q:
+            xs = torch.cat([o[0][0] for o in outs]).to(torch.bfloat16)
+            if n != 1:
+                return xs
+            return torch.cat([xs.reshape(-1), torch.cat([o[1][0] for o in outs]).to(torch.bfloat16).reshape(-1)])
         h1 = torch.cat([o[0] for o in outs]).to(torch.bfloat16)
         if self.r.last_col and rows <= 64:
             from inferd_amd.pipeline import record_elems
@@ -97,6 +111,12 @@ def _split(d, world, sizes):
         return [StageRange(0, 3, 0, 256), StageRange(3, 2, 256, 128), StageRange(5, 3, 128, 0)][:world]
     if sizes == "o":      # attention|o boundaries in layers 1 and 3
         return [StageRange(0, 3, last_o=True), StageRange(2, 5, first_o=True, last_o=True),
+                StageRange(6, 2, first_o=True)][:world]
+    if sizes == "q":          # q/k/v|attention boundaries in layers 1 and 3
+        return [StageRange(0, 3, last_q=True), StageRange(2, 5, first_q=True, last_q=True),
+                StageRange(6, 2, first_q=True)][:world]
+    if sizes == "q_o":        # a q/k/v|attention boundary, then an attention|o one
+        return [StageRange(0, 3, last_q=True), StageRange(2, 5, first_q=True, last_o=True),
                 StageRange(6, 2, first_o=True)][:world]
     if sizes == "o_gateup":   # an attention|o boundary, then a gate/up one (the same stage)
         return [StageRange(0, 3, last_o=True), StageRange(2, 3, 0, 256, first_o=True), StageRange(5, 3, 256, 0)]
@@ -176,7 +196,7 @@ def _reference(world, n_steps, sizes=None, force=False):
 
 @pytest.mark.parametrize("world,sizes", [(2, None), (3, None), (3, [1, 2, 1]), (2, [3, 1]),
                                          (2, [1.5, 2.5]), (3, [0.5, 2, 1.5]), (3, "gateup"),
-                                         (3, "o"), (3, "o_gateup")])
+                                         (3, "o"), (3, "o_gateup"), (3, "q"), (3, "q_o")])
 def test_pipeline_matches_single_process(world, sizes):
     n_steps = 4
     ctx = mp.get_context("spawn")

@@ -94,7 +94,8 @@ def test_record_sizes():
     assert P.handoff_elems(D8, 20, 2048) == P.record_elems(D8, 20)     # several: the whole record
     r = P.StageRange(9, 10, 2048, 4096)
     assert r.span_kwargs() == {"skip_first_attn": True, "skip_last_mlp": True, "gateup_split_first": 2048,
-                               "gateup_split_last": 4096, "o_split_first": False, "o_split_last": False}
+                               "gateup_split_last": 4096, "o_split_first": False, "o_split_last": False,
+                               "qkv_split_first": False, "qkv_split_last": False}
     assert r.label() == "4m@2048..9a+4096"
     with pytest.raises(AssertionError):
         P.StageRange(8, 10, 2048, 0)          # a gate/up boundary refines a half boundary
@@ -107,6 +108,12 @@ def test_record_sizes():
     assert P.handoff_elems(D8, 3, 0, o=True) == P.buffer_elems(D8, 3, 0, o=True) == P.o_record_elems(D8, 3, True)
     with pytest.raises(AssertionError):
         P.StageRange(29, 4, first_o=True)     # an attention|o boundary sits in an attention unit
+    r = P.StageRange(28, 11, first_q=True, last_q=True)
+    assert r.label() == "14k..19v" and r.end_unit == 38 and P.StageRange.from_label("14k..19v") == r
+    assert P.q_record_elems(D8, 16, True) == 16 * 4096 + 16 * 6144
+    assert P.handoff_elems(D8, 16, 0, q=True, pure=False) == 16 * 4096
+    for lab in ("4m@12032..9a+4096", "14o..18", "9m@768..14q", "19k..23a+8192", "0..4", "33m..35"):
+        assert P.StageRange.from_label(lab).label() == lab
 
 
 def test_packed_rows_round_trip():

@@ -15,7 +15,13 @@ first-norm / prologue launch every stage pays), attn (span ending after layer l'
 half), mlp[c] (span starting at layer l's MLP at gate/up column c, c = 0 the half boundary),
 send[c] (span = layer l's attention half + gate/up columns [0, c)), core (attention half
 without o: an attention|o boundary's sender), o_mlp (o projection + MLP: its receiver), head
-(final norm + lm_head + argmax on top of one layer), embed (embedding on top of one layer).
+(final norm + lm_head + argmax on top of one layer), embed (embedding on top of one layer),
+q_send (input norm + q/k/v projection: a q/k/v|attention boundary's sender), q_recv (attention +
+o + MLP: its receiver).
+
+  --only q --merge inferd_amd/data/decode_costs_qwen3_8b.json: measure q_send / q_recv with the
+  reference entries one_layer, attn, core, o_mlp beside them, and merge them into the table scaled
+  by the ratio of the reference entries (the table was measured on another box).
 """
 import argparse
 import json
@@ -40,6 +46,8 @@ def main():
     p.add_argument("--step", type=int, default=256)
     p.add_argument("--layer", type=int, default=10)
     p.add_argument("--out", default="gpurun_out/boundary_costs.json")
+    p.add_argument("--only", default="", help="q: only the q/k/v|attention boundary entries (+ references)")
+    p.add_argument("--merge", default="", help="with --only: the table to merge the scaled entries into")
     a = p.parse_args()
     d = MODELS[a.model]
     dev = torch.device("cuda", 0)
@@ -54,6 +62,24 @@ def main():
               flush=True)
         return v
 
+    if a.only == "q":
+        ref = {"one_layer": ms(StageRange(u, 2)), "attn": ms(StageRange(u, 1)), "core": ms(StageRange(u, 1, last_o=True)),
+               "o_mlp": ms(StageRange(u, 2, first_o=True))}
+        new = {"q_send": ms(StageRange(u, 1, last_q=True)), "q_recv": ms(StageRange(u, 2, first_q=True))}
+        res = {"measured": {**ref, **new}}
+        if a.merge:
+            with open(a.merge) as f:
+                table = json.load(f)
+            k = sum(table[key] for key in ref) / sum(ref.values())
+            for key, v in new.items():
+                table[key] = v * k
+            table.setdefault("merged", []).append({"entries": sorted(new), "scale": round(k, 5), "measured": res["measured"]})
+            res = table
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res.get("merged", res)), flush=True)
+        return
     one = ms(StageRange(u, 2))
     five = ms(StageRange(u, 10))
     layer = (five - one) / 4
@@ -64,6 +90,8 @@ def main():
     res["o_mlp"] = ms(StageRange(u, 2, first_o=True))
     res["head"] = ms(StageRange(u, 2), last=True) - one
     res["embed"] = ms(StageRange(u, 2), first=True) - one
+    res["q_send"] = ms(StageRange(u, 1, last_q=True))
+    res["q_recv"] = ms(StageRange(u, 2, first_q=True))
     cols = list(range(0, d.intermediate, a.step))
     res["mlp"] = {c: ms(StageRange(u + 1, 1, c, 0)) for c in cols}
     res["send"] = {c: (ms(StageRange(u, 1, 0, c)) if c else res["attn"]) for c in cols}

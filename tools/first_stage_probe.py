@@ -51,11 +51,15 @@ def main():
         res.setdefault(tag, []).append(round(ms * 1e3, 2))
         print(f"[{time.time() - t0:6.1f}s] {tag}: {ms * 1e3:.1f} us", file=sys.stderr, flush=True)
 
+    only = sys.argv[1] if len(sys.argv) > 1 else ""    # "first" / "inner": one kind (for rocprofv3)
     for _ in range(2):
-        run("first_ids", True)
-        run("inner_randn0.5", False)
-        run("inner_randn0.035", False, scale=0.035)
-        run("inner_embed_rows", False, embed=True)
+        if only in ("", "first"):
+            run("first_ids", True)
+        if only in ("", "inner"):
+            run("inner_randn0.5", False)
+        if not only:
+            run("inner_randn0.035", False, scale=0.035)
+            run("inner_embed_rows", False, embed=True)
     print(json.dumps(res))
 
 
