@@ -17,6 +17,13 @@ Per kernel class, mean over launches:
                       SIMD x 1024 SIMDs x clock)
   * valu_per_wave_cycle SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, lds_wait_frac SQ_WAIT_INST_LDS /
                       SQ_WAVE_CYCLES (both in quad-cycles)
+  * wave_cycle_split  (second pass, optional third argument) the wave cycles split into parked
+                      (SQ_WAIT_ANY: s_waitcnt / barrier), issue-stalled (SQ_WAIT_INST_ANY: MFMA
+                      dependency / pipe busy) and issuing (SQ_ACTIVE_INST_ANY) -- disjoint, summing
+                      to SQ_WAVE_CYCLES (MI355X_MICROARCH.md, SQ counters); coexec_frac
+                      SQ_VALU_MFMA_COEXEC_CYCLES / SQ_VALU_MFMA_BUSY_CYCLES (the share of matrix-busy
+                      cycles with vector instructions executing beside them); lds_conflict_frac
+                      SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
 """
 import csv
 import glob
@@ -77,6 +84,7 @@ def by_class(seq, key):
 
 def main():
     pmc = by_class(counters(sys.argv[1]), lambda e: (e["name"], e))
+    pmc2 = by_class(counters(sys.argv[3]), lambda e: (e["name"], e)) if len(sys.argv) > 3 else {}
     dur = {k: sum(v) / len(v) for k, v in by_class(durations(sys.argv[2]), lambda e: e).items()}
     fl = flops()
     out = {}
@@ -104,6 +112,18 @@ def main():
                 "frac_of_2500": round(fl[c] / t / 2.5e15, 4),
                 "frac_of_clock_peak": round(fl[c] / t / (1024 * 1024 * clk), 4),
             })
+        if c in pmc2:
+            l2 = pmc2[c]
+            m2 = {k: sum(e.get(k, 0.0) for e in l2) / len(l2) for k in
+                  ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                   "SQ_VALU_MFMA_COEXEC_CYCLES", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE")}
+            wc = m2["SQ_WAVE_CYCLES"] or 1.0
+            row["counters_pass2_mean"] = {k: round(v) for k, v in m2.items()}
+            row["wave_cycle_split"] = {"parked": round(m2["SQ_WAIT_ANY"] / wc, 4),
+                                       "issue_stalled": round(m2["SQ_WAIT_INST_ANY"] / wc, 4),
+                                       "issuing": round(m2["SQ_ACTIVE_INST_ANY"] / wc, 4)}
+            row["coexec_frac"] = round(m2["SQ_VALU_MFMA_COEXEC_CYCLES"] / max(m["SQ_VALU_MFMA_BUSY_CYCLES"], 1.0), 4)
+            row["lds_conflict_frac"] = round(m2["SQ_LDS_BANK_CONFLICT"] / max(m2["SQ_LDS_IDX_ACTIVE"], 1.0), 4)
         out[c] = row
     print(json.dumps({
         "workload": "qwen3-32b-prefill-8layers-T8192" + (f"-B{B}" if B > 1 else ""),
