@@ -367,11 +367,19 @@ def sub_split(d, n: int, o_cuts: bool):
     return P.gateup_split(d.layers, n, d.intermediate, o_cuts=o_cuts)
 
 
+# BASELINE config 4: uneven, balance.py-like splits, 36-layer models
+CONFIG4_SPLITS = {3: [5, 27, 4], 4: [6, 12, 12, 6], 8: [2, 3, 5, 6, 6, 6, 5, 3]}
+
+
 def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
     """The splits stage_projection measures: BASELINE config 3's even splits, the layer-granular
-    byte-balanced split and the half-layer time-balanced split at each stage count."""
-    from inferd_amd.pipeline import StageRange, halves_split
+    byte-balanced split, the half-layer and sub-layer time-balanced splits at each stage count,
+    and BASELINE config 4's uneven splits (their stage imbalance and bubble)."""
+    from inferd_amd.pipeline import StageRange, halves_split, ranges_from_sizes
     out = {}
+    if d.layers == 36:
+        for n, sp in CONFIG4_SPLITS.items():
+            out[f"config4_uneven{n}"] = ranges_from_sizes(sp)
     for n in sizes:
         if n > d.layers:
             continue

@@ -424,25 +424,32 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
     sa_lo = float(sa.min())
 
     def solve(T):
-        """(value, boundary cuts) of the best split with every stage within T"""
+        """(value, boundary cuts) of the best split with every stage within T (every end cut l of
+        a stage at once: a [ends, window] matrix of its candidate start cuts j, ascending, so
+        argmax keeps the first -- smallest -- best j)"""
         f = np.full(P + 1, -1.0)
         f[0] = np.inf
         arg = []
         for s in range(n):
             last = s == n - 1
+            scale = fs if s == 0 else 1.0
             extra = sn + (hd if last else 0.0) + (emb if s == 0 else 0.0)
             g = np.full(P + 1, -1.0)
             gi = np.zeros(P + 1, dtype=np.int64)
-            ends = [P] if last else range(s + 1, P - (n - 1 - s) + 1)
-            for l in ends:
-                j0 = max(int(np.searchsorted(tm, tm[l] - (T / (fs if s == 0 else 1.0) - extra) + sa_lo, side="left")), s)
-                if j0 >= l:
-                    continue
-                js = np.arange(j0, l)
-                fj = np.where((tm[l] - tm[j0:l] + sa[j0:l] + extra) * (fs if s == 0 else 1.0) <= T, f[j0:l], -1.0)
-                v = np.where(fj >= 0, np.minimum(fj, (by[l] - by[j0:l] + (mb["head"] if last else 0.0)) / T), -1.0)
-                k = int(v.argmax())
-                g[l], gi[l] = v[k], js[k]
+            ends = np.array([P]) if last else np.arange(s + 1, P - (n - 1 - s) + 1)
+            j0 = np.maximum(np.searchsorted(tm, tm[ends] - (T / scale - extra) + sa_lo, side="left"), s)
+            W = int((ends - j0).max()) if len(ends) else 0
+            if W > 0:
+                J = j0[:, None] + np.arange(W)[None, :]
+                valid = J < ends[:, None]
+                Jc = np.where(valid, J, 0)
+                ok = valid & ((tm[ends][:, None] - tm[Jc] + sa[Jc] + extra) * scale <= T) & (f[Jc] >= 0)
+                v = np.where(ok, np.minimum(f[Jc], (by[ends][:, None] - by[Jc] + (mb["head"] if last else 0.0)) / T),
+                             -1.0)
+                k = v.argmax(1)
+                r = np.arange(len(ends))
+                g[ends] = v[r, k]
+                gi[ends] = Jc[r, k]
             arg.append(gi)
             f = g
         if f[P] < 0:
