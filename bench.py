@@ -126,6 +126,8 @@ def parse():
     p.add_argument("--mode", choices=("decode", "prefill", "stages"), default="decode",
                    help="prefill: BASELINE config 5 (one 8-layer Qwen3-32B stage, 8k prompts, MFMA roofline); "
                         "stages: the per-stage decode projection of the 2/4/8-GPU splits on one GPU")
+    p.add_argument("--no-sublayer-split", action="store_true",
+                   help="N > 1 runs of the even split: skip the second measurement on the sub-layer split")
     p.add_argument("--no-stage-projection", action="store_true",
                    help="N=1 decode runs: skip the per-stage projection of the 2/4/8-GPU splits")
     p.add_argument("--prefill-layers", type=int, default=8)
@@ -332,7 +334,9 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
     embedding on stage 0, final norm + lm_head + argmax on the last).  The lockstep pipeline
     (pipeline.py) ticks at its slowest stage, so per split: tick = max stage ms, each stage's
     fraction of the HBM roofline at that tick = its algorithmic bytes / (tick x 8 TB/s) (SURVEY
-    §8(d)), bubble = 1 - sum / (S x tick), and the compute-only projected rate S x B / tick (the
+    §8(d)), bubble = 1 - sum / (S x tick), and the compute-only projected rate B / tick (one
+    microbatch of B sequences completes a decode step per tick: S microbatches in flight, each a
+    token every S ticks; the
     xGMI hand-off excluded)."""
     out = {}
     g = torch.Generator(device="cpu").manual_seed(seed + 5)
@@ -351,7 +355,7 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
         out[name] = {"stages": stages, "tick_ms": tick,
                      "min_frac_at_tick": min(st["frac_at_tick"] for st in stages),
                      "bubble_frac": round(1 - sum(st["ms"] for st in stages) / (S * tick), 4),
-                     "projected_tokens_per_s": round(S * B / (tick * 1e-3), 1)}
+                     "projected_tokens_per_s": round(B / (tick * 1e-3), 1)}
     return out
 
 
@@ -492,6 +496,65 @@ def cpu_config1(seed: int, steps: int = 16) -> dict:
 
 
 # ------------------------------------------------------------------ main
+def pipeline_run(d, ranges, rank: int, world: int, dev, dist, args, profile: bool = True) -> dict:
+    """One pipeline measurement on this rank: build the stage of `ranges`, prefill every
+    microbatch (untimed), W warm-up and K timed decode steps (one captured graph replay per stage
+    per microbatch step) between barriers, then the eager event-timed kernel profile.  Times are
+    the max over ranks."""
+    from inferd_amd import pipeline as P
+    B, ctx, K, W = args.batch, args.ctx, args.steps, args.warmup
+    rg = ranges[rank]
+    if world > 1:
+        print(f"bench.py: rank {rank} on {dev}: layers {rg.label()} of {d.layers}"
+              f"{' + embed' if rank == 0 else ''}{' + norm/lm_head' if rank == world - 1 else ''}",
+              file=sys.stderr, flush=True)
+    n_mb = world                                   # microbatches in flight
+    st = P.PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=args.seed,
+                         n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + args.profile_steps + 64,
+                         prefill_chunk=args.prefill_chunk, **rg.span_kwargs())
+    # ---- prefill (untimed): every microbatch's sequences get `ctx` real tokens
+    g = torch.Generator().manual_seed(args.seed + 17)
+    prompts = [torch.randint(0, d.vocab, (B, ctx), generator=g) for _ in range(n_mb)]
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    st.prefill(prompts)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t_prefill = time.perf_counter() - t0
+    # ---- decode: warmup + timed (one captured HIP graph replay per stage per microbatch step)
+    st.prepare_decode(W + K)
+    st.decode(W)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st.decode(K)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tick = st.tick_stats
+    # ---- per-kernel HIP-event timings: the same decode kernels launched eagerly (events
+    # cannot be timed inside a replayed graph); right after the timed region, same cache state
+    prof = st.profile_decode(args.profile_steps) if profile else None
+    t = torch.tensor([elapsed, t_prefill], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, t_prefill = float(t[0]), float(t[1])
+    # per-stage compute per microbatch step (event-timed kernels) -> imbalance / hand-off
+    stage_ms = torch.zeros(world, dtype=torch.float64, device=dev)
+    if prof:
+        stage_ms[rank] = sum(ms for ms, n in prof.values()) / (args.profile_steps * n_mb)
+    if dist:
+        dist.all_reduce(stage_ms, op=dist.ReduceOp.SUM)
+    stage_ms = [float(v) for v in stage_ms.cpu()]
+    return {"st": st, "elapsed": elapsed, "t_prefill": t_prefill, "tick": tick, "prof": prof, "stage_ms": stage_ms}
+
+
 def main():
     args = parse()
     if args.mode == "prefill":
@@ -546,56 +609,10 @@ def main():
         ranges = sub_split(d, world, args.split == "sublayer")
     else:
         ranges = [P.StageRange.layers(f, k) for f, k in stage_split(d, world, B, ctx, args.split)]
-    rg = ranges[rank]
-    if world > 1:
-        print(f"bench.py: rank {rank} on cuda:{dev_index}: layers {rg.label()} of {d.layers}"
-              f"{' + embed' if rank == 0 else ''}{' + norm/lm_head' if rank == world - 1 else ''}",
-              file=sys.stderr, flush=True)
-    n_mb = world                                   # microbatches in flight
-    st = P.PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=args.seed,
-                         n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + args.profile_steps + 64,
-                         prefill_chunk=args.prefill_chunk, **rg.span_kwargs())
-    # ---- prefill (untimed): every microbatch's sequences get `ctx` real tokens
-    g = torch.Generator().manual_seed(args.seed + 17)
-    prompts = [torch.randint(0, d.vocab, (B, ctx), generator=g) for _ in range(n_mb)]
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t0 = time.perf_counter()
-    st.prefill(prompts)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t_prefill = time.perf_counter() - t0
-    # ---- decode: warmup + timed (one captured HIP graph replay per stage per microbatch step)
-    st.prepare_decode(W + K)
-    st.decode(W)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    st.decode(K)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    tick = st.tick_stats
-    # ---- per-kernel HIP-event timings: the same decode kernels launched eagerly (events
-    # cannot be timed inside a replayed graph); right after the timed region, same cache state
-    prof = None if args.no_profile else st.profile_decode(args.profile_steps)
-    t = torch.tensor([elapsed, t_prefill], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, t_prefill = float(t[0]), float(t[1])
-    # per-stage compute per microbatch step (event-timed kernels) -> imbalance / hand-off
-    stage_ms = torch.zeros(world, dtype=torch.float64, device=dev)
-    if prof:
-        stage_ms[rank] = sum(ms for ms, n in prof.values()) / (args.profile_steps * n_mb)
-    if dist:
-        dist.all_reduce(stage_ms, op=dist.ReduceOp.SUM)
-    stage_ms = [float(v) for v in stage_ms.cpu()]
-
+    run = pipeline_run(d, ranges, rank, world, dev, dist, args, profile=not args.no_profile)
+    st, elapsed, t_prefill, tick, prof, stage_ms = (run[k] for k in ("st", "elapsed", "t_prefill", "tick", "prof",
+                                                                     "stage_ms"))
+    n_mb = world
     tokens = K * n_mb * B
     value = tokens / elapsed
     ms_per_step = elapsed / K * 1e3
@@ -668,6 +685,7 @@ def main():
             "backend": None if not dist else dist.get_backend(),
         }
         out["peaks_measured"] = measured_peaks(dev)
+        out["sublayer_split"] = None
         if world == 1 and not args.no_prefill_line:
             # BASELINE config 5 in the same run (the driver's default bench call times it too)
             st.release()
@@ -687,6 +705,22 @@ def main():
             st.release()
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)
             out["cpu_baseline_config1"] = cpu_config1(args.seed)
+    if world > 1 and not args.no_sublayer_split and args.split == "even" and not args.spans:
+        # north_star's balanced pipeline beside config 3's even split, same run: the sub-layer split
+        # (every stage >= 60 % of the HBM roofline at the tick by the stage projection)
+        st.release()
+        alt = sub_split(d, world, True)
+        r2 = pipeline_run(d, alt, rank, world, dev, dist, args, profile=False)
+        r2["st"].release()
+        if rank == 0:
+            out["sublayer_split"] = {
+                "value": round(K * world * B / r2["elapsed"], 2), "unit": "tokens/s",
+                "ms_per_step": round(r2["elapsed"] / K * 1e3, 4), "stage_ranges": [r.label() for r in alt],
+                "tick_ms": round(r2["elapsed"] / K * 1e3 / world, 4),
+                "exchange_us_per_tick_rank0": r2["tick"]["exchange_us_per_tick"],
+                "note": "the same workload on pipeline.sublayer_split's stages (measured cost table); "
+                        "`value` above is BASELINE config 3's even split"}
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
