@@ -32,8 +32,11 @@ def main():
     res = {}
     orig_randn = torch.randn
 
-    def run(tag, first, scale=None, embed=False):
+    def run(tag, first, scale=None, embed=False, ballast=None):
         g = torch.Generator(device="cpu").manual_seed(5)
+        hold = None
+        if ballast == "before":   # 1.24 GB allocated before the span (the embedding table's size)
+            hold = torch.empty(d.vocab * d.hidden, dtype=torch.bfloat16, device=dev)
         if embed:     # inner stage fed embedding rows (what stage 0's layers see)
             def fake(*shape, generator=None, **kw):
                 n = 1
@@ -48,10 +51,11 @@ def main():
             ms = bench.stage_ms(d, r, first, False, B, ctx, dev, g, seed, warmup=5, reps=40)
         finally:
             torch.randn = orig_randn
+        del hold
         res.setdefault(tag, []).append(round(ms * 1e3, 2))
         print(f"[{time.time() - t0:6.1f}s] {tag}: {ms * 1e3:.1f} us", file=sys.stderr, flush=True)
 
-    only = sys.argv[1] if len(sys.argv) > 1 else ""    # "first" / "inner": one kind (for rocprofv3)
+    only = sys.argv[1] if len(sys.argv) > 1 else ""    # "first" / "inner" / "ballast": one kind
     for _ in range(2):
         if only in ("", "first"):
             run("first_ids", True)
@@ -60,6 +64,9 @@ def main():
         if not only:
             run("inner_randn0.035", False, scale=0.035)
             run("inner_embed_rows", False, embed=True)
+        if only in ("", "ballast"):
+            run("inner_ballast_before", False, ballast="before")
+            run("inner_plain", False)
     print(json.dumps(res))
 
 
