@@ -125,3 +125,33 @@ def test_half_layer_spans_chain_equals_whole_layers():
         y = one.forward_cached("s", ids)
         assert torch.equal(x, y), step
         ids = torch.argmax(y[:, -1], -1)[:, None]
+
+
+def test_sublayer_record_spans_chain_equals_whole_layers():
+    """The oracle's attention|o and q/k/v|attention boundaries (RefSpan o_split_* / qkv_split_*):
+    the tiny model cut as [0..1 before o] [1 o.. 2 after q/k/v] [2 attention..3] composes to the
+    whole-layer span bit-exactly -- the hand-offs are the records (x, attention output) and
+    (x, raw q/k/v rows), or x alone where a q/k/v cut's call is not a pure decode call -- full
+    recompute and cached prefill + 3 decode steps, pinned to the reference-generated golden logits."""
+    d = R.CONFIGS["tiny"]
+    g = load("tiny_petals.npz")
+    prompt = torch.from_numpy(g["prompt"])[None]
+    chain = [R.RefSpan(d, SEED, 0, 1, True, False, torch.bfloat16, "sdpa", o_split_last=True),
+             R.RefSpan(d, SEED, 1, 2, False, False, torch.bfloat16, "sdpa", o_split_first=True, qkv_split_last=True),
+             R.RefSpan(d, SEED, 2, 3, False, True, torch.bfloat16, "sdpa", qkv_split_first=True)]
+    one = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, torch.bfloat16, "sdpa")
+
+    def run(fwd, x, decode):
+        x = fwd(chain[0], x)                        # (x, attention output)
+        xq = fwd(chain[1], x)                       # (x, q/k/v rows)
+        return fwd(chain[2], xq if decode else (xq[0], None))
+
+    x = run(lambda sp, v: sp.forward(v), prompt, False)
+    assert torch.equal(x, one.forward(prompt))
+    assert torch.equal(x, tensor(g["bf16_logits"]))
+    ids = prompt
+    for step in range(4):
+        x = run(lambda sp, v: sp.forward_cached("s", v), ids, step > 0)
+        y = one.forward_cached("s", ids)
+        assert torch.equal(x, y), step
+        ids = torch.argmax(y[:, -1], -1)[:, None]
