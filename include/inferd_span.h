@@ -190,6 +190,13 @@ int inferd_span_graph_capture(InferdSpan* span, const InferdBatch* batch, int32_
                               void* logits, void* stream, InferdGraph** out);
 int inferd_graph_launch(InferdGraph* graph, void* stream);
 void inferd_graph_destroy(InferdGraph* graph);
+/* The work of one replay of such a graph, launched eagerly on `stream`: the device-side
+ * scheduler step (advance = 1, the same in-place batch update) and the span forward, kernel by
+ * kernel, with the replay's arguments.  Measured against graph replays of a 5-layer Qwen3-8B
+ * stage (profiles/r05/graph_gap_probe.json): 3-5 us less per step on the GPU, ~26 host kernel
+ * launches instead of one graph launch. */
+int inferd_span_step(InferdSpan* span, const InferdBatch* batch, int32_t advance, const int32_t* ids,
+                     const void* x_in, void* x_out, int32_t* next_ids, void* logits, void* stream);
 /* Sticky device error flags, read and cleared (synchronises the device).  Bit 0: a token id
  * outside [0, vocab) reached the embedding gather (it reads row 0 instead; the reference's
  * nn.Embedding raises IndexError, so the Python host validates ids before the launch);

@@ -54,6 +54,7 @@ SIGNATURES = {
     "inferd_span_graph_capture": (C.c_int, [c_p, C.POINTER(Batch), c_i32, c_p, c_p, c_p, c_p, c_p, c_p,
                                             C.POINTER(c_p)]),
     "inferd_graph_launch": (C.c_int, [c_p, c_p]),
+    "inferd_span_step": (C.c_int, [c_p, C.POINTER(Batch), c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
     "inferd_graph_destroy": (None, [c_p]),
     "inferd_span_error_flags": (C.c_int, [c_p, C.POINTER(c_i32)]),
     "inferd_span_kv_layer": (C.c_int, [c_p, c_i32, C.POINTER(c_p)]),

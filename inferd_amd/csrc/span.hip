@@ -793,16 +793,10 @@ struct InferdGraph {
   }
 };
 
-extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, int32_t advance, const int32_t* ids,
-                                         const void* x_in, void* x_out, int32_t* next_ids, void* logits,
-                                         void* stream, InferdGraph** out) {
-  if (!s || !b || !out) return fail(INFERD_ERR_ARG, "null argument");
-  if (!stream) return fail(INFERD_ERR_ARG, "graph capture needs a non-null stream");
-  if (advance && !b->decode) return fail(INFERD_ERR_ARG, "advance needs a decode batch");
-  hipStream_t st = (hipStream_t)stream;
-  s->prof_on = false;  // event pairs are timed eagerly only (HIP cannot time captured events)
-  HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-  int rc = INFERD_OK;
+namespace {
+// the scheduler step of a decode replay (advance) + the forward, on `st` (captured or eager)
+int step_body(InferdSpan* s, const InferdBatch* b, int32_t advance, const int32_t* ids, const void* x_in, void* x_out,
+              int32_t* next_ids, void* logits, hipStream_t st) {
   if (advance && s->cfg.n_layers > 0) {  // run by layer 0's input norm (NormPrologue)
     s->adv = NormPrologue{};
     s->adv.positions = (int32_t*)b->positions;
@@ -817,8 +811,36 @@ extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, in
     launch_decode_advance((int32_t*)b->positions, (int32_t*)b->slots, (int32_t*)b->ctx_lens, b->block_table,
                           b->max_pages, b->n_seqs, s->err, st);
   }
-  rc = inferd_span_forward(s, b, ids, x_in, x_out, next_ids, logits, nullptr, stream);
+  const int rc = inferd_span_forward(s, b, ids, x_in, x_out, next_ids, logits, nullptr, st);
   s->adv_pending = false;
+  return rc;
+}
+}  // namespace
+
+extern "C" int inferd_span_step(InferdSpan* s, const InferdBatch* b, int32_t advance, const int32_t* ids,
+                                const void* x_in, void* x_out, int32_t* next_ids, void* logits, void* stream) {
+  if (!s || !b) return fail(INFERD_ERR_ARG, "null argument");
+  if (advance && !b->decode) return fail(INFERD_ERR_ARG, "advance needs a decode batch");
+  return step_body(s, b, advance, ids, x_in, x_out, next_ids, logits, (hipStream_t)stream);
+}
+
+extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, int32_t advance, const int32_t* ids,
+                                         const void* x_in, void* x_out, int32_t* next_ids, void* logits,
+                                         void* stream, InferdGraph** out) {
+  if (!s || !b || !out) return fail(INFERD_ERR_ARG, "null argument");
+  if (!stream) return fail(INFERD_ERR_ARG, "graph capture needs a non-null stream");
+  if (advance && !b->decode) return fail(INFERD_ERR_ARG, "advance needs a decode batch");
+  hipStream_t st = (hipStream_t)stream;
+  s->prof_on = false;  // event pairs are timed eagerly only (HIP cannot time captured events)
+  HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  const int rc = step_body(s, b, advance, ids, x_in, x_out, next_ids, logits, st);
+    s->adv = NormPrologue{};
+    s->adv.positions = (int32_t*)b->positions;
+    s->adv.slots = (int32_t*)b->slots;
+    s->adv.ctx_lens = (int32_t*)b->ctx_lens;
+    s->adv.block_table = b->block_table;
+    s->adv.max_pages = b->max_pages;
+    s->adv.B = b->n_seqs;
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(st, &g);
   if (rc) {

@@ -285,6 +285,13 @@ struct DecodeGraph : torch::CustomClassHolder {
   std::vector<at::Tensor> keep;
   at::Device device;
   InferdGraph* graph = nullptr;
+  // what launch_eager() passes to inferd_span_step (the captured replay's arguments)
+  InferdBatch batch{};
+  const int32_t* p_ids = nullptr;
+  const void* p_x = nullptr;
+  void* p_out = nullptr;
+  int32_t* p_next = nullptr;
+  void* p_logits = nullptr;
 
   DecodeGraph(int64_t span_, int64_t table_, std::vector<int64_t> seqs_, int64_t n_steps_,
               std::optional<at::Tensor> ids, std::optional<at::Tensor> x, std::optional<at::Tensor> x_out,
@@ -324,6 +331,12 @@ struct DecodeGraph : torch::CustomClassHolder {
     (void)hipStreamWaitEvent(cur, ev, 0);
     (void)hipEventDestroy(ev);
     ok(rc, "DecodeGraph: graph_capture");
+    batch = b;
+    p_ids = (const int32_t*)opt_ptr(ids);
+    p_x = opt_ptr(x);
+    p_out = (void*)opt_ptr(x_out);
+    p_next = (int32_t*)opt_ptr(next_ids);
+    p_logits = (void*)opt_ptr(logits);
   }
   ~DecodeGraph() override {
     if (graph) inferd_graph_destroy(graph);
@@ -336,6 +349,17 @@ struct DecodeGraph : torch::CustomClassHolder {
     // the host page table follows the device-side advance: one native call per replay
     ok(inferd_kv_advance_many(handle<InferdKvTable>(table, "DecodeGraph"), seqs.data(), (int32_t)seqs.size(), 1),
        "DecodeGraph.launch: kv_advance");
+  }
+  // the same step launched kernel by kernel (no graph: no per-replay graph launch cost on the GPU)
+  void launch_eager() {
+    TORCH_CHECK(launched < n_steps, "decode graph ran out of reserved steps (", n_steps, ")");
+    c10::hip::HIPGuard g(device.index());
+    ok(inferd_span_step(handle<InferdSpan>(span, "DecodeGraph"), &batch, 1, p_ids, p_x, p_out, p_next, p_logits,
+                        stream_of(device)),
+       "DecodeGraph.launch_eager");
+    ++launched;
+    ok(inferd_kv_advance_many(handle<InferdKvTable>(table, "DecodeGraph"), seqs.data(), (int32_t)seqs.size(), 1),
+       "DecodeGraph.launch_eager: kv_advance");
   }
   int64_t steps_left() const { return n_steps - launched; }
 };
@@ -370,5 +394,6 @@ TORCH_LIBRARY(inferd, m) {
                        std::optional<at::Tensor>, std::optional<at::Tensor>, std::optional<at::Tensor>,
                        std::optional<at::Tensor>, at::Device>())
       .def("launch", &DecodeGraph::launch)
+      .def("launch_eager", &DecodeGraph::launch_eager)
       .def("steps_left", &DecodeGraph::steps_left);
 }

@@ -196,6 +196,11 @@ class DecodeGraph:
             with torch.cuda.stream(stream):
                 self.graph.launch()
 
+    def launch_eager(self):
+        """The same step launched kernel by kernel on the current stream (inferd_span_step): no
+        graph launch on the GPU, host launch time instead."""
+        self.graph.launch_eager()
+
 
 class SpanRuntime:
     """One layer span on one GPU (FirstStage / StageInner / LastStage compute)."""

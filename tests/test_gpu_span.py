@@ -717,3 +717,33 @@ def test_q8b_decode_ragged_contexts_vs_oracle():
             assert e < TOL_REL, (step, lens[b], e)
     s.check_errors()
     print(f"ragged decode, 16 sequences of 1..1500 cached tokens, 6 steps: worst rel err {worst:.2e}")
+
+
+def test_eager_step_equals_graph_replay():
+    """DecodeGraph.launch_eager (inferd_span_step: the replay's scheduler step and forward
+    launched kernel by kernel) walks the sequences exactly as graph replays do: two identical
+    Qwen3-0.6B 2-layer spans, one replaying its graph and one stepping eagerly, give bit-identical
+    hidden states over 6 steps, with the steps interleaved on the eager span too."""
+    from inferd_amd.runtime import DecodeGraph
+    d = R.CONFIGS["qwen3-0.6b"]
+    B, T, STEPS = 3, 20, 6
+    gen = torch.Generator().manual_seed(51)
+    x_pre = (torch.randn(B * T, d.hidden, generator=gen) * 0.5).to(torch.bfloat16)
+    steps = [(torch.randn(B, d.hidden, generator=gen) * 0.5).to(torch.bfloat16) for _ in range(STEPS)]
+    outs = []
+    for mode in ("graph", "eager", "mixed"):
+        s = span("qwen3-0.6b", 3, 2, False, False, kv_pages=8, max_tokens=B * T, max_seqs=B, max_positions=256)
+        sess = [f"e{b}" for b in range(B)]
+        s.forward([(sid, T) for sid in sess], x=x_pre.to(DEV), want_hidden=False)
+        xin = torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV)
+        hout = torch.zeros(B, d.hidden, dtype=torch.bfloat16, device=DEV)
+        g = DecodeGraph(s, sess, STEPS, x=xin, hidden_out=hout)
+        seq = []
+        for k in range(STEPS):
+            xin.copy_(steps[k])
+            eager = mode == "eager" or (mode == "mixed" and k % 2)
+            (g.launch_eager if eager else g.launch)()
+            seq.append(hout.cpu().clone())
+        s.check_errors()
+        outs.append(torch.stack(seq))
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
