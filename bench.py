@@ -279,13 +279,14 @@ def range_bytes(d, r, B: int, ctx_mean: float, lm_head: bool) -> float:
 
 
 def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int, warmup: int = 3,
-             reps: int = 20) -> float:
+             reps: int = 20, eager: bool = True) -> float:
     """One stage (StageRange r, with the embedding when first and final norm + lm_head + argmax
     when last) measured alone on this GPU: the span is built, B sequences are prefilled with
     ctx tokens through the real prefill path (stage 0 from random ids, later stages from random
     hidden states / records), one microbatch's decode step is captured as the stage's decode
-    graph, and `reps` replays are timed with HIP events on the launch stream outside the graph
-    (after `warmup` replays).  Returns ms per replay."""
+    graph, and `reps` steps are timed with HIP events on the launch stream (after `warmup` steps),
+    each stepped as the pipeline steps it: eagerly (DecodeGraph.launch_eager, the default) or as
+    the graph's replay (eager=False).  Returns ms per step."""
     from inferd_amd.runtime import DecodeGraph, SpanRuntime
     chunk = 2
     span = SpanRuntime(d, r.first_layer, r.n_layers, has_embed=first, has_lm_head=last,
@@ -313,13 +314,14 @@ def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int,
                                          dtype=torch.bfloat16, device=dev)
     nid = torch.empty(B, dtype=torch.int32, device=dev) if last else None
     graph = DecodeGraph(span, sess, warmup + reps, ids=ids, x=x, hidden_out=hout, next_ids=nid)
+    go = graph.launch_eager if eager else graph.launch     # eager: the same step kernel by kernel
     for _ in range(warmup):
-        graph.launch()
+        go()
     stream = torch.cuda.current_stream(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(reps):
-        graph.launch()
+        go()
     e1.record(stream)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / reps
@@ -498,7 +500,7 @@ def cpu_config1(seed: int, steps: int = 16) -> dict:
 # ------------------------------------------------------------------ main
 def pipeline_run(d, ranges, rank: int, world: int, dev, dist, args, profile: bool = True) -> dict:
     """One pipeline measurement on this rank: build the stage of `ranges`, prefill every
-    microbatch (untimed), W warm-up and K timed decode steps (one captured graph replay per stage
+    microbatch (untimed), W warm-up and K timed decode steps (one decode-graph step per stage
     per microbatch step) between barriers, then the eager event-timed kernel profile.  Times are
     the max over ranks."""
     from inferd_amd import pipeline as P
@@ -524,7 +526,7 @@ def pipeline_run(d, ranges, rank: int, world: int, dev, dist, args, profile: boo
     if dist:
         dist.barrier()
     t_prefill = time.perf_counter() - t0
-    # ---- decode: warmup + timed (one captured HIP graph replay per stage per microbatch step)
+    # ---- decode: warmup + timed (one decode-graph step per stage per microbatch step, launched eagerly)
     st.prepare_decode(W + K)
     st.decode(W)
     torch.cuda.synchronize()

@@ -518,10 +518,14 @@ def measured_split(n_layers: int, n: int, intermediate: int, o_cuts: bool = True
 
 
 class SpanExecutor:
-    """Runs one span's compute for pipeline items on this rank's GPU."""
+    """Runs one span's compute for pipeline items on this rank's GPU.  A decode item is one step of
+    the microbatch's DecodeGraph: launched kernel by kernel (eager, the default: inferd_span_step,
+    bit-identical to the replay and 6-8 us faster per stage step on the GPU, profiles/r05/
+    stage_eager_ab.json) or as the captured graph's replay (eager=False)."""
 
-    def __init__(self, span: SpanRuntime):
+    def __init__(self, span: SpanRuntime, eager: bool = True):
         self.span = span
+        self.eager = eager
         self.device = span.device
         self.dims = span.dims
         self.has_embed, self.has_lm_head = span.has_embed, span.has_lm_head
@@ -543,7 +547,10 @@ class SpanExecutor:
                        for m, sessions in enumerate(microbatches)]
 
     def decode(self, m):
-        self.graphs[m].launch()
+        if self.eager:
+            self.graphs[m].launch_eager()
+        else:
+            self.graphs[m].launch()
 
     def profile_decode(self, microbatches, bufs, n_steps):
         """Eager (non-graph) decode steps with per-kernel-class HIP events on the launch
@@ -571,7 +578,7 @@ class PipelineStage:
                  executor=None, group=None, profile: str = "random", want_logits: bool = False,
                  skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
                  gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False,
-                 qkv_split_first: bool = False, qkv_split_last: bool = False):
+                 qkv_split_first: bool = False, qkv_split_last: bool = False, eager_decode: bool = True):
         """profile: the synthetic weight profile (runtime.SpanRuntime.init_synthetic: "peaked"
         for token-exact parity runs).  want_logits (last stage): every decode step's and the
         prefill's last-row logits are kept, for parity checks against the oracle's.
@@ -598,7 +605,7 @@ class PipelineStage:
                                o_split_last=o_split_last, qkv_split_first=qkv_split_first,
                                qkv_split_last=qkv_split_last)
             span.init_synthetic(seed, profile)
-            executor = SpanExecutor(span)
+            executor = SpanExecutor(span, eager=eager_decode)
         self.ex = executor
         self.span = getattr(executor, "span", None)
         self.sessions = [[("mb", m, b) for b in range(batch)] for m in range(n_microbatches)]
