@@ -747,3 +747,22 @@ def test_eager_step_equals_graph_replay():
         s.check_errors()
         outs.append(torch.stack(seq))
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+def test_record_boundaries_refuse_multi_call_forwards():
+    """A forward whose hand-off is a record is one engine call: an attention|o span refuses a
+    request larger than its workspace (chunked prefill would need one record per chunk), a
+    q/k/v|attention span refuses a non-decode call planned with a one-token-pieces engine call,
+    and a span ending before o always hands over its record (want_hidden=False refused)."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["qwen3-0.6b"]
+    so = SpanRuntime(d, 1, 2, has_embed=False, has_lm_head=False, device=DEV, kv_pages=16, max_tokens=64,
+                     max_seqs=4, o_split_last=True)
+    so.init_synthetic(SEED)
+    x = torch.zeros(100, d.hidden, dtype=torch.bfloat16)
+    with pytest.raises(ValueError, match="one engine call"):
+        so.forward([("a", 100)], x=x)
+    with pytest.raises(ValueError, match="always hands over its record"):
+        so.forward([("b", 10)], x=x[:10], want_hidden=False)
+    out = so.forward([("c", 10)], x=x[:10])
+    assert out["record"].numel() == 10 * d.hidden + 10 * d.heads * d.head_dim
