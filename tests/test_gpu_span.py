@@ -751,9 +751,8 @@ def test_eager_step_equals_graph_replay():
 
 def test_record_boundaries_refuse_multi_call_forwards():
     """A forward whose hand-off is a record is one engine call: an attention|o span refuses a
-    request larger than its workspace (chunked prefill would need one record per chunk), a
-    q/k/v|attention span refuses a non-decode call planned with a one-token-pieces engine call,
-    and a span ending before o always hands over its record (want_hidden=False refused)."""
+    request larger than its workspace (chunked prefill would need one record per chunk), and a span
+    ending before o always hands over its record (want_hidden=False refused)."""
     from inferd_amd.runtime import MODELS, SpanRuntime
     d = MODELS["qwen3-0.6b"]
     so = SpanRuntime(d, 1, 2, has_embed=False, has_lm_head=False, device=DEV, kv_pages=16, max_tokens=64,
