@@ -361,6 +361,28 @@ def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: 
     return out
 
 
+def projected_scaling(proj: dict, one_gpu: float) -> dict:
+    """The 1/2/4/8-GPU curve the stage projection implies (compute only, no hand-off): per stage
+    count the even split's (BASELINE config 3), the fastest split's and the best-balanced split's
+    (highest lowest-stage HBM fraction) projected tokens/s, with efficiency against N x this
+    run's one-GPU value."""
+    out = {"1": {"tokens_per_s": round(one_gpu, 1)}}
+    for n in (2, 4, 8):
+        cand = {k: v for k, v in proj.items() if k.endswith(str(n)) and not k.startswith("config4")}
+        if f"even{n}" not in cand:
+            continue
+        fast = max(cand, key=lambda k: cand[k]["projected_tokens_per_s"])
+        bal = max(cand, key=lambda k: cand[k]["min_frac_at_tick"])
+        ev = cand[f"even{n}"]["projected_tokens_per_s"]
+        row = {"even": ev, "even_efficiency": round(ev / (n * one_gpu), 3)}
+        for tag, k in (("fastest", fast), ("balanced", bal)):
+            row[tag] = {"split": k, "tokens_per_s": cand[k]["projected_tokens_per_s"],
+                        "efficiency": round(cand[k]["projected_tokens_per_s"] / (n * one_gpu), 3),
+                        "min_stage_frac": cand[k]["min_frac_at_tick"]}
+        out[str(n)] = row
+    return out
+
+
 def sub_split(d, n: int, o_cuts: bool):
     """The sub-layer splits (pipeline.gateup_split: gate/up boundaries; o_cuts: attention|o
     boundaries too) on the measured boundary-cost table where one exists for the model
@@ -703,6 +725,7 @@ def main():
             # the 2/4/8-GPU splits, every stage's decode graph timed alone on this GPU
             st.release()
             out["stage_projection"] = stage_projection(d, projection_splits(d, B, ctx), B, ctx, dev, args.seed)
+            out["projected_scaling"] = projected_scaling(out["stage_projection"], value)
         if world == 1 and not args.no_cpu_baseline:
             st.release()
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)
