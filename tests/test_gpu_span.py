@@ -271,34 +271,38 @@ def test_half_layer_stage_chain_bit_exact():
         s.check_errors()
 
 
-@pytest.mark.parametrize("T", [70, 9], ids=["prefill_h1", "prefill_record"])
+@pytest.mark.parametrize("T", [70, 9, (70, 9, 33), (30, 9, 17)],
+                         ids=["prefill_h1", "prefill_record", "ragged_h1", "ragged_record"])
 def test_gateup_boundary_chain_bit_exact(T):
     """Stage boundaries inside a layer's gate/up projection (InferdSpanConfig gateup_split_*):
     Qwen3-0.6B layers 0..3 as [0..1a+1024] (embed), [1m@1024..2a+2048], [2m@2048..3] (lm_head)
     give bit-identical logits to one span: a prefill of 3 sequences (T = 70: 210 rows, h1
     hand-offs, the receiver runs the whole MLP; T = 9: 27 rows, decode-sized calls with record
     hand-offs), then 5 decode-graph steps whose hand-offs are records (h1, then act columns
-    [0, c) fragment-packed, completed in place by the receiver)."""
+    [0, c) fragment-packed, completed in place by the receiver).  A tuple T gives ragged prompts
+    (112 rows: h1 hand-offs; 56 rows: records)."""
     from inferd_amd.pipeline import StageRange, handoff_elems, record_elems
     from inferd_amd.runtime import DecodeGraph
     d = R.CONFIGS["qwen3-0.6b"]
     B, STEPS = 3, 5
     gen = torch.Generator().manual_seed(41)
-    prompts = torch.randint(0, d.vocab, (B, T), generator=gen)
+    lens = T if isinstance(T, tuple) else (T,) * B
+    ids = torch.randint(0, d.vocab, (sum(lens),), generator=gen)
     forced = torch.randint(0, d.vocab, (STEPS, B), generator=gen)
     ranges = [StageRange(0, 3, 0, 1024), StageRange(3, 2, 1024, 2048), StageRange(5, 3, 2048, 0)]
-    chain = [span("qwen3-0.6b", r.first_layer, r.n_layers, i == 0, i == 2, kv_pages=16, max_tokens=B * T + 64,
+    chain = [span("qwen3-0.6b", r.first_layer, r.n_layers, i == 0, i == 2, kv_pages=16, max_tokens=sum(lens) + 64,
                   max_seqs=B, max_positions=1024, **r.span_kwargs()) for i, r in enumerate(ranges)]
-    one = span("qwen3-0.6b", 0, 4, True, True, kv_pages=16, max_tokens=B * T + 64, max_seqs=B, max_positions=1024)
+    one = span("qwen3-0.6b", 0, 4, True, True, kv_pages=16, max_tokens=sum(lens) + 64, max_seqs=B,
+               max_positions=1024)
     sess = [f"g{b}" for b in range(B)]
-    reqs = [(sid, T) for sid in sess]
-    o0 = chain[0].forward(reqs, ids=prompts.reshape(-1))
+    reqs = [(sid, n) for sid, n in zip(sess, lens)]
+    o0 = chain[0].forward(reqs, ids=ids)
     h0 = o0.get("record", o0["hidden"])
     o1 = chain[1].forward(reqs, x=h0)
     h1 = o1.get("record", o1["hidden"])
-    assert ("record" in o0) == (B * T <= 64)
+    assert ("record" in o0) == (sum(lens) <= 64)
     lc = chain[2].forward(reqs, x=h1, want_logits=True, want_hidden=False)["logits"]
-    lo = one.forward(reqs, ids=prompts.reshape(-1), want_logits=True, want_hidden=False)["logits"]
+    lo = one.forward(reqs, ids=ids, want_logits=True, want_hidden=False)["logits"]
     assert torch.equal(lc, lo), (lc.float() - lo.float()).abs().max()
     ids_c = torch.zeros(B, dtype=torch.int32, device=DEV)
     ids_o = torch.zeros(B, dtype=torch.int32, device=DEV)
@@ -324,9 +328,10 @@ def test_gateup_boundary_chain_bit_exact(T):
         s.check_errors()
 
 
-@pytest.mark.parametrize("split,T", [("o", 70), ("o", 9), ("o_gateup", 9), ("q", 70), ("q", 9), ("q_o", 9)],
+@pytest.mark.parametrize("split,T", [("o", 70), ("o", 9), ("o_gateup", 9), ("q", 70), ("q", 9), ("q_o", 9),
+                                     ("o", (70, 9, 33)), ("q_o", (70, 9, 33))],
                          ids=["o_prefill_rows", "o_prefill_small", "o_then_gateup", "q_prefill_rows", "q_prefill_small",
-                              "q_then_o"])
+                              "q_then_o", "o_ragged", "q_then_o_ragged"])
 def test_o_boundary_chain_bit_exact(split, T):
     """Stage boundaries between a layer's attention and its o projection (InferdSpanConfig
     o_split_*): Qwen3-0.6B layers 0..3 as [0..1q] (embed), [1o..3q], [3o..3] (lm_head) -- or
@@ -337,15 +342,18 @@ def test_o_boundary_chain_bit_exact(split, T):
     the oracle's.  "q" / "q_o": q/k/v|attention boundaries (InferdSpanConfig qkv_split_*) in
     place of the first (and second) ones -- prefill hands over x alone and the receiver runs the
     whole layer; decode records carry x and the raw q/k/v rows (split-K slices summed by the
-    sender as the fused attention sums them)."""
+    sender as the fused attention sums them).  A tuple T gives ragged prompts (one length per sequence):
+    the prefill record's rows and every decode step's contexts then differ per sequence."""
     from inferd_amd.pipeline import StageRange, buffer_elems, o_record_elems, unpack_rows
     from inferd_amd.runtime import DecodeGraph
     d = R.CONFIGS["qwen3-0.6b"]
     B, STEPS = 3, 5
     Hd = d.heads * d.head_dim
     gen = torch.Generator().manual_seed(43)
-    prompts = torch.randint(0, d.vocab, (B, T), generator=gen)
+    lens = T if isinstance(T, tuple) else (T,) * B
+    prompts = [torch.randint(0, d.vocab, (n,), generator=gen) for n in lens]
     forced = torch.randint(0, d.vocab, (STEPS, B), generator=gen)
+    N = sum(lens)
     if split == "o":
         ranges = [StageRange(0, 3, last_o=True), StageRange(2, 5, first_o=True, last_o=True),
                   StageRange(6, 2, first_o=True)]
@@ -357,22 +365,31 @@ def test_o_boundary_chain_bit_exact(split, T):
                   StageRange(6, 2, first_o=True)]
     else:
         ranges = [StageRange(0, 3, last_o=True), StageRange(2, 3, 0, 1024, first_o=True), StageRange(5, 3, 1024, 0)]
-    chain = [span("qwen3-0.6b", r.first_layer, r.n_layers, i == 0, i == 2, kv_pages=16, max_tokens=B * T + 64,
+    chain = [span("qwen3-0.6b", r.first_layer, r.n_layers, i == 0, i == 2, kv_pages=16, max_tokens=N + 64,
                   max_seqs=B, max_positions=1024, **r.span_kwargs()) for i, r in enumerate(ranges)]
-    one = span("qwen3-0.6b", 0, 4, True, True, kv_pages=16, max_tokens=B * T + 64, max_seqs=B, max_positions=1024)
+    one = span("qwen3-0.6b", 0, 4, True, True, kv_pages=16, max_tokens=N + 64, max_seqs=B, max_positions=1024)
     sess = [f"o{b}" for b in range(B)]
-    reqs = [(sid, T) for sid in sess]
-    o0 = chain[0].forward(reqs, ids=prompts.reshape(-1))
+    reqs = [(sid, n) for sid, n in zip(sess, lens)]
+    ids = torch.cat(prompts)
+    o0 = chain[0].forward(reqs, ids=ids)
     qsplit = split.startswith("q")
     rec0 = o0["hidden"].reshape(-1) if qsplit else o0["record"]
-    assert rec0.numel() == (B * T * d.hidden if qsplit else o_record_elems(d, B * T, False))
+    assert rec0.numel() == (N * d.hidden if qsplit else o_record_elems(d, N, False))
     o1 = chain[1].forward(reqs, x=rec0)
     lc = chain[2].forward(reqs, x=o1.get("record", o1["hidden"]), want_logits=True, want_hidden=False)["logits"]
-    lo = one.forward(reqs, ids=prompts.reshape(-1), want_logits=True, want_hidden=False)["logits"]
+    lo = one.forward(reqs, ids=ids, want_logits=True, want_hidden=False)["logits"]
     assert torch.equal(lc, lo), (lc.float() - lo.float()).abs().max()
-    xr, ar = R.RefSpan(d, SEED, 0, 1, True, False, o_split_last=not qsplit, qkv_split_last=qsplit).forward(prompts)
-    ex = rel_err(rec0[:B * T * d.hidden].reshape(B, T, -1), xr)
-    ea = 0.0 if qsplit else rel_err(rec0[B * T * d.hidden:].reshape(B, T, -1), ar)
+    ref = R.RefSpan(d, SEED, 0, 1, True, False, o_split_last=not qsplit, qkv_split_last=qsplit)
+    xa = rec0[:N * d.hidden].view(N, -1)
+    aa = None if qsplit else rec0[N * d.hidden:].view(N, -1)
+    ex = ea = 0.0
+    off = 0
+    for p in prompts:   # per sequence (ragged prompts: each its own oracle forward)
+        xr, ar = ref.forward(p.view(1, -1))
+        ex = max(ex, rel_err(xa[off:off + len(p)].view(1, len(p), -1), xr))
+        if aa is not None:
+            ea = max(ea, rel_err(aa[off:off + len(p)].view(1, len(p), -1), ar))
+        off += len(p)
     print(f"{split} record vs oracle: x rel err {ex:.2e}, attention output rel err {ea:.2e}")
     assert ex < TOL_REL and ea < TOL_REL
     ids_c = torch.zeros(B, dtype=torch.int32, device=DEV)
