@@ -768,10 +768,15 @@ __device__ __forceinline__ void tile_order_v(const SplitTail& st, int grid_m, in
       sidx = x * (st.tiles_per_xcd - st.full_per_xcd) + j / st.split;
     }
   }
-#ifndef W4_GM
-#define W4_GM 8
+  // row-group depth: 8 row blocks up to 8192 rows (M <= 16383), 4 beyond.  Per-shape A/Bs of the
+  // 32B projections (profiles/r05/gemm_gm_ab*.txt): at M = 32768 (config 5, B = 4) GM = 4 ran
+  // gate/up 6.8 %, q/k/v 4.8 %, down 1.2 % faster than 8 (A = 335 MB no longer stays in the
+  // Infinity Cache, so shallower groups keep each XCD's A panels hot); at M = 8192 within 0-2 %.
+#ifdef W4_GM
+  constexpr int GM = W4_GM;  // lab builds pin it (tools/build_probes.sh)
+#else
+  const int GM = grid_m >= 64 ? 4 : 8;
 #endif
-  constexpr int GM = W4_GM;  // lab builds vary it (tools/build_probes.sh)
   const int group = tile / (GM * grid_n);
   const int first_m = group * GM;
   const int gsz = min(grid_m - first_m, GM);

@@ -138,13 +138,15 @@ def test_gemm_swiglu(lib, M, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 512, 192), (777, 768, 1088), (2048, 1024, 4096), (1300, 256, 640),
-                                   (4096, 2048, 1024), (8092, 4096, 448), (300, 384, 1024)])
+                                   (4096, 2048, 1024), (8092, 4096, 448), (300, 384, 1024), (16500, 1024, 256),
+                                   (20000, 2048, 512)])
 def test_gemm_prefill_bodies(lib, M, N, K):
     """The prefill GEMM bodies on ragged M, short and long K, all epilogues: persistent
     gemm_w4p; gemm_w4 with the tail split ((2048, 1024, 4096) and (4096, 2048, 1024) cut K
     8 / 2 ways); (8092, 4096, 448): 512 whole tiles, so w4p walks two tiles per workgroup
     (ragged last row block, cross-tile prefetch, exact-count epilogue waits); (300, 384,
-    1024): the 128x128 gemm_tiled."""
+    1024): the 128x128 gemm_tiled; (16500, 1024, 256) and (20000, 2048, 512): >= 64 row blocks
+    (ragged), so tile_order_v's row groups are 4 blocks deep."""
     torch.manual_seed(M + N + K)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.03).to(torch.bfloat16)
