@@ -41,6 +41,9 @@ def test_decode_graph_class_registered():
     for name in O.CLASSES:
         cls = getattr(torch.classes.inferd, name)
         assert cls is not None
+    # its methods: graph replay, the same step launched kernel by kernel, the steps left
+    names = {str(x).split("(")[0] for x in torch._C._jit_get_custom_class_schemas() if "inferd.DecodeGraph _0" in str(x)}
+    assert {"__init__", "launch", "launch_eager", "steps_left"} <= names, names
     # a DecodeGraph needs a GPU device; the schema refuses a CPU one before touching a handle
     with pytest.raises(RuntimeError, match="GPU"):
         torch.classes.inferd.DecodeGraph(1, 1, [0], 1, None, None, None, None, None, torch.device("cpu"))
