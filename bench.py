@@ -130,6 +130,15 @@ def parse():
                    help="N > 1 runs of the even split: skip the second measurement on the sub-layer split")
     p.add_argument("--no-stage-projection", action="store_true",
                    help="N=1 decode runs: skip the per-stage projection of the 2/4/8-GPU splits")
+    p.add_argument("--head", choices=("vocab", "last"), default="vocab",
+                   help="N > 1: vocab = the greedy head vocab-parallel over the stages (lm_head shards sized by "
+                        "head_shards, the normed rows and running keys handed round the ring; the default), last = the "
+                        "whole lm_head on the last stage (the reference's LastStage)")
+    p.add_argument("--ring-slack", type=int, default=1,
+                   help="microbatches in flight beyond the ring's minimum (S, or 2S with the vocab-parallel head)")
+    p.add_argument("--no-calibrate", action="store_true",
+                   help="N > 1, vocab head: size the lm_head shards from the cost table only (default: every rank "
+                        "times its own stage first and the shards are re-balanced on the measured times)")
     p.add_argument("--prefill-layers", type=int, default=8)
     p.add_argument("--prefill-batch", type=int, default=1)
     p.add_argument("--prefill-len", type=int, default=8192)
@@ -278,31 +287,97 @@ def range_bytes(d, r, B: int, ctx_mean: float, lm_head: bool) -> float:
     return nb
 
 
+# a vocab-parallel lm_head shard's fixed cost per decode step (its GEMV's ramp and tail, the key
+# reduction, two launches), us; the per-row cost is the whole head's (cost table "head" less the
+# final norm) / vocab.
+HEAD_SHARD_FIXED_US = 7.0
+FINAL_NORM_US = 5.5
+
+
+def stage_base_us(d, ranges, B: int, ctx: int, head_last: bool = False):
+    """Predicted decode time of each stage's layers (+ embedding on stage 0; the whole head on the last
+    with head_last, else its final norm), us, and the whole head's GEMV cost: the measured cost table
+    (pipeline.load_decode_costs) where one exists for the model, else bytes at 5 TB/s."""
+    from inferd_amd import pipeline as P
+    name = d.name.replace("-", "_")
+    S = len(ranges)
+    if os.path.exists(os.path.join(os.path.dirname(P.__file__), "data", f"decode_costs_{name}.json")):
+        cal = P.load_decode_costs(name)
+        base = [P.predicted_stage_us(r, cal, s == 0, head_last and s == S - 1) for s, r in enumerate(ranges)]
+        head_us = cal["head"] - FINAL_NORM_US
+    else:
+        base = [range_bytes(d, r, B, ctx, head_last and s == S - 1) / 5e3 for s, r in enumerate(ranges)]
+        head_us = d.vocab * d.hidden * 2 / 5e3
+    if not head_last:
+        base[-1] += FINAL_NORM_US
+    return base, head_us
+
+
+def head_shards(d, ranges, B: int, ctx: int, stage_us=None):
+    """(first, rows) of the vocab-parallel lm_head per stage (pipeline.head_shard_split): the shards
+    level the stages' decode times -- each stage's layer time (stage_us: measured, e.g. by the
+    per-rank calibration; else stage_base_us's prediction) plus its shard's GEMV."""
+    from inferd_amd.pipeline import head_shard_split
+    base, head_us = stage_base_us(d, ranges, B, ctx)
+    if stage_us is not None:
+        base = list(stage_us)
+    step = 128 if d.vocab % 128 == 0 else 16
+    return head_shard_split(base, d.vocab, head_us, HEAD_SHARD_FIXED_US, step)
+
+
+class _StageHead:
+    """A stage's part of the vocab-parallel head, as PipelineStage._head runs it each ring
+    iteration: stage 0 starts the running keys, a middle stage folds its shard in, the last stage
+    finishes the argmax (a stage without rows only passes keys on / decodes them)."""
+
+    def __init__(self, span, first: bool, last: bool, B: int, dev, normed=None, ids=None):
+        self.span, self.first, self.last, self.B = span, first, last, B
+        self.normed = normed if normed is not None else torch.zeros(span.normed_elems(B), dtype=torch.bfloat16,
+                                                                    device=dev)
+        self.keys = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.ids = ids if ids is not None else torch.zeros(B, dtype=torch.int32, device=dev)
+
+    def __call__(self):
+        if self.span.head_range[1]:
+            self.span.head_shard(self.normed, self.B, keys_in=None if self.first else self.keys,
+                                 keys_out=None if self.last else self.keys, ids=self.ids if self.last else None)
+        elif self.last:
+            torch.ops.inferd.argmax_combine(self.keys, 1, self.B, self.ids)
+        elif self.first:
+            self.keys.zero_()
+
+
 def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int, warmup: int = 3,
-             reps: int = 20, eager: bool = True) -> float:
+             reps: int = 20, eager: bool = True, head=None, stats: dict | None = None) -> float:
     """One stage (StageRange r, with the embedding when first and final norm + lm_head + argmax
     when last) measured alone on this GPU: the span is built, B sequences are prefilled with
     ctx tokens through the real prefill path (stage 0 from random ids, later stages from random
     hidden states / records), one microbatch's decode step is captured as the stage's decode
     graph, and `reps` steps are timed with HIP events on the launch stream (after `warmup` steps),
     each stepped as the pipeline steps it: eagerly (DecodeGraph.launch_eager, the default) or as
-    the graph's replay (eager=False).  Returns ms per step."""
+    the graph's replay (eager=False).  head = (first row, rows): the greedy head runs
+    vocab-parallel -- this stage owns those lm_head rows and runs its shard after every step
+    (_StageHead), and the last stage ends with the final norm instead of the whole head.  Returns ms
+    per step (stats, a dict: "head_ms" = the head part alone, timed the same way)."""
     from inferd_amd.runtime import DecodeGraph, SpanRuntime
     chunk = 2
-    span = SpanRuntime(d, r.first_layer, r.n_layers, has_embed=first, has_lm_head=last,
+    vh = head is not None
+    hf, hr = head if vh else (0, 0)
+    span = SpanRuntime(d, r.first_layer, r.n_layers, has_embed=first, has_lm_head=last and not vh,
                        kv_pages=B * ((ctx + warmup + reps) // 64 + 2) + 4, max_tokens=chunk * ctx,
-                       max_seqs=B, max_positions=ctx + warmup + reps + 64, device=dev, **r.span_kwargs())
+                       max_seqs=B, max_positions=ctx + warmup + reps + 64, device=dev, head_first=hf, head_rows=hr,
+                       final_norm_out=last and vh, **r.span_kwargs())
     span.init_synthetic(seed)
     sess = [("proj", b) for b in range(B)]
     for c in range(0, B, chunk):
         reqs = [(sid, ctx) for sid in sess[c:c + chunk]]
         if first:
             ids = torch.randint(0, d.vocab, (len(reqs) * ctx,), generator=g, dtype=torch.int32)
-            span.forward(reqs, ids=ids, want_hidden=False, want_next_ids=last)
+            span.forward(reqs, ids=ids, want_hidden=False, want_next_ids=last and not vh)
         else:     # (a record x | attention output at an attention|o boundary)
             n_in = buffer_elems(d, len(reqs) * ctx, 0, r.first_o, False, r.first_q)
             x = (torch.randn(n_in, generator=g) * 0.5).to(torch.bfloat16)
-            span.forward(reqs, x=x, want_hidden=r.last_o or r.last_q, want_next_ids=last)
+            span.forward(reqs, x=x, want_hidden=r.last_o or r.last_q, want_next_ids=last and not vh)
     ids = torch.zeros(B, dtype=torch.int32, device=dev) if first else None
     x = None if first else (torch.randn(B, d.hidden, generator=g) * 0.5).to(torch.bfloat16).to(dev)
     if r.first_col or r.first_o or r.first_q:
@@ -313,8 +388,17 @@ def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int,
     hout = None if last else torch.empty(buffer_elems(d, B, r.last_col, r.last_o, True, r.last_q),
                                          dtype=torch.bfloat16, device=dev)
     nid = torch.empty(B, dtype=torch.int32, device=dev) if last else None
+    if vh and last:       # the final-normed rows; the ids come from the head shard
+        hout, nid = torch.zeros(span.normed_elems(B), dtype=torch.bfloat16, device=dev), None
     graph = DecodeGraph(span, sess, warmup + reps, ids=ids, x=x, hidden_out=hout, next_ids=nid)
-    go = graph.launch_eager if eager else graph.launch     # eager: the same step kernel by kernel
+    step = graph.launch_eager if eager else graph.launch     # eager: the same step kernel by kernel
+    go = step
+    if vh:
+        hd = _StageHead(span, first, last, B, dev, normed=hout if last else None)
+
+        def go():
+            step()
+            hd()
     for _ in range(warmup):
         go()
     stream = torch.cuda.current_stream(dev)
@@ -325,40 +409,111 @@ def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int,
     e1.record(stream)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / reps
+    if vh and stats is not None:
+        e0.record(stream)
+        for _ in range(reps):
+            hd()
+        e1.record(stream)
+        e1.synchronize()
+        stats["head_ms"] = e0.elapsed_time(e1) / reps
     span.check_errors()
     del graph, span
     torch.cuda.synchronize(dev)
     return ms
 
 
-def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: int = 3, reps: int = 20) -> dict:
+# the per-hop hand-off latency the ring projection charges (us): the RCCL self-loop proxy of a
+# record's send + receive on one GPU (tools/rccl_ring_probe.py -> the newest profiles/rccl_ring_probe_rNN.json)
+# plus the record's bytes over one xGMI link (~153 GB/s per direction); without a probe file, this
+HANDOFF_US_DEFAULT = 30.0
+XGMI_LINK_GBS = 153.0
+
+
+def handoff_us(nbytes: int) -> dict:
+    """The per-hop hand-off charge for a record of nbytes: {"us", "proxy_us", "link_us", "source"}."""
+    import glob
+    link = nbytes / (XGMI_LINK_GBS * 1e3)
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "rccl_ring_probe_r*.json")), reverse=True):
+        with open(fn) as f:
+            pr = json.load(f)
+        pts = sorted((int(k), v["gpu_us"]) for k, v in pr.get("self_loop", {}).items())
+        if pts:
+            b = min(pts, key=lambda p: abs(p[0] - nbytes))      # the nearest measured size
+            return {"us": round(b[1] + link, 2), "proxy_us": b[1], "link_us": round(link, 2),
+                    "source": os.path.basename(fn)}
+    return {"us": HANDOFF_US_DEFAULT, "proxy_us": None, "link_us": round(link, 2), "source": "default"}
+
+
+def ring_tick_us(c, h, vhead: bool, n_mb: int, x: float) -> float:
+    """The asynchronous ring's period (pipeline.PipelineStage) for stage times c[s] (layers + head
+    shard, us), head-shard parts h[s], per-hop hand-off latency x, n_mb microbatches in flight: no
+    stage faster than its own work, and no microbatch faster than its lap round the ring.  Whole head
+    (S hops per lap): n_mb P >= sum c + S x.  Vocab-parallel head: the ids of item i leave the last
+    stage one lap behind its layers, S P after its normed rows, so (n_mb - S) P >= sum (c - h) + h[S-1]
+    + S x (the layer path plus the last shard), and the normed rows reach stage 0's shard in time,
+    S P >= sum (c - h) - (c[0] - h[0]) + S x."""
+    S = len(c)
+    P = max(c)
+    if S == 1:
+        return P
+    L = [ci - hi for ci, hi in zip(c, h)]
+    if not vhead:
+        return max(P, (sum(c) + S * x) / n_mb)
+    return max(P, (sum(L) + h[-1] + S * x) / (n_mb - S), (sum(L) - L[0] + S * x) / S)
+
+
+def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: int = 3, reps: int = 20,
+                     slack: int = 1) -> dict:
     """Every stage of every split measured alone on this GPU with its real role (stage_ms:
-    embedding on stage 0, final norm + lm_head + argmax on the last).  The lockstep pipeline
-    (pipeline.py) ticks at its slowest stage, so per split: tick = max stage ms, each stage's
-    fraction of the HBM roofline at that tick = its algorithmic bytes / (tick x 8 TB/s) (SURVEY
-    §8(d)), bubble = 1 - sum / (S x tick), and the compute-only projected rate B / tick (one
-    microbatch of B sequences completes a decode step per tick: S microbatches in flight, each a
-    token every S ticks; the
-    xGMI hand-off excluded)."""
+    embedding on stage 0, final norm + lm_head + argmax on the last, or -- a split whose value is
+    {"ranges", "vhead": True} -- the greedy head vocab-parallel: every stage also runs its lm_head shard
+    (head_shards) and the last one the final norm).  Per split: tick = the slowest stage (compute
+    only); ring_tick = the asynchronous ring's period with the hand-off in it (ring_tick_us: n_mb =
+    ring_microbatches(S, vhead, slack), x = handoff_us of the 128 KB-and-up records); each stage's
+    fraction of the HBM roofline at the ring tick = its algorithmic bytes (+ its shard's rows x hidden x
+    2) / (ring tick x 8 TB/s), bubble = 1 - sum / (S x ring tick), and the projected rate
+    B / ring tick (one microbatch of B sequences completes a decode step per period)."""
+    from inferd_amd.pipeline import ring_microbatches
     out = {}
     g = torch.Generator(device="cpu").manual_seed(seed + 5)
-    for name, ranges in splits.items():
+    for name, sp in splits.items():
+        vhead = isinstance(sp, dict) and sp.get("vhead", False)
+        ranges = sp["ranges"] if isinstance(sp, dict) else sp
         S = len(ranges)
-        stages = []
+        shards = head_shards(d, ranges, B, ctx) if vhead else None
+        stages, hms = [], []
         for s, r in enumerate(ranges):
             last = s == S - 1
-            ms = stage_ms(d, r, s == 0, last, B, ctx, dev, g, seed, warmup, reps)
-            nb = range_bytes(d, r, B, ctx + warmup + (reps + 1) / 2.0, last)
-            stages.append({"range": r.label(), "units": r.n_units, "ms": round(ms, 4), "alg_bytes": int(nb),
-                           "frac_own": round(nb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+            st = {}
+            ms = stage_ms(d, r, s == 0, last, B, ctx, dev, g, seed, warmup, reps, head=shards[s] if vhead else None,
+                          stats=st)
+            nb = range_bytes(d, r, B, ctx + warmup + (reps + 1) / 2.0, last and not vhead)
+            if vhead:
+                nb += shards[s][1] * d.hidden * 2
+            hms.append(st.get("head_ms", 0.0))
+            row = {"range": r.label(), "units": r.n_units, "ms": round(ms, 4), "alg_bytes": int(nb),
+                   "frac_own": round(nb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            if vhead:
+                row.update(head_rows=shards[s][1], head_ms=round(hms[-1], 4))
+            stages.append(row)
         tick = max(st["ms"] for st in stages)
+        n_mb = ring_microbatches(S, vhead, slack)
+        x = handoff_us(B * d.hidden * 2)
+        rt = ring_tick_us([st["ms"] * 1e3 for st in stages], [v * 1e3 for v in hms], vhead, n_mb, x["us"]) * 1e-3
         for st in stages:
-            st["frac_at_tick"] = round(st["alg_bytes"] / (tick * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-        out[name] = {"stages": stages, "tick_ms": tick,
+            st["frac_at_tick"] = round(st["alg_bytes"] / (rt * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        out[name] = {"stages": stages, "tick_ms": tick, "ring_tick_ms": round(rt, 4), "microbatches": n_mb,
+                     "handoff_us": x, "vocab_parallel_head": vhead,
                      "min_frac_at_tick": min(st["frac_at_tick"] for st in stages),
-                     "bubble_frac": round(1 - sum(st["ms"] for st in stages) / (S * tick), 4),
-                     "projected_tokens_per_s": round(B / (tick * 1e-3), 1)}
+                     "bubble_frac": round(1 - sum(st["ms"] for st in stages) / (S * rt), 4),
+                     "projected_tokens_per_s": round(B / (rt * 1e-3), 1)}
     return out
+
+
+def projection_summary(proj: dict) -> dict:
+    """The compact per-split view of stage_projection: {split: [ring tick ms, lowest stage's HBM
+    fraction at it, bubble]} (the per-stage detail stays under stage_projection)."""
+    return {k: [v["ring_tick_ms"], v["min_frac_at_tick"], v["bubble_frac"]] for k, v in proj.items()}
 
 
 def projected_scaling(proj: dict, one_gpu: float) -> dict:
@@ -375,6 +530,11 @@ def projected_scaling(proj: dict, one_gpu: float) -> dict:
         bal = max(cand, key=lambda k: cand[k]["min_frac_at_tick"])
         ev = cand[f"even{n}"]["projected_tokens_per_s"]
         row = {"even": ev, "even_efficiency": round(ev / (n * one_gpu), 3)}
+        if f"vhead_even{n}" in cand:      # config 3's even split with the vocab-parallel head (the bench's N > 1 default)
+            v = cand[f"vhead_even{n}"]
+            row["even_vocab_head"] = {"tokens_per_s": v["projected_tokens_per_s"],
+                                      "efficiency": round(v["projected_tokens_per_s"] / (n * one_gpu), 3),
+                                      "min_stage_frac": v["min_frac_at_tick"]}
         for tag, k in (("fastest", fast), ("balanced", bal)):
             row[tag] = {"split": k, "tokens_per_s": cand[k]["projected_tokens_per_s"],
                         "efficiency": round(cand[k]["projected_tokens_per_s"] / (n * one_gpu), 3),
@@ -405,6 +565,13 @@ def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
     and BASELINE config 4's uneven splits (their stage imbalance and bubble)."""
     from inferd_amd.pipeline import StageRange, halves_split, ranges_from_sizes
     out = {}
+    for n in sizes:       # the greedy head vocab-parallel: config 3's even split and equal half-layer stages
+        if n > d.layers or n == 1:
+            continue
+        out[f"vhead_even{n}"] = {"ranges": [StageRange.layers(f, k) for f, k in stage_split(d, n, B, ctx, "even")],
+                                 "vhead": True}
+        if (2 * d.layers) % n == 0 and (2 * d.layers // n) % 2:
+            out[f"vhead_halves{n}"] = {"ranges": ranges_from_sizes([d.layers / n] * n), "vhead": True}
     if d.layers == 36:
         for n, sp in CONFIG4_SPLITS.items():
             out[f"config4_uneven{n}"] = ranges_from_sizes(sp)
@@ -417,7 +584,7 @@ def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
             out[f"balanced{n}"] = bal
         for name, sp in (("halves", halves_split(d.layers, n)), ("gateup", sub_split(d, n, False)),
                          ("sublayer", sub_split(d, n, True))):
-            if all(sp != v for v in out.values()):
+            if all(isinstance(v, dict) or sp != v for v in out.values()):
                 out[f"{name}{n}"] = sp
     return out
 
@@ -520,22 +687,52 @@ def cpu_config1(seed: int, steps: int = 16) -> dict:
 
 
 # ------------------------------------------------------------------ main
-def pipeline_run(d, ranges, rank: int, world: int, dev, dist, args, profile: bool = True) -> dict:
-    """One pipeline measurement on this rank: build the stage of `ranges`, prefill every
-    microbatch (untimed), W warm-up and K timed decode steps (one decode-graph step per stage
-    per microbatch step) between barriers, then the eager event-timed kernel profile.  Times are
-    the max over ranks."""
+def calibrate_shards(d, ranges, rank: int, world: int, dev, dist, args) -> dict:
+    """Per-rank calibration before the pipeline is built (vocab-parallel head): every rank times
+    its own stage's layers alone (stage_ms with its real role, the whole head excluded) on its own
+    GPU, the times are all-gathered and the lm_head shards are sized on them (head_shards) -- so the
+    split follows the GPUs it runs on, not one box's cost table (MI355X_MICROARCH.md: 1-3 % spread
+    between devices on memory-bound kernels)."""
+    rg = ranges[rank]
+    g = torch.Generator(device="cpu").manual_seed(args.seed + 29 + rank)
+    first, last = rank == 0, rank == world - 1
+    zero = (0, 16) if first else (16, 16)          # a one-tile shard: the stage's layers + final norm, ~no head
+    st = {}
+    ms = stage_ms(d, rg, first, last, args.batch, args.ctx, dev, g, args.seed, 3, 20, head=zero, stats=st)
+    t = torch.zeros(world, dtype=torch.float64, device=dev)
+    t[rank] = (ms - st.get("head_ms", 0.0)) * 1e3
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    us = [float(v) for v in t.cpu()]
+    pred, _ = stage_base_us(d, ranges, args.batch, args.ctx)
+    return {"stage_us": [round(v, 1) for v in us], "predicted_us": [round(v, 1) for v in pred],
+            "shards": head_shards(d, ranges, args.batch, args.ctx, stage_us=us)}
+
+
+def pipeline_run(d, ranges, rank: int, world: int, dev, dist, args, profile: bool = True, vhead: bool = False,
+                 shards=None) -> dict:
+    """One pipeline measurement on this rank: build the stage of `ranges` (vhead: the greedy head
+    vocab-parallel, this rank owning lm_head rows shards[rank]), prefill every microbatch (untimed),
+    W warm-up and K timed decode steps (one decode step per stage per microbatch step, the
+    asynchronous ring of pipeline.PipelineStage) between barriers, then the eager event-timed kernel
+    profile.  Times are the max over ranks."""
     from inferd_amd import pipeline as P
     B, ctx, K, W = args.batch, args.ctx, args.steps, args.warmup
     rg = ranges[rank]
+    vhead = vhead and world > 1
+    if vhead and shards is None:
+        shards = head_shards(d, ranges, B, ctx)
     if world > 1:
+        head = (f" + lm_head rows {shards[rank][0]}..{shards[rank][0] + shards[rank][1] - 1}" if shards[rank][1]
+                else "") + (" + final norm" if rank == world - 1 else "") if vhead else \
+            (" + norm/lm_head" if rank == world - 1 else "")
         print(f"bench.py: rank {rank} on {dev}: layers {rg.label()} of {d.layers}"
-              f"{' + embed' if rank == 0 else ''}{' + norm/lm_head' if rank == world - 1 else ''}",
-              file=sys.stderr, flush=True)
-    n_mb = world                                   # microbatches in flight
+              f"{' + embed' if rank == 0 else ''}{head}", file=sys.stderr, flush=True)
+    n_mb = P.ring_microbatches(world, vhead, args.ring_slack)     # microbatches in flight
     st = P.PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=args.seed,
                          n_microbatches=n_mb, batch=B, max_ctx=ctx + K + W + args.profile_steps + 64,
-                         prefill_chunk=args.prefill_chunk, **rg.span_kwargs())
+                         prefill_chunk=args.prefill_chunk, sharded_head=vhead,
+                         head_shard=shards[rank] if vhead else (0, 0), **rg.span_kwargs())
     # ---- prefill (untimed): every microbatch's sequences get `ctx` real tokens
     g = torch.Generator().manual_seed(args.seed + 17)
     prompts = [torch.randint(0, d.vocab, (B, ctx), generator=g) for _ in range(n_mb)]
@@ -576,7 +773,8 @@ def pipeline_run(d, ranges, rank: int, world: int, dev, dist, args, profile: boo
     if dist:
         dist.all_reduce(stage_ms, op=dist.ReduceOp.SUM)
     stage_ms = [float(v) for v in stage_ms.cpu()]
-    return {"st": st, "elapsed": elapsed, "t_prefill": t_prefill, "tick": tick, "prof": prof, "stage_ms": stage_ms}
+    return {"st": st, "elapsed": elapsed, "t_prefill": t_prefill, "tick": tick, "prof": prof, "stage_ms": stage_ms,
+            "n_mb": n_mb, "shards": shards}
 
 
 def main():
@@ -633,15 +831,22 @@ def main():
         ranges = sub_split(d, world, args.split == "sublayer")
     else:
         ranges = [P.StageRange.layers(f, k) for f, k in stage_split(d, world, B, ctx, args.split)]
-    run = pipeline_run(d, ranges, rank, world, dev, dist, args, profile=not args.no_profile)
+    vhead = world > 1 and args.head == "vocab"
+    cal = None
+    if vhead and not args.no_calibrate:
+        cal = calibrate_shards(d, ranges, rank, world, dev, dist, args)
+    run = pipeline_run(d, ranges, rank, world, dev, dist, args, profile=not args.no_profile, vhead=vhead,
+                       shards=cal["shards"] if cal else None)
     st, elapsed, t_prefill, tick, prof, stage_ms = (run[k] for k in ("st", "elapsed", "t_prefill", "tick", "prof",
                                                                      "stage_ms"))
-    n_mb = world
+    n_mb = run["n_mb"]
     tokens = K * n_mb * B
     value = tokens / elapsed
     ms_per_step = elapsed / K * 1e3
     ctx_mean = ctx + W + K + (args.profile_steps + 1) / 2.0   # context during the profiled steps
     kb = kernel_bytes(d, B, ctx_mean)
+    if run["shards"]:        # this rank's lm_head shard (vocab-parallel head) streams only its rows
+        kb["lm_head_argmax"] = run["shards"][rank][1] * d.hidden * 2 + B * d.hidden * 2
 
     # dominant kernel class of this rank (by total event time) -> roofline
     roof, kernels = None, None
@@ -683,7 +888,11 @@ def main():
                        # layers per stage (a shared attention unit counts a quarter layer on each side)
                        "spans": [r.n_units / 2 + (r.last_col - r.first_col) / d.intermediate / 2 -
                                  0.25 * (r.first_o + r.last_o + r.first_q + r.last_q) for r in ranges],
-                       "stage_ranges": [r.label() for r in ranges]},
+                       "stage_ranges": [r.label() for r in ranges],
+                       "head": ("vocab-parallel: lm_head rows per stage " + str([n for _, n in run["shards"]]))
+                       if run["shards"] else "whole lm_head on the last stage",
+                       "ring": f"asynchronous, {n_mb} microbatches" if world > 1 else None},
+            "calibration": cal,
             "roofline": roof,
             "roofline_step": {"bound": "hbm", "alg_bytes_per_step": int(sb),
                               "achieved": round(sb / (ms_per_step * 1e-3) / 1e9 / world, 1),
@@ -698,10 +907,11 @@ def main():
                 "handoff_ms_per_tick": round(ms_per_step / n_mb - max(stage_ms), 4),
                 "host_us_per_tick_rank0": tick["host_us_per_tick"],
                 "exchange_us_per_tick_rank0": tick["exchange_us_per_tick"],
-                "note": "compute from event-timed eager kernels (slightly above in-graph time); tick = "
-                        "ms_per_step / microbatches; handoff = tick - slowest stage; host_us = rank 0's host "
-                        "time per tick outside the stage exchange (graph launch, page-table advance, "
-                        "schedule), exchange_us = its batch_isend_irecv + wait"},
+                "note": "compute from event-timed eager kernels (slightly above in-graph time), with the "
+                        "rank's lm_head shard under a vocab-parallel head; tick = ms_per_step / microbatches; "
+                        "handoff = tick - slowest stage; host_us = rank 0's host time per ring iteration "
+                        "outside the hand-offs (launches, page-table advance, schedule), exchange_us = its "
+                        "receive / send posts and stream waits"},
             "prefill": {"tokens": n_mb * B * ctx, "seconds": round(t_prefill, 3),
                         "tokens_per_s": round(n_mb * B * ctx / t_prefill, 1)},
             "cpu_baseline": None,
@@ -724,8 +934,10 @@ def main():
         if world == 1 and not args.no_stage_projection:
             # the 2/4/8-GPU splits, every stage's decode graph timed alone on this GPU
             st.release()
-            out["stage_projection"] = stage_projection(d, projection_splits(d, B, ctx), B, ctx, dev, args.seed)
+            out["stage_projection"] = stage_projection(d, projection_splits(d, B, ctx), B, ctx, dev, args.seed,
+                                                       slack=args.ring_slack)
             out["projected_scaling"] = projected_scaling(out["stage_projection"], value)
+            out["stage_projection_summary"] = projection_summary(out["stage_projection"])
         if world == 1 and not args.no_cpu_baseline:
             st.release()
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)
@@ -739,13 +951,21 @@ def main():
         r2["st"].release()
         if rank == 0:
             out["sublayer_split"] = {
-                "value": round(K * world * B / r2["elapsed"], 2), "unit": "tokens/s",
+                "value": round(K * r2["n_mb"] * B / r2["elapsed"], 2), "unit": "tokens/s",
                 "ms_per_step": round(r2["elapsed"] / K * 1e3, 4), "stage_ranges": [r.label() for r in alt],
-                "tick_ms": round(r2["elapsed"] / K * 1e3 / world, 4),
+                "microbatches": r2["n_mb"], "tick_ms": round(r2["elapsed"] / K * 1e3 / r2["n_mb"], 4),
                 "exchange_us_per_tick_rank0": r2["tick"]["exchange_us_per_tick"],
-                "note": "the same workload on pipeline.sublayer_split's stages (measured cost table); "
-                        "`value` above is BASELINE config 3's even split"}
+                "note": "the same workload on pipeline.sublayer_split's stages (measured cost table) with the "
+                        "whole lm_head on the last stage; `value` above is BASELINE config 3's even split"}
     if rank == 0:
+        # the driver keeps the tail of stdout: the compact results go last
+        for k in ("stage_projection_summary", "projected_scaling", "sublayer_split", "prefill_config5",
+                  "prefill_config5_b4"):
+            if k in out:
+                v = out.pop(k)
+                if k.startswith("prefill_config5") and v is not None:
+                    out.setdefault("prefill_kernels", {})[k] = v.pop("kernels", None)
+                out[k] = v
         print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

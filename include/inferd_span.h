@@ -71,16 +71,18 @@ typedef struct InferdSpanConfig {
    * the same bf16 [n_tokens][hidden] tensor a layer boundary hands over. */
   int32_t skip_first_attn; /* the span begins at its first layer's MLP half (input: h1; no embed) */
   int32_t skip_last_mlp;   /* the span ends after its last layer's attention half (output: h1; no lm_head) */
-  /* A finer boundary inside the gate/up projection, decode calls (<= 64 rows) only: the span
-   * before the boundary also computes gate/up columns [0, c) of that layer's SwiGLU product
-   * `act`, the span after it the columns [c, intermediate) and the down projection.  In a
-   * decode call the hand-off is then a RECORD: h1 bf16 [n_tokens][hidden] row-major, followed
-   * by act bf16 [ceil(n_tokens/16)*16][intermediate] fragment-packed (columns [0, c) filled;
-   * the receiving span completes the other columns in place).  Prefill calls hand over h1 only
-   * and the receiving span computes the whole MLP.  Values and rounding points are those of
-   * one span: act columns are independent, down runs whole on one side.  c: 0 = none, else a
-   * multiple of 128 below intermediate. */
-  int32_t gateup_split_first; /* with skip_first_attn: columns [0, c) arrive in x_in's record */
+  /* A finer boundary inside the gate/up projection, for calls of <= 64 rows (any kind, decode or
+   * a short prefill): the span before the boundary also computes gate/up columns [0, c) of that
+   * layer's SwiGLU product `act`, the span after it the columns [c, intermediate) and the down
+   * projection.  Every call of <= 64 rows then hands over a RECORD: h1 bf16 [n_tokens][hidden]
+   * row-major, followed by act bf16 [ceil(n_tokens/16)*16][intermediate] fragment-packed (columns
+   * [0, c) filled).  The receiving span completes the other columns IN PLACE in x_in's record (x_in
+   * is written although the API passes it as const void*), so both sides must size x_in / x_out
+   * for the whole record (the C-ABI does not check buffer sizes; the torch extension does).
+   * Calls of more than 64 rows hand over h1 only and the receiving span computes the whole MLP.
+   * Values and rounding points are those of one span: act columns are independent, down runs
+   * whole on one side.  c: 0 = none, else a multiple of 128 below intermediate. */
+  int32_t gateup_split_first; /* with skip_first_attn: columns [0, c) arrive in x_in's record (written in place) */
   int32_t gateup_split_last;  /* with skip_last_mlp: columns [0, c) are computed into x_out's record */
   /* A boundary between a layer's attention kernel and its o projection: the span before it
    * runs input_layernorm, q/k/v and the attention of that layer (its K/V pages live there),
@@ -100,6 +102,23 @@ typedef struct InferdSpanConfig {
    * the layer's input_layernorm and q/k/v weights too).  0 or 1. */
   int32_t qkv_split_first; /* the span starts at its first layer's attention (x_in: the record) */
   int32_t qkv_split_last;  /* the span ends after its last layer's q/k/v projection (x_out: the record) */
+  /* Vocab-parallel lm_head (ABI 5).  The reference's last span owns the whole lm_head
+   * (split_model.py:97-102) and takes argmax(logits[:, -1]) (partitioned_models.py:95-96,162).
+   * In a pipeline that 1.24 GB GEMV sits on one stage; these fields spread it over the stages:
+   * the model's last span keeps only the final norm (final_norm_out) and hands out the normed
+   * last rows, every span may own a contiguous shard of lm_head rows, inferd_span_head_shard
+   * reduces a shard to one (max logit, first index) key per row, and inferd_argmax_combine
+   * takes the max over the shards' keys -- torch.argmax's value and lowest-index tie-break, bit
+   * for bit (a logit's value does not depend on which shard computes it: one 16-column GEMV tile
+   * per workgroup over the whole K range, tiles aligned to 16 rows). */
+  int32_t head_first;     /* first lm_head row of this span's shard (a multiple of 16) */
+  int32_t head_rows;      /* rows of the shard (a multiple of 16; 0 = none).  Not with has_lm_head,
+                             which owns all rows (and may also be reduced by inferd_span_head_shard) */
+  int32_t final_norm_out; /* the model's last span, head vocab-parallel: owns the final norm (weight
+                             "norm"; no lm_head); a forward with x_out writes the final-normed last
+                             row of each sequence there, fragment-packed over ceil(n_seqs/16)*16 rows
+                             ([n_seqs <= 64][hidden]: the A operand of inferd_span_head_shard), instead
+                             of the last layer's hidden rows.  Ends at a layer boundary. */
 } InferdSpanConfig;
 
 /* One forward call's batch: n_seqs sequences, their new tokens concatenated
@@ -172,6 +191,26 @@ int inferd_span_forward(InferdSpan* span, const InferdBatch* batch, const int32_
  * inferd_span_forward computes the last row of each sequence only).  Last span only,
  * rows <= max_tokens. */
 int inferd_span_lm_head(InferdSpan* span, const void* x, int32_t rows, void* logits, void* stream);
+
+/* Vocab-parallel greedy head (ABI 5; InferdSpanConfig head_first / head_rows): the span's lm_head
+ * shard over `rows` (<= 64) final-normed rows `normed` (bf16, fragment-packed over
+ * ceil(rows/16)*16 rows: what a final_norm_out span's forward writes to x_out).  A row's KEY is
+ * (order(bf16 logit) << 32 | (0xFFFFFFFF - c)) maximised over columns c, c the GLOBAL vocabulary
+ * index: the max key is the max logit, ties to the lowest index (torch.argmax).  All outputs are
+ * optional and device-side:
+ *   keys_in   uint64 [rows]: the running max key of the shards before this one (NULL: none)
+ *   keys_out  uint64 [rows]: max(keys_in, this shard's key) (may alias keys_in)
+ *   ids       int32 [rows]: the greedy token of that max key
+ *   logits    bf16 [rows][head_rows] row-major: the shard's columns
+ * Chaining the call over the shards in any order (keys_out -> the next keys_in) and taking ids at
+ * the end gives argmax(norm(x) @ lm_head^T) of the whole vocabulary.  A span with has_lm_head
+ * reduces all rows.  Replaces, split over the stages, LastStage's lm_head + argmax
+ * (partitioned_models.py:95-96,162). */
+int inferd_span_head_shard(InferdSpan* span, const void* normed, int32_t rows, const uint64_t* keys_in,
+                           uint64_t* keys_out, int32_t* ids, void* logits, void* stream);
+/* ids[r] = the index in the max key over n_parts shards' keys [n_parts][rows] (device uint64):
+ * the greedy token, ties to the lowest index as torch.argmax.  Device int32 ids [rows]. */
+int inferd_argmax_combine(const uint64_t* keys, int32_t n_parts, int32_t rows, int32_t* ids, void* stream);
 
 /* Decode graphs.  Captures one span forward of `batch` (same arguments as
  * inferd_span_forward; `logits`, last span only, optional: bf16 [n_seqs][vocab] last-row

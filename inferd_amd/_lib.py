@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # INFERD_LIB: another build of the same library (A/B timing runs of tools/ builds only)
 LIB_PATH = os.environ.get("INFERD_LIB") or os.path.join(_HERE, "libinferd_span.so")
 
-ABI_VERSION = 4   # inferd_abi_version() of the header this table binds
+ABI_VERSION = 5   # inferd_abi_version() of the header this table binds
 INFERD_OK = 0
 INFERD_ERR_ARG, INFERD_ERR_NOMEM = 1, 4
 EPI_NONE, EPI_RESID, EPI_SILU = 0, 1, 2
@@ -31,7 +31,8 @@ class SpanConfig(C.Structure):
                [("rms_eps", c_f), ("rope_theta", c_f)] + \
                [(n, c_i32) for n in ("max_positions", "kv_pages", "max_tokens", "max_seqs", "skip_first_attn",
                                      "skip_last_mlp", "gateup_split_first", "gateup_split_last", "o_split_first",
-                                     "o_split_last", "qkv_split_first", "qkv_split_last")]
+                                     "o_split_last", "qkv_split_first", "qkv_split_last", "head_first", "head_rows",
+                                     "final_norm_out")]
 
 
 class Batch(C.Structure):
@@ -51,6 +52,8 @@ SIGNATURES = {
     "inferd_span_profile_start": (C.c_int, [c_p, c_i32]),
     "inferd_span_profile_stop": (C.c_int, [c_p, C.POINTER(C.c_double), C.POINTER(c_i32), c_i32]),
     "inferd_span_lm_head": (C.c_int, [c_p, c_p, c_i32, c_p, c_p]),
+    "inferd_span_head_shard": (C.c_int, [c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "inferd_argmax_combine": (C.c_int, [c_p, c_i32, c_i32, c_p, c_p]),
     "inferd_span_graph_capture": (C.c_int, [c_p, C.POINTER(Batch), c_i32, c_p, c_p, c_p, c_p, c_p, c_p,
                                             C.POINTER(c_p)]),
     "inferd_graph_launch": (C.c_int, [c_p, c_p]),

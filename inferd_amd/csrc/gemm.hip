@@ -1688,6 +1688,68 @@ void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
   hipLaunchKernelGGL(argmax_reduce_kernel, dim3(M), dim3(1024), 0, s, partial, n_tiles, ids);
 }
 
+// The same reduction for a vocab-parallel lm_head shard (inferd_span_head_shard): the row's max
+// key with the shard's first vocabulary row col0 folded into the index part (~(col0 + c) =
+// ~c - col0: no borrow, col0 + c < 2^32), so keys of different shards compare as one row's keys;
+// folded with the running key of the shards before (keys_in), stored (keys_out, may alias
+// keys_in: one thread reads then writes its row) and/or decoded to the greedy id.
+__global__ __launch_bounds__(1024) void argmax_keys_kernel(const unsigned long long* __restrict__ partial, int n_tiles,
+                                                           unsigned int col0, const unsigned long long* keys_in,
+                                                           unsigned long long* keys_out, int32_t* __restrict__ ids) {
+  __shared__ unsigned long long red[16];
+  const int row = blockIdx.x;
+  const unsigned long long* p = partial + (int64_t)row * n_tiles;
+  unsigned long long best = 0;
+  for (int t = threadIdx.x; t < n_tiles; t += 4 * 1024) {
+    unsigned long long k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = (t + u * 1024 < n_tiles) ? p[t + u * 1024] : 0ull;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) best = k[u] > best ? k[u] : best;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long other = __shfl_xor(best, o);
+    best = other > best ? other : best;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long b = red[0];
+    for (int w = 1; w < 16; ++w) b = red[w] > b ? red[w] : b;
+    b -= (unsigned long long)col0;
+    if (keys_in) {
+      const unsigned long long r = keys_in[row];
+      b = r > b ? r : b;
+    }
+    if (keys_out) keys_out[row] = b;
+    if (ids) ids[row] = (int32_t)(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull));
+  }
+}
+
+void launch_argmax_keys(const unsigned long long* partial, int n_tiles, int M, int col0,
+                        const unsigned long long* keys_in, unsigned long long* keys_out, int32_t* ids, hipStream_t s) {
+  hipLaunchKernelGGL(argmax_keys_kernel, dim3(M), dim3(1024), 0, s, partial, n_tiles, (unsigned int)col0, keys_in,
+                     keys_out, ids);
+}
+
+// ids[r] from the max over n_parts shards' keys [n_parts][rows] (inferd_argmax_combine)
+__global__ void argmax_combine_kernel(const unsigned long long* __restrict__ keys, int n_parts, int rows,
+                                      int32_t* __restrict__ ids) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  unsigned long long b = 0;
+  for (int p = 0; p < n_parts; ++p) {
+    const unsigned long long k = keys[(int64_t)p * rows + r];
+    b = k > b ? k : b;
+  }
+  ids[r] = (int32_t)(0xFFFFFFFFu - (uint32_t)(b & 0xFFFFFFFFull));
+}
+
+void launch_argmax_combine(const unsigned long long* keys, int n_parts, int rows, int32_t* ids, hipStream_t s) {
+  hipLaunchKernelGGL(argmax_combine_kernel, dim3((rows + 63) / 64), dim3(64), 0, s, keys, n_parts, rows, ids);
+}
+
 // ============================================================ fused prefill q/k/v projection
 // launch_gemm's persistent whole-tile path with the EPI_QKV epilogue: q/k RMSNorm + RoPE to
 // q_out and the K cache, V to the cache (what launch_qk_norm_rope_kv does from a stored q/k/v

@@ -134,6 +134,11 @@ void launch_gemm_decode_partial(const u16* A, int64_t lda, const u16* Wp, int M,
                                 float* part, const DecodeNorm& norm, hipStream_t s, int pack = 0);
 void launch_argmax_reduce(const unsigned long long* partial, int n_tiles, int M,
                           int32_t* ids, hipStream_t s);
+// vocab-parallel lm_head: a shard's per-row max key with its first vocabulary row folded into the
+// index part, and the combine over shards (inferd_span_head_shard / inferd_argmax_combine)
+void launch_argmax_keys(const unsigned long long* partial, int n_tiles, int M, int col0,
+                        const unsigned long long* keys_in, unsigned long long* keys_out, int32_t* ids, hipStream_t s);
+void launch_argmax_combine(const unsigned long long* keys, int n_parts, int rows, int32_t* ids, hipStream_t s);
 
 // attention.hip
 struct AttnBatch {

@@ -49,7 +49,7 @@ int inferd_fail(int code, const std::string& msg) { return fail(code, msg); }
   } while (0)
 
 extern "C" const char* inferd_last_error(void) { return g_err.c_str(); }
-extern "C" int inferd_abi_version(void) { return 4; }
+extern "C" int inferd_abi_version(void) { return 5; }
 
 namespace {
 
@@ -165,6 +165,10 @@ struct InferdSpan {
   // the last layer of a span that ends inside the layer's gate/up projection computes part of it
   bool has_gateup(int l) const { return has_mlp(l) || (l == cfg.n_layers - 1 && cfg.gateup_split_last); }
   int kv_layers() const { return cfg.n_layers - (first_no_attn() ? 1 : 0) - (cfg.qkv_split_last ? 1 : 0); }
+  // the lm_head rows this span owns (InferdSpanConfig head_first / head_rows): all of them with
+  // has_lm_head, else its vocab-parallel shard (0 rows: none)
+  int lm_rows() const { return cfg.has_lm_head ? cfg.vocab : cfg.head_rows; }
+  int lm_first() const { return cfg.has_lm_head ? 0 : cfg.head_first; }
   u16* kv_of(int l) const { return kv_pool + kv_layer_elems * (l - (first_no_attn() ? 1 : 0)); }
 };
 
@@ -215,6 +219,15 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
                                 "embedding (first) and lm_head (last)");
   if ((c.qkv_split_first || c.qkv_split_last) && c.n_layers < 1)
     return fail(INFERD_ERR_ARG, "a q/k/v|attention boundary needs n_layers >= 1");
+  if (c.head_rows < 0 || c.head_first < 0 || c.head_rows % 16 || c.head_first % 16 ||
+      (int64_t)c.head_first + c.head_rows > c.vocab)
+    return fail(INFERD_ERR_ARG, "lm_head shard: rows [head_first, head_first + head_rows) within the vocabulary, "
+                                "multiples of 16");
+  if (c.final_norm_out & ~1) return fail(INFERD_ERR_ARG, "final_norm_out is 0 or 1");
+  if (c.has_lm_head && (c.head_rows || c.final_norm_out))
+    return fail(INFERD_ERR_ARG, "a span with the whole lm_head has no shard and no final_norm_out");
+  if (c.final_norm_out && (c.skip_last_mlp || c.o_split_last || c.qkv_split_last || c.max_seqs > 64))
+    return fail(INFERD_ERR_ARG, "a final_norm_out span ends at a layer boundary and takes max_seqs <= 64");
   if (c.n_layers == 1 && ((c.o_split_first && (c.o_split_last || c.skip_last_mlp)) ||
                           (c.o_split_last && c.skip_first_attn) ||
                           (c.qkv_split_last && (c.skip_first_attn || c.o_split_first || c.qkv_split_first)) ||
@@ -250,10 +263,8 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
     if (s->has_mlp(l)) SALLOC(L.down, (size_t)h * I * 2);
   }
   if (c.has_embed) SALLOC(s->embed, (size_t)c.vocab * h * 2);
-  if (c.has_lm_head) {
-    SALLOC(s->final_norm, (size_t)h * 2);
-    SALLOC(s->lm_head, (size_t)c.vocab * h * 2);
-  }
+  if (c.has_lm_head || c.final_norm_out) SALLOC(s->final_norm, (size_t)h * 2);
+  if (s->lm_rows() > 0) SALLOC(s->lm_head, (size_t)s->lm_rows() * h * 2);
   // rope tables
   SALLOC(s->cos_t, (size_t)c.max_positions * 64 * 2);
   SALLOC(s->sin_t, (size_t)c.max_positions * 64 * 2);
@@ -291,7 +302,7 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
   SALLOC(s->attn_ws, s->attn_ws_bytes);
   if (hipMemset(s->attn_ws, 0, s->attn_ws_bytes) != hipSuccess) return bail(fail(INFERD_ERR_HIP, "memset failed"));
   SALLOC(s->ssq, (size_t)(2 * c.n_layers) * SSQ_SLOT_WORDS * 8);
-  if (c.has_lm_head) SALLOC(s->argmax_partial, (size_t)(c.vocab / 16) * 64 * 8);
+  if (s->lm_rows() > 0) SALLOC(s->argmax_partial, (size_t)(s->lm_rows() / 16) * 64 * 8);
   SALLOC(s->qkv_part, (size_t)QKV_KSL * 16 * s->qkv_rows() * 4);
   // the prefill tail split's workspace, once (a forward never allocates): only spans whose
   // calls can reach the 256x256 GEMMs (>= 512 rows) need it
@@ -320,6 +331,7 @@ struct Target {
   int packed;     // 1: fragment-pack at n-tile offset
   int64_t rows, cols;
   uint32_t tid_idx;
+  int64_t elem0 = 0;  // generator counter of the first element (an lm_head shard: head_first * hidden)
 };
 
 int resolve_layer(InferdSpan* s, int layer, const char* name, Target* t);
@@ -331,7 +343,10 @@ int resolve(InferdSpan* s, int layer, const char* name, Target* t) {
   if (layer < 0) {
     if (!strcmp(name, "embed_tokens") && s->embed) { *t = {s->embed, 0, c.vocab, h, T_EMBED}; return 0; }
     if (!strcmp(name, "norm") && s->final_norm) { *t = {s->final_norm, 0, 1, h, T_NORM}; return 0; }
-    if (!strcmp(name, "lm_head") && s->lm_head) { *t = {s->lm_head, 1, c.vocab, h, T_LM}; return 0; }
+    if (!strcmp(name, "lm_head") && s->lm_head) {
+      *t = {s->lm_head, 1, s->lm_rows(), h, T_LM, (int64_t)s->lm_first() * h};
+      return 0;
+    }
     return fail(INFERD_ERR_ARG, std::string("unknown/unowned global weight ") + name);
   }
   if (layer >= c.n_layers) return fail(INFERD_ERR_ARG, "layer index out of span");
@@ -398,7 +413,7 @@ extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* st
   const InferdSpanConfig& c = s->cfg;
   // temp buffer for the largest row-major tensor that needs packing
   int64_t biggest = (int64_t)c.hidden * (c.intermediate > c.heads * HEAD_DIM ? c.intermediate : c.heads * HEAD_DIM);
-  if (c.has_lm_head && (int64_t)c.vocab * c.hidden > biggest) biggest = (int64_t)c.vocab * c.hidden;
+  if ((int64_t)s->lm_rows() * c.hidden > biggest) biggest = (int64_t)s->lm_rows() * c.hidden;
   u16* tmp = nullptr;
   HIP_TRY(hipMalloc((void**)&tmp, biggest * 2));
   static const char* layer_names[] = {"input_layernorm", "post_attention_layernorm", "q_norm", "k_norm",
@@ -411,7 +426,7 @@ extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* st
     const float scale = is_norm ? NORM_SCALE : LINEAR_SCALE;
     const float center = is_norm ? 1.0f : 0.0f;
     const uint32_t tid = layer < 0 ? t.tid_idx : (uint32_t)((c.first_layer + layer) * 16 + t.tid_idx);
-    const uint64_t key = tensor_key(seed, tid);
+    const uint64_t key = tensor_key(seed, tid) + (uint64_t)t.elem0;
     const int64_t n = t.rows * t.cols;
     if (t.packed) {
       launch_weightgen(tmp, n, key, scale, center, st);
@@ -426,8 +441,8 @@ extern "C" int inferd_span_init_synthetic(InferdSpan* s, uint64_t seed, void* st
     for (const char* nm : layer_names)
       if (owns_weight(s, l, nm) && (rc = gen(l, nm))) break;
   if (!rc && c.has_embed) rc = gen(-1, "embed_tokens");
-  if (!rc && c.has_lm_head) rc = gen(-1, "norm");
-  if (!rc && c.has_lm_head) rc = gen(-1, "lm_head");
+  if (!rc && s->final_norm) rc = gen(-1, "norm");
+  if (!rc && s->lm_head) rc = gen(-1, "lm_head");
   hipError_t e = hipStreamSynchronize(st);
   (void)hipFree(tmp);
   if (rc) return rc;
@@ -486,6 +501,11 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     pro = s->adv;
     s->adv_pending = false;
   }
+  // a final_norm_out span: x_out receives the final-normed last rows (below); the last layer's
+  // hidden rows stay in the workspace, as on a span with lm_head
+  void* const normed_out = c.final_norm_out ? x_out : nullptr;
+  if (c.final_norm_out) x_out = nullptr;
+  if (normed_out && B > 64) return fail(INFERD_ERR_ARG, "final_norm_out supports <= 64 sequences per call");
   if (M <= 64 && c.gateup_split_first && !x_in)
     return fail(INFERD_ERR_ARG, "a span starting inside a gate/up projection needs x_in (the hand-off record)");
   if ((c.o_split_last || c.qkv_split_last) && !x_out)
@@ -764,6 +784,42 @@ extern "C" int inferd_span_forward(InferdSpan* s, const InferdBatch* b, const in
     if (next_ids) launch_argmax_reduce(s->argmax_partial, c.vocab / 16, B, next_ids, st);
     s->prof_end(pe, st);
   }
+  if (normed_out) {
+    // vocab-parallel head: the last row of each sequence, final-normed and fragment-packed (the
+    // A operand of every stage's inferd_span_head_shard), handed over instead of running lm_head
+    pe = s->prof_begin(PROF_NORM, st);
+    launch_rmsnorm(x, h, b->seq_start + 1, 1, s->final_norm, (u16*)normed_out, h, B, h, c.rms_eps, st, true);
+    s->prof_end(pe, st);
+  }
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+// Vocab-parallel lm_head shard: the greedy key of each row over this span's lm_head rows
+// (InferdSpanConfig head_first / head_rows), column indices global.  The same GEMV and 16-column
+// tiles as the whole head (inferd_span_forward's EPI_ARGMAX launch), so each logit is the one a
+// single lm_head computes.
+extern "C" int inferd_span_head_shard(InferdSpan* s, const void* normed, int32_t rows, const uint64_t* keys_in,
+                                      uint64_t* keys_out, int32_t* ids, void* logits, void* stream) {
+  if (!s || !normed || rows <= 0 || rows > 64) return fail(INFERD_ERR_ARG, "bad head_shard args (rows 1..64)");
+  const InferdSpanConfig& c = s->cfg;
+  const int n = s->lm_rows();
+  if (n <= 0) return fail(INFERD_ERR_ARG, "span owns no lm_head rows");
+  hipStream_t st = (hipStream_t)stream;
+  const long pe = s->prof_begin(PROF_LMHEAD, st);
+  GEMM_TRY(launch_gemm((const u16*)normed, c.hidden, s->lm_head, rows, n, c.hidden, (u16*)logits, n, nullptr, 0,
+                       EPI_ARGMAX, s->argmax_partial, st, nullptr, nullptr, nullptr, GEMM_PACK_A));
+  if (keys_out || ids)
+    launch_argmax_keys(s->argmax_partial, n / 16, rows, s->lm_first(), (const unsigned long long*)keys_in,
+                       (unsigned long long*)keys_out, ids, st);
+  s->prof_end(pe, st);
+  LAUNCH_CHECK();
+  return INFERD_OK;
+}
+
+extern "C" int inferd_argmax_combine(const uint64_t* keys, int32_t n_parts, int32_t rows, int32_t* ids, void* stream) {
+  if (!keys || !ids || n_parts <= 0 || rows <= 0) return fail(INFERD_ERR_ARG, "bad argmax_combine args");
+  launch_argmax_combine((const unsigned long long*)keys, n_parts, rows, ids, (hipStream_t)stream);
   LAUNCH_CHECK();
   return INFERD_OK;
 }
@@ -834,13 +890,6 @@ extern "C" int inferd_span_graph_capture(InferdSpan* s, const InferdBatch* b, in
   s->prof_on = false;  // event pairs are timed eagerly only (HIP cannot time captured events)
   HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
   const int rc = step_body(s, b, advance, ids, x_in, x_out, next_ids, logits, st);
-    s->adv = NormPrologue{};
-    s->adv.positions = (int32_t*)b->positions;
-    s->adv.slots = (int32_t*)b->slots;
-    s->adv.ctx_lens = (int32_t*)b->ctx_lens;
-    s->adv.block_table = b->block_table;
-    s->adv.max_pages = b->max_pages;
-    s->adv.B = b->n_seqs;
   hipGraph_t g = nullptr;
   hipError_t e = hipStreamEndCapture(st, &g);
   if (rc) {

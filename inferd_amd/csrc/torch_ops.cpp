@@ -89,9 +89,11 @@ void check_forward_args(const InferdSpanConfig& c, const at::Tensor& words, cons
             M * h + (dec && c.gateup_split_first ? rec : 0) + (c.o_split_first ? orec : 0) +
                 (c.qkv_split_first ? qrec : 0),
             "x");
+  // a final_norm_out span's x_out: the final-normed last rows, fragment-packed over 16-row tiles
   check_arg(x_out, dev, at::kBFloat16,
-            M * h + (dec && c.gateup_split_last ? rec : 0) + (c.o_split_last ? orec : 0) +
-                (c.qkv_split_last ? qrec : 0),
+            c.final_norm_out ? (B + 15) / 16 * 16 * h
+                             : M * h + (dec && c.gateup_split_last ? rec : 0) + (c.o_split_last ? orec : 0) +
+                                   (c.qkv_split_last ? qrec : 0),
             "x_out");
   check_arg(next_ids, dev, at::kInt, B, "next_ids");
   check_arg(logits, dev, at::kBFloat16, B * (int64_t)c.vocab, "logits");
@@ -102,10 +104,10 @@ void check_forward_args(const InferdSpanConfig& c, const at::Tensor& words, cons
 // cfg: [hidden, intermediate, heads, kv_heads, head_dim, vocab, first_layer, n_layers, has_embed,
 //       has_lm_head, max_positions, kv_pages, max_tokens, max_seqs, skip_first_attn, skip_last_mlp,
 //       gateup_split_first, gateup_split_last, o_split_first, o_split_last, qkv_split_first,
-//       qkv_split_last]
-// (the sub-layer boundary fields may be omitted: 14 ints = whole layers)
+//       qkv_split_last, head_first, head_rows, final_norm_out]
+// (the trailing fields may be omitted: 14 ints = whole layers, whole head)
 int64_t span_create(at::IntArrayRef cfg, double rms_eps, double rope_theta, at::Device device) {
-  TORCH_CHECK(cfg.size() >= 14 && cfg.size() <= 22 && cfg.size() % 2 == 0, "span_create: 14 .. 22 config ints");
+  TORCH_CHECK(cfg.size() >= 14 && cfg.size() <= 25, "span_create: 14 .. 25 config ints");
   auto opt = [&](size_t i) { return cfg.size() > i ? (int32_t)cfg[i] : 0; };
   TORCH_CHECK(device.is_cuda(), "span_create: a GPU device");
   c10::hip::HIPGuard g(device.index());
@@ -113,7 +115,7 @@ int64_t span_create(at::IntArrayRef cfg, double rms_eps, double rope_theta, at::
                      (int32_t)cfg[5], (int32_t)cfg[6], (int32_t)cfg[7], (int32_t)cfg[8], (int32_t)cfg[9],
                      (float)rms_eps, (float)rope_theta, (int32_t)cfg[10], (int32_t)cfg[11], (int32_t)cfg[12],
                      (int32_t)cfg[13], opt(14), opt(15), opt(16), opt(17), opt(18), opt(19), opt(20),
-                     opt(21)};
+                     opt(21), opt(22), opt(23), opt(24)};
   InferdSpan* s = nullptr;
   ok(inferd_span_create(&c, &s), "span_create");
   return reinterpret_cast<int64_t>(s);
@@ -126,7 +128,7 @@ std::vector<int64_t> span_config(int64_t span) {
   return {c.hidden, c.intermediate, c.heads, c.kv_heads, c.head_dim, c.vocab, c.first_layer, c.n_layers,
           c.has_embed, c.has_lm_head, c.max_positions, c.kv_pages, c.max_tokens, c.max_seqs,
           c.skip_first_attn, c.skip_last_mlp, c.gateup_split_first, c.gateup_split_last, c.o_split_first,
-          c.o_split_last, c.qkv_split_first, c.qkv_split_last};
+          c.o_split_last, c.qkv_split_first, c.qkv_split_last, c.head_first, c.head_rows, c.final_norm_out};
 }
 
 void span_init_synthetic(int64_t span, int64_t seed, at::Device device) {
@@ -194,6 +196,64 @@ void span_lm_head(int64_t span, const at::Tensor& x, const at::Tensor& logits) {
   check_arg(logits, x.device(), at::kBFloat16, x.size(0) * (int64_t)c.vocab, "logits");
   c10::hip::HIPGuard g(x.device().index());
   ok(inferd_span_lm_head(s, x.data_ptr(), (int32_t)x.size(0), logits.data_ptr(), stream_of(x.device())), "span_lm_head");
+}
+
+// vocab-parallel lm_head: the span's shard over `rows` final-normed rows (fragment-packed, 16-row
+// tiles); keys are int64 tensors holding the uint64 key bits: keys_in (the running max of the
+// shards before, optional) -> keys_out = max(keys_in, this shard's) (optional, may alias), ids int32
+// [rows] (optional), shard logits bf16 [rows, head rows] (optional)
+void span_head_shard(int64_t span, const at::Tensor& normed, int64_t rows, const std::optional<at::Tensor>& keys_in,
+                     const std::optional<at::Tensor>& keys_out, const std::optional<at::Tensor>& ids,
+                     const std::optional<at::Tensor>& logits) {
+  InferdSpan* s = handle<InferdSpan>(span, "span_head_shard");
+  const InferdSpanConfig c = config_of(s);
+  const int64_t n = c.has_lm_head ? c.vocab : c.head_rows;
+  TORCH_CHECK(n > 0, "span_head_shard: the span owns no lm_head rows");
+  TORCH_CHECK(rows >= 1 && rows <= 64, "span_head_shard: 1 .. 64 rows");
+  TORCH_CHECK(normed.is_cuda(), "span_head_shard: normed must be on a GPU");
+  const at::Device dev = normed.device();
+  check_arg(normed, dev, at::kBFloat16, (rows + 15) / 16 * 16 * (int64_t)c.hidden, "normed");
+  check_arg(keys_in, dev, at::kLong, rows, "keys_in");
+  check_arg(keys_out, dev, at::kLong, rows, "keys_out");
+  check_arg(ids, dev, at::kInt, rows, "ids");
+  check_arg(logits, dev, at::kBFloat16, rows * n, "logits");
+  c10::hip::HIPGuard g(dev.index());
+  ok(inferd_span_head_shard(s, normed.data_ptr(), (int32_t)rows, (const uint64_t*)opt_ptr(keys_in),
+                            (uint64_t*)opt_ptr(keys_out), (int32_t*)opt_ptr(ids), (void*)opt_ptr(logits),
+                            stream_of(dev)),
+     "span_head_shard");
+}
+
+// greedy ids from n_parts shards' keys int64 [n_parts, rows] -> ids int32 [rows]
+void argmax_combine(const at::Tensor& keys, int64_t n_parts, int64_t rows, const at::Tensor& ids) {
+  TORCH_CHECK(keys.is_cuda() && n_parts >= 1 && rows >= 1, "argmax_combine: GPU keys, n_parts >= 1, rows >= 1");
+  const at::Device dev = keys.device();
+  check_arg(keys, dev, at::kLong, n_parts * rows, "keys");
+  check_arg(ids, dev, at::kInt, rows, "ids");
+  c10::hip::HIPGuard g(dev.index());
+  ok(inferd_argmax_combine((const uint64_t*)keys.data_ptr(), (int32_t)n_parts, (int32_t)rows, ids.data_ptr<int32_t>(),
+                           stream_of(dev)),
+     "argmax_combine");
+}
+
+// A compute stream with a hardware queue of its own: a CU-masked stream over every CU.  HIP maps its
+// ordinary streams round-robin onto GPU_MAX_HW_QUEUES (4) hardware queues, and kernels of streams
+// that share a queue run in submission order -- an RCCL receive posted ahead of its data (resident,
+// waiting) would hold back every compute kernel queued behind it.  CU-masked streams get dedicated
+// queues outside that pool (tools/rccl_ring_probe.py: no waiter on any pool stream blocks one).
+// Returned as a hipStream_t in an int64 (torch.cuda.ExternalStream); it lives for the process.
+int64_t dedicated_stream(at::Device device) {
+  TORCH_CHECK(device.is_cuda(), "dedicated_stream: a GPU device");
+  c10::hip::HIPGuard g(device.index());
+  hipDeviceProp_t p;
+  TORCH_CHECK(hipGetDeviceProperties(&p, device.index()) == hipSuccess, "dedicated_stream: device properties");
+  const int n = p.multiProcessorCount;
+  std::vector<uint32_t> mask((n + 31) / 32, 0xFFFFFFFFu);
+  if (n % 32) mask.back() = (1u << (n % 32)) - 1;
+  hipStream_t s = nullptr;
+  TORCH_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess,
+              "dedicated_stream: hipExtStreamCreateWithCUMask failed");
+  return reinterpret_cast<int64_t>(s);
 }
 
 // one synthetic weight tensor (the counter-based generator; oracle/weightgen.py defines the same values)
@@ -379,6 +439,11 @@ TORCH_LIBRARY(inferd, m) {
         "Tensor(b!)? next_ids, Tensor(c!)? logits, Tensor(d!)? layers=None) -> ()",
         &span_forward);
   m.def("span_lm_head(int span, Tensor x, Tensor(a!) logits) -> ()", &span_lm_head);
+  m.def("span_head_shard(int span, Tensor normed, int rows, Tensor? keys_in, Tensor(a!)? keys_out, "
+        "Tensor(b!)? ids, Tensor(c!)? logits=None) -> ()",
+        &span_head_shard);
+  m.def("argmax_combine(Tensor keys, int n_parts, int rows, Tensor(a!) ids) -> ()", &argmax_combine);
+  m.def("dedicated_stream(Device device) -> int", &dedicated_stream);
   m.def("weightgen(Tensor(a!) dst, int seed, int tensor_id, float scale, float center) -> ()", &weightgen);
   m.def("kv_create(int n_pages) -> int", &kv_create);
   m.def("kv_destroy(int table) -> ()", &kv_destroy);

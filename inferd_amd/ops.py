@@ -30,7 +30,9 @@ torch.ops.load_library(LIB_PATH)
 ops = torch.ops.inferd
 
 OPS = ("span_create", "span_destroy", "span_config", "span_init_synthetic", "span_set_weight", "span_error_flags",
-       "span_profile_start", "span_profile_stop", "span_forward", "span_lm_head", "weightgen", "kv_create",
+       "span_profile_start", "span_profile_stop", "span_forward", "span_lm_head", "span_head_shard", "argmax_combine",
+       "dedicated_stream",
+       "weightgen", "kv_create",
        "kv_destroy", "kv_reserve", "kv_advance", "kv_release", "kv_query", "kv_pages", "kv_free_pages",
        "kv_build_batch")
 CLASSES = ("DecodeGraph",)
@@ -42,9 +44,11 @@ def span_config(dims, first_layer: int, n_layers: int, *, has_embed: bool, has_l
                 max_tokens: int, max_seqs: int, max_positions: int, skip_first_attn: bool = False,
                 skip_last_mlp: bool = False, gateup_split_first: int = 0, gateup_split_last: int = 0,
                 o_split_first: bool = False, o_split_last: bool = False, qkv_split_first: bool = False,
-                qkv_split_last: bool = False) -> list:
-    """The 22 config ints of span_create (InferdSpanConfig order)."""
+                qkv_split_last: bool = False, head_first: int = 0, head_rows: int = 0,
+                final_norm_out: bool = False) -> list:
+    """The 25 config ints of span_create (InferdSpanConfig order)."""
     return [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
             n_layers, int(has_embed), int(has_lm_head), max_positions, kv_pages, max_tokens, max_seqs,
             int(skip_first_attn), int(skip_last_mlp), int(gateup_split_first), int(gateup_split_last),
-            int(o_split_first), int(o_split_last), int(qkv_split_first), int(qkv_split_last)]
+            int(o_split_first), int(o_split_last), int(qkv_split_first), int(qkv_split_last), int(head_first),
+            int(head_rows), int(final_norm_out)]

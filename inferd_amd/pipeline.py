@@ -552,10 +552,21 @@ class SpanExecutor:
         else:
             self.graphs[m].launch()
 
-    def profile_decode(self, microbatches, bufs, n_steps):
+    def head(self, normed, rows, keys_in=None, keys_out=None, ids=None):
+        """This span's lm_head shard over `rows` normed rows (vocab-parallel head; SpanRuntime.head_shard)."""
+        self.span.head_shard(normed, rows, keys_in, keys_out, ids)
+
+    @staticmethod
+    def combine(keys, n_parts, rows, ids):
+        """ids from n_parts shards' keys [n_parts, rows] (torch.ops.inferd.argmax_combine)."""
+        from .ops import ops as T
+        T.argmax_combine(keys, n_parts, rows, ids)
+
+    def profile_decode(self, microbatches, bufs, n_steps, head=None):
         """Eager (non-graph) decode steps with per-kernel-class HIP events on the launch
         stream, for kernel timings (HIP cannot time event-record nodes inside a replayed
-        graph: hipEventElapsedTime rejects them).  Returns {kernel class: (total ms, launches)}."""
+        graph: hipEventElapsedTime rejects them); `head` (a callable) runs after every
+        microbatch step (a vocab-parallel head's shard).  Returns {kernel class: (total ms, launches)}."""
         self.span.profile_start(1 << 17)
         for _ in range(n_steps):
             for m, sessions in enumerate(microbatches):
@@ -564,46 +575,165 @@ class SpanExecutor:
                 b = bufs[m]
                 self.span.run(batch, ids=b.get("ids"), x=b.get("x"), hidden=b.get("hidden_out"),
                               next_ids=b.get("next_ids"))
+                if head is not None:
+                    head()
                 for st in states:
                     st.length += 1
         torch.cuda.synchronize(self.device)
         return self.span.profile_stop()
 
 
+def ring_microbatches(world: int, sharded_head: bool = False, slack: int = 1) -> int:
+    """Microbatches in flight on the decode ring: one per stage for the layer path, one per stage
+    more when the greedy head runs vocab-parallel (its chain goes round the ring once more before the
+    ids reach stage 0), plus `slack` (each unit lets the ring absorb one tick of summed hand-off
+    latency: throughput = min(1 / tick, n_mb / (S * (tick + x))) per hop latency x)."""
+    return world * (2 if sharded_head else 1) + (slack if world > 1 else 0)
+
+
+def head_shard_split(stage_us, vocab: int, head_us: float, fixed_us: float = 6.0, step: int = 256,
+                     min_rows: int = 0):
+    """Rows of a vocab-parallel lm_head per stage ([(first, rows)] in stage order, covering
+    [0, vocab)) that level the stages' decode times: stage s costs stage_us[s] (its layers) plus,
+    with a shard of r rows, fixed_us + head_us * r / vocab (the shard GEMV streams r * hidden * 2
+    bytes; fixed_us: its launches, ramp and key reduction).  Water-filling on a 0.01-us grid; rows in
+    multiples of `step` (the remainder to the stage with the most room left).  min_rows: every stage
+    gets at least that many rows (0: stages whose layers already reach the level get none)."""
+    n = len(stage_us)
+    per_row = head_us / vocab
+    units = vocab // step
+    assert units * step == vocab or vocab % 16 == 0
+
+    def rows_at(level):
+        return [max(0.0, (level - t - fixed_us) / per_row) for t in stage_us]
+    lo, hi = min(stage_us), max(stage_us) + head_us + fixed_us
+    for _ in range(100):
+        mid = (lo + hi) / 2
+        if sum(rows_at(mid)) >= vocab:
+            hi = mid
+        else:
+            lo = mid
+    want = rows_at(hi)
+    rows = [max(min_rows, int(w // step) * step) for w in want]
+    left = vocab - sum(rows)
+    # hand out the rest in steps to the stages with the lowest resulting time
+    while left > 0:
+        cost = [stage_us[s] + (fixed_us + per_row * rows[s] if rows[s] else 0.0) for s in range(n)]
+        s = min(range(n), key=lambda k: cost[k] + (fixed_us if rows[k] == 0 else 0.0))
+        take = min(step, left)
+        rows[s] += take
+        left -= take
+    while left < 0:      # min_rows overshoot: take back from the slowest
+        cost = [stage_us[s] + fixed_us + per_row * rows[s] for s in range(n)]
+        s = max((k for k in range(n) if rows[k] > min_rows), key=lambda k: cost[k])
+        give = min(step, -left, rows[s] - min_rows)
+        rows[s] -= give
+        left += give
+    out, f = [], 0
+    for r in rows:
+        out.append((f, r))
+        f += r
+    return out
+
+
+class _InLink:
+    """The receiving end of this stage's ring edge from its predecessor: the messages the predecessor
+    sends, in its order (one communicator per edge keeps them FIFO), posted as receives a bounded
+    window ahead of their use.  need() posts up to and including a message and makes the current
+    stream wait for it (host-blocking only on gloo)."""
+
+    def __init__(self, stage: "PipelineStage", msgs):
+        self.st, self.msgs = stage, msgs
+        self.index = {m: i for i, m in enumerate(msgs)}
+        self.posted, self.high = 0, -1
+        self.handles = {}
+
+    def _post_next(self):
+        spec = self.msgs[self.posted]
+        self.handles[spec] = self.st._post_recv(spec)
+        self.posted += 1
+
+    def need(self, spec):
+        """Receives are posted in the sender's order; they may be waited for in another order
+        (with more slack than one item stage 0 uses a microbatch's ids after later normed rows)."""
+        i = self.index[spec]
+        self.high = max(self.high, i)
+        while self.posted <= i:
+            self._post_next()
+        h, buf = self.handles.pop(spec)
+        self.st._wait(h)
+        return buf
+
+    def drained(self) -> bool:
+        return self.posted == len(self.msgs) and not self.handles
+
+    def prefetch(self, n: int = 1):
+        """keep the next n messages after the last one needed posted (their transfer overlaps the
+        compute launched next)"""
+        while self.posted < min(len(self.msgs), self.high + 1 + n):
+            self._post_next()
+
+
 class PipelineStage:
-    """One rank of the span pipeline (rank 0 = FirstStage, rank S-1 = LastStage)."""
+    """One rank of the span pipeline (rank 0 = FirstStage, rank S-1 = LastStage).
+
+    Decode runs as an ASYNCHRONOUS RING (round 6): n_mb >= S microbatches are in flight and every
+    stage processes work items (decode step k, microbatch m; item i = k * n_mb + m) in order, each as
+    soon as its inputs have arrived -- there is no global tick.  Each directed ring edge s -> s+1 (and
+    the wrap S-1 -> 0) is a 2-rank process group of its own, so every RCCL hand-off runs on that
+    communicator's stream: a stage posts the receive of item i+1 before it launches item i (the
+    transfer overlaps the compute), its sends are posted right after the producing launch, and the
+    compute stream waits (work.wait(): a stream wait, the host never blocks on RCCL) only on the
+    input it is about to use.  With n_mb = S + 1 the ring holds one item of slack: throughput is
+    min(1 / c, n_mb / (S (c + x))) for stage time c and per-hop latency x, so up to x = c / S of
+    hand-off per hop is hidden.
+
+    Vocab-parallel greedy head (sharded_head): the last stage ends with the final norm and hands the
+    normed last rows (128 KiB at B = 16) round the ring; stage s runs its lm_head shard on them S
+    items after the layers (one ring lap behind), folding its (max logit, first index) keys into the
+    running keys it forwards; the last stage's shard finishes the argmax and sends the ids to stage
+    0.  Every hand-off stays on the ring's own edges (one inbound and one outbound communicator per
+    GPU).  Item j's ids reach stage 0 S iterations after its normed rows left the last stage, 2S
+    iterations after stage 0 ran its layers: n_mb = 2S + slack."""
 
     def __init__(self, dims: ModelDims, rank: int, world: int, first_layer: int, n_layers: int, *,
                  device, seed: int, n_microbatches: int, batch: int, max_ctx: int, prefill_chunk: int = 2,
                  executor=None, group=None, profile: str = "random", want_logits: bool = False,
                  skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
                  gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False,
-                 qkv_split_first: bool = False, qkv_split_last: bool = False, eager_decode: bool = True):
+                 qkv_split_first: bool = False, qkv_split_last: bool = False, eager_decode: bool = True,
+                 sharded_head: bool = False, head_shard=(0, 0)):
         """profile: the synthetic weight profile (runtime.SpanRuntime.init_synthetic: "peaked"
-        for token-exact parity runs).  want_logits (last stage): every decode step's and the
-        prefill's last-row logits are kept, for parity checks against the oracle's.
-        skip_first_attn / skip_last_mlp / gateup_split_*: the stage's sub-layer boundaries
-        (StageRange.span_kwargs()); across a gate/up boundary a decode-sized hand-off is a record
-        (h1 + the packed SwiGLU product, handoff_elems), across an attention|o boundary (o_split_*)
-        every hand-off is one (x + the attention output), across a q/k/v|attention boundary
-        (qkv_split_*) every decode hand-off (x + the raw q/k/v rows)."""
-        assert n_microbatches == world, "the ring schedule keeps exactly one microbatch per stage in flight"
+        for token-exact parity runs).  want_logits (last stage, whole head only): every decode step's
+        and the prefill's last-row logits are kept, for parity checks against the oracle's.
+        skip_first_attn / skip_last_mlp / gateup_split_* / o_split_* / qkv_split_*: the stage's
+        sub-layer boundaries (StageRange.span_kwargs(); the hand-offs are records, handoff_elems).
+        n_microbatches: >= world (ring_microbatches(world, sharded_head) adds the ring's slack).
+        sharded_head / head_shard: the greedy head vocab-parallel over the stages, this stage owning
+        lm_head rows [head_shard[0], head_shard[0] + head_shard[1]) (head_shard_split)."""
+        assert n_microbatches >= world * (2 if sharded_head and world > 1 else 1), \
+            "the ring needs a microbatch per stage in flight (two with a vocab-parallel head)"
+        assert not (sharded_head and want_logits), "logits capture needs the whole head on the last stage"
         self.dims, self.rank, self.world = dims, rank, world
         self.S = world
         self.n_mb, self.B = n_microbatches, batch
         self.device = torch.device(device)
         self.group = group
         self.prefill_chunk = prefill_chunk
+        self.sharded = bool(sharded_head) and world > 1
+        self.head_first, self.head_rows = (int(head_shard[0]), int(head_shard[1])) if self.sharded else (0, 0)
+        last = rank == world - 1
         if executor is None:
             pages_per_seq = (max_ctx + KV_PAGE - 1) // KV_PAGE + 1
-            span = SpanRuntime(dims, first_layer, n_layers, has_embed=(rank == 0), has_lm_head=(rank == world - 1),
+            span = SpanRuntime(dims, first_layer, n_layers, has_embed=(rank == 0), has_lm_head=last and not self.sharded,
                                kv_pages=n_microbatches * batch * pages_per_seq + 4,
                                max_tokens=max(prefill_chunk * max_ctx, batch), max_seqs=max(batch, prefill_chunk),
                                max_positions=max_ctx, device=self.device, skip_first_attn=skip_first_attn,
                                skip_last_mlp=skip_last_mlp, gateup_split_first=gateup_split_first,
                                gateup_split_last=gateup_split_last, o_split_first=o_split_first,
                                o_split_last=o_split_last, qkv_split_first=qkv_split_first,
-                               qkv_split_last=qkv_split_last)
+                               qkv_split_last=qkv_split_last, head_first=self.head_first, head_rows=self.head_rows,
+                               final_norm_out=last and self.sharded)
             span.init_synthetic(seed, profile)
             executor = SpanExecutor(span, eager=eager_decode)
         self.ex = executor
@@ -624,16 +754,41 @@ class PipelineStage:
         self.h_in = [buf(self.col_in, self.o_in, self.q_in) for _ in mb]
         self.h_out = [buf(self.col_out, self.o_out, self.q_out) for _ in mb]
         self.ids_out = [torch.zeros(batch, dtype=torch.int32, device=dev) for _ in mb]
-        self.want_logits = want_logits and rank == world - 1
+        # vocab-parallel head: the last stage's final-normed rows (fragment-packed 16-row tiles) and
+        # every stage's head record [normed rows | running keys int64 [B]] (bytes)
+        self.normed_bytes = (batch + 15) // 16 * 16 * h * 2
+        if self.sharded:
+            self.normed = [torch.zeros(self.normed_bytes // 2, dtype=torch.bfloat16, device=dev) for _ in mb] \
+                if last else None
+            self.head_rec = [torch.zeros(self.normed_bytes + 8 * batch, dtype=torch.uint8, device=dev) for _ in mb]
+        self.want_logits = want_logits and last
         self.logits = [torch.zeros(batch, dims.vocab, dtype=torch.bfloat16, device=dev) for _ in mb] \
             if self.want_logits else None
         self.step_base = 0   # decode steps already run (absolute step of the next decode call)
-        # host time per tick of the last decode() call, split into the hand-off (exchange wait
-        # included) and the rest (graph launch, page-table advance, schedule bookkeeping)
+        # host time per tick of the last decode() call, split into the hand-off (posts and waits)
+        # and the rest (launches, page-table advance, schedule bookkeeping)
         self.tick_stats = None
         self.first_layer, self.n_layers = first_layer, n_layers
         self._exchanged = False     # first hand-off done (logged once)
         self._inflight = None       # the last exchange's transient tensors (see _exchange)
+        self._pending = {}          # buffer key -> a send still reading that buffer
+        self.prev_rank, self.next_rank = (rank - 1) % world, (rank + 1) % world
+        self.link_in = self.link_out = None
+        # streams (GPU ranks of a multi-stage pipeline): every launch of the stage runs on a compute
+        # stream with a hardware queue of its own (torch.ops.inferd.dedicated_stream), so an RCCL
+        # receive posted ahead of its data -- resident on its communicator's stream -- never holds
+        # back a compute kernel that happens to share its queue; receives are posted from a side
+        # stream that waits only on the event of the buffer's last use (self._use), not on the
+        # compute queued since
+        self.cstream = self.pstream = None
+        self._use = {}
+        if world > 1 and self.device.type == "cuda":
+            from .ops import ops as T
+            self.cstream = torch.cuda.ExternalStream(T.dedicated_stream(self.device), device=self.device)
+            self.pstream = torch.cuda.Stream(device=self.device)
+        if world > 1:
+            with self._compute():
+                self._make_links()
 
     @property
     def first(self):
@@ -643,6 +798,146 @@ class PipelineStage:
     def last(self):
         return self.rank == self.S - 1
 
+    def head_normed(self, rec):
+        return rec[:self.normed_bytes].view(torch.bfloat16)
+
+    def head_keys(self, rec):
+        return rec[self.normed_bytes:self.normed_bytes + 8 * self.B].view(torch.int64)
+
+    # ------------------------------------------------------------------ ring links
+    def _global(self, r: int) -> int:
+        import torch.distributed as dist
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def _make_links(self):
+        """One 2-rank process group per directed ring edge e -> e+1 (e = 0 .. S-1; at S = 2 the two
+        directions are two groups over the same pair), created by every rank in the same order (as
+        new_group requires), then warmed up edge by edge in that order: RCCL sets a p2p connection up
+        at its first use, so each edge's first send / receive happens here, pairwise in a global
+        order -- no rank can be waiting on a connection its partner has not reached."""
+        import torch.distributed as dist
+        S = self.S
+        links = [dist.new_group([self._global(e), self._global((e + 1) % S)]) for e in range(S)]
+        self.link_out, self.link_in = links[self.rank], links[(self.rank - 1) % S]
+        one = torch.zeros(1, dtype=torch.int32, device=self.device)
+        for e in range(S):
+            if self.rank == e:
+                self._wait(self._post(True, one, (e + 1) % S, links[e]))
+            elif self.rank == (e + 1) % S:
+                self._wait(self._post(False, one, e, links[e]))
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def _post(self, send: bool, t, peer: int, group):
+        """Post one isend / irecv of tensor t to / from stage `peer` on `group`.  Returns a handle
+        for _wait.  RCCL: the op runs on the group's stream after the current stream's earlier
+        work.  gloo with device tensors (GPU ranks rehearsing without RCCL): staged through host
+        memory (a send copies out at once; a receive lands in a host tensor copied in at _wait)."""
+        import torch.distributed as dist
+        staged = t.is_cuda and dist.get_backend(group) == "gloo"
+        dst = None
+        if staged:
+            if send:
+                t = t.cpu()
+            else:
+                dst, t = t, torch.empty(t.shape, dtype=t.dtype)
+        works = dist.batch_isend_irecv([dist.P2POp(dist.isend if send else dist.irecv, t, self._global(peer), group)])
+        return works, t, dst
+
+    @staticmethod
+    def _wait(h):
+        works, t, dst = h
+        for w in works:
+            w.wait()
+        if dst is not None:
+            dst.copy_(t)
+
+    def _settle(self, key):
+        """Before a buffer is written again (by a launch or a receive): the send still reading it
+        must be done -- on RCCL a stream wait (free: the send was posted an item or more ago)."""
+        h = self._pending.pop(key, None)
+        if h is not None:
+            self._wait(h)
+
+    def _send(self, key, t):
+        self._settle(key)
+        self._pending[key] = self._post(True, t, self.next_rank, self.link_out)
+
+    def _used(self, *keys):
+        """The compute stream's launches so far are the last users of these buffers (an event per
+        buffer; a receive into one waits on it, _post_recv)."""
+        if self.cstream is None:
+            return
+        for k in keys:
+            ev = self._use.get(k)
+            if ev is None:
+                ev = self._use[k] = torch.cuda.Event()
+            ev.record(self.cstream)
+
+    def _post_recv(self, spec):
+        """Post the receive of ring message `spec` into its buffer, once the buffer's last user (a
+        launch, _used; a send forwarding it, _pending) is done -- from the side stream, so the receive
+        starts then and not after the compute queued since.  Returns (handle, buffer)."""
+        buf, key = self._recv_buf(spec)
+        if self.pstream is None:
+            self._settle(key)
+            return self._post(False, buf, self.prev_rank, self.link_in), buf
+        with torch.cuda.stream(self.pstream):
+            self._settle(key)                       # a forwarded record still being sent from it
+            ev = self._use.get(key)
+            if ev is not None:
+                self.pstream.wait_event(ev)
+            return self._post(False, buf, self.prev_rank, self.link_in), buf
+
+    def _compute(self):
+        """Context: the stage's launches on its compute stream, ordered after the caller's stream's
+        earlier work and before its later work."""
+        import contextlib
+        if self.cstream is None:
+            return contextlib.nullcontext()
+        st = self
+
+        class _Ctx:
+            def __enter__(self):
+                self.caller = torch.cuda.current_stream(st.device)
+                st.cstream.wait_stream(self.caller)
+                self.cm = torch.cuda.stream(st.cstream)
+                self.cm.__enter__()
+
+            def __exit__(self, *a):
+                self.cm.__exit__(*a)
+                self.caller.wait_stream(st.cstream)
+        return _Ctx()
+
+    # messages on the edge out of stage s at iteration t of a decode call of n items (the sender's
+    # order; one communicator per edge keeps them FIFO): ("h", i) the layer hand-off of item i,
+    # ("k", j) the head record after stage s's shard of item j, ("n", t) the last stage's normed rows,
+    # ("i", j) the greedy ids of item j (last stage -> stage 0)
+    def _msgs_out(self, s: int, t: int, n_items: int, D: int):
+        last = s == self.S - 1
+        out = []
+        if t < n_items:
+            out.append(("h", t) if not last else (("n", t) if self.sharded else ("i", t)))
+        j = t - D
+        if self.sharded and 0 <= j < n_items:
+            out.append(("i", j) if last else ("k", j))
+        return out
+
+    def _recv_buf(self, spec):
+        """(tensor, buffer key) a message lands in on this stage"""
+        kind, i = spec
+        m = i % self.n_mb
+        if kind == "h":
+            t = self.h_in[m]
+            if self.col_in or self.o_in or self.q_in:
+                t = t[:handoff_elems(self.dims, self.B, self.col_in, self.o_in, True, self.q_in)]
+            return t, ("h_in", m)
+        if kind == "i":
+            return self.ids[m], ("ids", m)
+        if kind == "n":
+            return self.head_normed(self.head_rec[m]), ("head", m)
+        return self.head_rec[m], ("head", m)
+
     def _bufs(self, m):
         """Fixed buffers of microbatch m for this stage's role."""
         lg = {"logits": self.logits[m]} if self.want_logits else {}
@@ -651,29 +946,24 @@ class PipelineStage:
         if self.first:
             return {"ids": self.ids[m], "x": None, "hidden_out": self.h_out[m], "next_ids": None}
         if self.last:
+            if self.sharded:
+                return {"ids": None, "x": self.h_in[m], "hidden_out": self.normed[m], "next_ids": None}
             return {"ids": None, "x": self.h_in[m], "hidden_out": None, "next_ids": self.ids_out[m], **lg}
         return {"ids": None, "x": self.h_in[m], "hidden_out": self.h_out[m], "next_ids": None}
 
     def _exchange(self, send=None, send_to=None, recv=None, recv_from=None):
-        """One grouped hand-off of this tick: isend `send` to the next stage, irecv `recv` from
-        the previous one (the reference's HTTP hop node.py:102-130, as RCCL p2p over xGMI).
+        """One grouped hand-off on the pipeline's process group (prefill; lockstep): isend `send`
+        to stage send_to, irecv `recv` from stage recv_from (the reference's HTTP hop
+        node.py:102-130, as RCCL p2p over xGMI).
 
         Tensor lifetimes on the nccl path (RCCL runs on its own stream; `work.wait()` makes
         torch's current stream wait for it without blocking the host, and the process group
-        orders its stream after the current stream's earlier work):
-          * decode: send / recv are the stage's fixed per-microbatch buffers (h_out / ids_out,
-            h_in / ids), allocated once in __init__ and captured by the decode graphs: they
-            live as long as the stage.  A buffer is rewritten by its microbatch's next graph
-            replay, which runs on the current stream after the wait, i.e. after the send
-            finished reading it; a recv lands before the graph that reads it (same wait).
-          * prefill: the send is a per-chunk output popped from bufs_out and the recv a fresh
-            tensor per tick.  Both are kept referenced here until the NEXT exchange (one tick
-            later), so the caching allocator cannot hand their blocks to a new tensor while
-            the send may be in flight, whether or not the process group records its stream on
-            p2p inputs.
-          * the first-ids hand-off after prefill (`flat`): a one-off tensor, kept the same way.
-        On gloo (CPU-rank tests, GPU ranks rehearsing without RCCL) device tensors are staged
-        through host memory synchronously."""
+        orders its stream after the current stream's earlier work): the prefill send is a per-chunk
+        output and the recv a fresh tensor per tick; both are kept referenced here until the NEXT
+        exchange, so the caching allocator cannot hand their blocks to a new tensor while the send
+        may be in flight, whether or not the process group records its stream on p2p inputs; the
+        first-ids hand-off after prefill (`flat`) likewise.  On gloo (CPU-rank tests, GPU ranks
+        rehearsing without RCCL) device tensors are staged through host memory synchronously."""
         import torch.distributed as dist
         staged = dist.get_backend(self.group) == "gloo"
         dst = None
@@ -684,9 +974,9 @@ class PipelineStage:
                 dst, recv = recv, torch.empty(recv.shape, dtype=recv.dtype)
         ops = []
         if send is not None:
-            ops.append(dist.P2POp(dist.isend, send, send_to, self.group))
+            ops.append(dist.P2POp(dist.isend, send, self._global(send_to), self.group))
         if recv is not None:
-            ops.append(dist.P2POp(dist.irecv, recv, recv_from, self.group))
+            ops.append(dist.P2POp(dist.irecv, recv, self._global(recv_from), self.group))
         t0 = time.perf_counter() if not self._exchanged else 0.0
         if ops:
             for w in dist.batch_isend_irecv(ops):
@@ -705,9 +995,24 @@ class PipelineStage:
                   f" (send->{send_to if send is not None else '-'}, recv<-{recv_from if recv is not None else '-'},"
                   f" {(time.perf_counter() - t0) * 1e3:.1f} ms)", file=sys.stderr, flush=True)
 
+    # ------------------------------------------------------------------ head (vocab-parallel)
+    def _head(self, normed, keys_in, keys_out, ids):
+        """This stage's lm_head shard over the B normed rows, folded into the running keys (or the
+        ids on the last stage); a stage without rows passes the keys on (stage 0 starts them at 0)."""
+        if self.head_rows:
+            self.ex.head(normed, self.B, keys_in=keys_in, keys_out=keys_out, ids=ids)
+        elif ids is not None:
+            self.ex.combine(keys_in, 1, self.B, ids)
+        elif keys_in is None:
+            keys_out.zero_()
+
     # ------------------------------------------------------------------ prefill
     @torch.no_grad()
     def prefill(self, prompts, capture=None):
+        with self._compute():
+            self._prefill(prompts, capture)
+
+    def _prefill(self, prompts, capture=None):
         """prompts: per microbatch an int tensor [B, T] (read on the first stage only).
         Runs every microbatch's prompt through the pipeline in chunks of prefill_chunk
         sequences; leaves the first decode ids of every microbatch on stage 0.  `capture`
@@ -752,20 +1057,24 @@ class PipelineStage:
                 sess = self.sessions[m][c:c + self.prefill_chunk]
                 wl = self.want_logits and capture is not None
                 kw = {"want_logits": True} if wl else {}
+                want_ids = self.last and not self.sharded
                 if self.first:
                     ids = prompts[m][c:c + len(sess)].reshape(-1).to(self.device, torch.int32)
-                    out = self.ex.prefill(sess, T, ids=ids, want_ids=self.last, **kw)
+                    out = self.ex.prefill(sess, T, ids=ids, want_ids=want_ids, **kw)
                 else:
-                    out = self.ex.prefill(sess, T, x=bufs_in.pop(i_cur), want_ids=self.last, **kw)
+                    out = self.ex.prefill(sess, T, x=bufs_in.pop(i_cur), want_ids=want_ids, **kw)
                 if self.last:
                     if wl:
                         out, lg = out
                         capture.setdefault("logits_parts", {})[(m, c)] = lg.cpu()
-                    ids_parts[(m, c)] = out
+                    ids_parts[(m, c)] = out      # the greedy ids, or (vocab-parallel head) the normed rows
                 else:
                     bufs_out[i_cur] = out
                     if capture is not None and i_cur == 0:     # h1 rows (the head of a record)
                         capture["hidden"] = out.reshape(-1)[:len(sess) * T * h].reshape(len(sess) * T, h).cpu()
+        if self.sharded:
+            self._prefill_head(ids_parts)
+            return
         if self.last:
             for m in range(self.n_mb):
                 first_ids[m] = torch.cat([ids_parts[(m, c)] for c in range(0, self.B, self.prefill_chunk)])
@@ -787,31 +1096,72 @@ class PipelineStage:
                 for m in range(self.n_mb):
                     self.ids[m].copy_(flat[m * self.B:(m + 1) * self.B])
 
+    def _prefill_head(self, normed_parts):
+        """The vocab-parallel head of every microbatch's prompt (its last rows): the last stage's
+        normed rows go to stage 0 and along the ring through every shard, the last stage finishes
+        the argmax and returns the first decode ids to stage 0 -- one microbatch at a time on the
+        pipeline's group (untimed)."""
+        S, h, B = self.S, self.dims.hidden, self.B
+        full = {}
+        if self.last:     # each chunk's packed rows -> the microbatch's B rows, packed
+            for m in range(self.n_mb):
+                rows = [unpack_rows(normed_parts[(m, c)].reshape(-1), min(self.prefill_chunk, B - c), h)
+                        for c in range(0, B, self.prefill_chunk)]
+                full[m] = torch.zeros(self.normed_bytes // 2, dtype=torch.bfloat16, device=self.device)
+                p = pack_rows(torch.cat(rows))
+                full[m][:p.numel()].copy_(p)
+        for m in range(self.n_mb):
+            rec = self.head_rec[m]
+            if self.last:
+                self._exchange(send=full[m], send_to=0)
+                self._exchange(recv=rec, recv_from=S - 2)
+                self._head(full[m], self.head_keys(rec), None, self.ids_out[m])
+                self._exchange(send=self.ids_out[m], send_to=0)
+                continue
+            if self.first:
+                self._exchange(recv=self.head_normed(rec), recv_from=S - 1)
+                self._head(self.head_normed(rec), None, self.head_keys(rec), None)
+            else:
+                self._exchange(recv=rec, recv_from=self.rank - 1)
+                self._head(self.head_normed(rec), self.head_keys(rec), self.head_keys(rec), None)
+            self._exchange(send=rec, send_to=self.rank + 1)
+            if self.first:
+                self._exchange(recv=self.ids[m], recv_from=S - 1)
+        self._inflight = (full, None)
+        if self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+
     # ------------------------------------------------------------------ decode
     def prepare_decode(self, n_steps: int):
         """Reserve cache pages for n_steps tokens per sequence and capture the decode graphs."""
-        self.ex.prepare_decode(self.sessions, n_steps, [self._bufs(m) for m in range(self.n_mb)])
+        with self._compute():
+            self.ex.prepare_decode(self.sessions, n_steps, [self._bufs(m) for m in range(self.n_mb)])
 
     @torch.no_grad()
     def decode(self, n_steps: int, record=None, record_logits=None, force=None):
+        with self._compute():
+            self._decode(n_steps, record, record_logits, force)
+
+    def _decode(self, n_steps: int, record=None, record_logits=None, force=None):
         """Run n_steps decode steps of every microbatch.  `record` (stage 0 only): list that
         receives (absolute step, microbatch, ids tensor copy) of every input fed to the first
         span; `record_logits` (last stage of a want_logits pipeline): list that receives
         (absolute step, microbatch, device copy of the step's last-row logits [B, vocab]);
         `force` (stage 0 only, teacher forcing for parity runs): int tensor [steps, B] -- the
         ids fed at absolute step k are force[k] instead of the last stage's greedy choice.
-        Sets self.tick_stats: host microseconds per tick, hand-off (exchange) and the rest."""
+        Sets self.tick_stats: host microseconds per item, hand-off (posts and waits) and the rest.
+        On return stage 0 holds every microbatch's next ids (the next call continues the ring)."""
         def feed(k, m):
             if force is not None and self.first:
                 self.ids[m].copy_(force[self.step_base + k].to(self.ids[m].device, torch.int32),
                                   non_blocking=True)
-        S = self.S
-        n_items = n_steps * self.n_mb
+        S, n_mb = self.S, self.n_mb
+        n_items = n_steps * n_mb
         t_x = 0.0
         t0 = time.perf_counter()
         if S == 1:
             for i in range(n_items):
-                k, m = divmod(i, self.n_mb)
+                k, m = divmod(i, n_mb)
                 feed(k, m)
                 if record is not None:
                     record.append((self.step_base + k, m, self.ids[m].clone()))
@@ -821,36 +1171,68 @@ class PipelineStage:
             self.step_base += n_steps
             self._tick_stats(n_items, time.perf_counter() - t0, 0.0)
             return
-        for t in range(n_items + S):
-            i_cur = t - self.rank
-            i_prev = t - 1 - self.rank
-            send = recv = None
-            if 0 <= i_prev < n_items:                      # output of last tick
-                mp = i_prev % self.n_mb
-                send = self.ids_out[mp] if self.last else self.h_out[mp]
-                if (self.col_out or self.o_out or self.q_out) and not self.last:   # a record (the part carrying data)
-                    send = send[:handoff_elems(self.dims, self.B, self.col_out, self.o_out, True, self.q_out)]
-            if self.first:
-                j = t - S                                  # ids of item j feed item j + S
-                if 0 <= j < n_items:
-                    recv = self.ids[j % self.n_mb]
-            elif 0 <= i_cur < n_items:
-                recv = self.h_in[i_cur % self.n_mb]
-                if self.col_in or self.o_in or self.q_in:
-                    recv = recv[:handoff_elems(self.dims, self.B, self.col_in, self.o_in, True, self.q_in)]
-            tx = time.perf_counter()
-            self._exchange(send, (self.rank + 1) % S, recv, (self.rank - 1) % S)
-            t_x += time.perf_counter() - tx
-            if 0 <= i_cur < n_items:
-                k, m = divmod(i_cur, self.n_mb)
+        D = S if self.sharded else 0          # the head runs one ring lap behind the layers
+        n_iter = n_items + D
+        pred = (self.rank - 1) % S
+        link = _InLink(self, [m for t in range(n_iter) for m in self._msgs_out(pred, t, n_items, D)])
+        hand = self.col_out or self.o_out or self.q_out
+        n_hand = handoff_elems(self.dims, self.B, self.col_out, self.o_out, True, self.q_out) if hand else 0
+        for it in range(n_iter):
+            if it < n_items:
+                k, m = divmod(it, n_mb)
+                tx = time.perf_counter()
+                if not self.first:
+                    link.need(("h", it))
+                elif it >= n_mb:
+                    link.need(("i", it - n_mb))       # this microbatch's ids, from its previous step
+                t_x += time.perf_counter() - tx
                 feed(k, m)
                 if self.first and record is not None:
                     record.append((self.step_base + k, m, self.ids[m].clone()))
+                out_key, out = (("h_out", m), self.h_out[m]) if not self.last else \
+                    ((("normed", m), self.normed[m]) if self.sharded else (("ids_out", m), self.ids_out[m]))
+                self._settle(out_key)
                 self.ex.decode(m)
+                self._used(("ids", m) if self.first else ("h_in", m))
                 if record_logits is not None and self.want_logits:
                     record_logits.append((self.step_base + k, m, self.logits[m].clone()))
+                tx = time.perf_counter()
+                self._send(out_key, out[:n_hand] if (hand and not self.last) else out)
+                # the next message's receive, posted after this iteration's sends: a receive waiting
+                # for its data never sits in front of a send (two communicators may share a queue)
+                link.prefetch(1)
+                t_x += time.perf_counter() - tx
+            j = it - D
+            if self.sharded and 0 <= j < n_items:
+                mj = j % n_mb
+                tx = time.perf_counter()
+                rec = link.need(("n", j) if self.first else ("k", j))
+                t_x += time.perf_counter() - tx
+                rec = self.head_rec[mj]
+                if self.last:
+                    self._settle(("ids_out", mj))
+                    self._head(self.normed[mj], self.head_keys(rec), None, self.ids_out[mj])
+                    self._used(("head", mj))
+                    tx = time.perf_counter()
+                    self._send(("ids_out", mj), self.ids_out[mj])
+                else:
+                    self._head(self.head_normed(rec), None if self.first else self.head_keys(rec),
+                               self.head_keys(rec), None)
+                    self._used(("head", mj))
+                    tx = time.perf_counter()
+                    self._send(("head", mj), rec)
+                link.prefetch(1)
+                t_x += time.perf_counter() - tx
+        if self.first:     # the next call's first ids: the last n_mb items' greedy choices
+            tx = time.perf_counter()
+            for j in range(max(0, n_items - n_mb), n_items):
+                link.need(("i", j))
+            t_x += time.perf_counter() - tx
+        assert link.drained(), "decode ended with ring messages not received"
+        for key in list(self._pending):
+            self._settle(key)
         self.step_base += n_steps
-        self._tick_stats(n_items + S, time.perf_counter() - t0, t_x)
+        self._tick_stats(n_iter, time.perf_counter() - t0, t_x)
 
     def _tick_stats(self, ticks, total_s, exchange_s):
         self.tick_stats = {"ticks": ticks, "host_us_per_tick": round((total_s - exchange_s) / ticks * 1e6, 1),
@@ -858,8 +1240,17 @@ class PipelineStage:
 
     def profile_decode(self, n_steps: int):
         """Per-kernel timings from eager (event-instrumented) decode steps on this stage,
-        without exchanges (kernel durations do not depend on where inputs came from)."""
-        return self.ex.profile_decode(self.sessions, [self._bufs(m) for m in range(self.n_mb)], n_steps)
+        without exchanges (kernel durations do not depend on where inputs came from); with a
+        vocab-parallel head each step also runs this stage's shard."""
+        head = None
+        if self.sharded:
+            rec = self.head_rec[0]
+            normed = self.normed[0] if self.last else self.head_normed(rec)
+            head = lambda: self._head(normed, self.head_keys(rec) if not self.first else None,  # noqa: E731
+                                      None if self.last else self.head_keys(rec),
+                                      self.ids_out[0] if self.last else None)
+        with self._compute():
+            return self.ex.profile_decode(self.sessions, [self._bufs(m) for m in range(self.n_mb)], n_steps, head)
 
     def release(self):
         if self.span is not None:

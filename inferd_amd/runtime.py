@@ -210,7 +210,8 @@ class SpanRuntime:
                  max_positions: int | None = None, device: str | torch.device = "cuda",
                  skip_first_attn: bool = False, skip_last_mlp: bool = False, gateup_split_first: int = 0,
                  gateup_split_last: int = 0, o_split_first: bool = False, o_split_last: bool = False,
-                 qkv_split_first: bool = False, qkv_split_last: bool = False):
+                 qkv_split_first: bool = False, qkv_split_last: bool = False, head_first: int = 0,
+                 head_rows: int = 0, final_norm_out: bool = False):
         """skip_first_attn / skip_last_mlp: sub-layer stage boundaries (InferdSpanConfig): the
         span starts at its first layer's MLP half (x = that layer's post-attention residual)
         and/or ends after its last layer's attention half (hidden out = that residual).
@@ -221,7 +222,11 @@ class SpanRuntime:
         residual, then the attention output: o_record_elems()).  qkv_split_first / _last: the
         boundary sits between a layer's q/k/v projection and its attention; a pure decode call
         hands over a record (x, then the raw q/k/v rows: q_record_elems()), other calls x alone
-        (the receiver runs the whole layer)."""
+        (the receiver runs the whole layer).
+        head_first / head_rows: this span's shard of a vocab-parallel lm_head (head_shard());
+        final_norm_out: the model's last span of such a head -- it owns the final norm, and its
+        forward / decode steps write the final-normed last rows, fragment-packed (normed_elems()),
+        to the hidden output instead of the last layer's rows (InferdSpanConfig, ABI 5)."""
         self.dims = dims
         self.first_layer, self.n_layers = first_layer, n_layers
         self.has_embed, self.has_lm_head = has_embed, has_lm_head
@@ -229,6 +234,7 @@ class SpanRuntime:
         self.gateup_split_first, self.gateup_split_last = int(gateup_split_first), int(gateup_split_last)
         self.o_split_first, self.o_split_last = bool(o_split_first), bool(o_split_last)
         self.qkv_split_first, self.qkv_split_last = bool(qkv_split_first), bool(qkv_split_last)
+        self.head_first, self.head_rows, self.final_norm_out = int(head_first), int(head_rows), bool(final_norm_out)
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -237,7 +243,8 @@ class SpanRuntime:
         cfg = [dims.hidden, dims.intermediate, dims.heads, dims.kv_heads, dims.head_dim, dims.vocab, first_layer,
                n_layers, int(has_embed), int(has_lm_head), self.max_positions, kv_pages, max_tokens, max_seqs,
                int(skip_first_attn), int(skip_last_mlp), int(gateup_split_first), int(gateup_split_last),
-               int(o_split_first), int(o_split_last), int(qkv_split_first), int(qkv_split_last)]
+               int(o_split_first), int(o_split_last), int(qkv_split_first), int(qkv_split_last), int(head_first),
+               int(head_rows), int(final_norm_out)]
         self.handle = None
         self.handle = T.span_create(cfg, dims.eps, dims.rope_theta, self.device)
         self.kv = KvTable(kv_pages)
@@ -269,6 +276,17 @@ class SpanRuntime:
         d = self.dims
         return rows * d.hidden + (rows * (d.heads + 2 * d.kv_heads) * d.head_dim if decode else 0)
 
+    def normed_elems(self, rows: int) -> int:
+        """bf16 elements of a final_norm_out span's hand-off: the final-normed last rows,
+        fragment-packed over 16-row tiles (the A operand of every stage's head_shard)."""
+        return (rows + 15) // 16 * 16 * self.dims.hidden
+
+    @property
+    def head_range(self):
+        """(first, rows) of the lm_head rows this span owns: all of them with the whole head,
+        its shard of a vocab-parallel head, or (0, 0)."""
+        return (0, self.dims.vocab) if self.has_lm_head else (self.head_first, self.head_rows)
+
     # ----------------------------------------------------------------- weights
     def _stream(self):
         return torch.cuda.current_stream(self.device)
@@ -281,19 +299,21 @@ class SpanRuntime:
             raise ValueError(f"unknown synthetic profile {profile!r}")
         with torch.cuda.device(self.device):
             T.span_init_synthetic(self.handle, seed, self.device)
-            if profile in PROFILE_BOOST and (self.has_embed or self.has_lm_head):
+            h0, hn = self.head_range
+            if profile in PROFILE_BOOST and (self.has_embed or hn):
                 d = self.dims
                 emb = gen_tensor(seed, GLOBAL_TENSOR_IDS["embed_tokens"], (d.vocab, d.hidden), False,
                                  self.device).float()
                 if self.has_embed:
                     self.set_weight(-1, "embed_tokens", (emb * PROFILE_BOOST[profile]).to(torch.bfloat16))
-                if self.has_lm_head:
+                if hn:     # the whole head or this span's rows of it
                     lm = gen_tensor(seed, GLOBAL_TENSOR_IDS["lm_head"], (d.vocab, d.hidden), False,
                                     self.device).float()
                     perm = (torch.arange(d.vocab, device=self.device, dtype=torch.int64) * PERM_MUL + PERM_ADD) \
                         % d.vocab
                     lm[perm] = lm[perm] + LM_MIX * emb
-                    self.set_weight(-1, "lm_head", lm.to(torch.bfloat16))
+                    self.set_weight(-1, "lm_head", lm[h0:h0 + hn].to(torch.bfloat16).contiguous())
+                    del lm
                 del emb
             self._stream().synchronize()
 
@@ -365,6 +385,16 @@ class SpanRuntime:
         st = self._seq(session_id)
         self.kv.reserve(st.seq, n_tokens)
         return st
+
+    def head_shard(self, normed: torch.Tensor, rows: int, keys_in: torch.Tensor | None = None,
+                   keys_out: torch.Tensor | None = None, ids: torch.Tensor | None = None,
+                   logits: torch.Tensor | None = None):
+        """This span's lm_head rows (head_range) over `rows` final-normed rows (fragment-packed,
+        normed_elems): keys_out int64 [rows] = max(keys_in, each row's (logit, lowest global index)
+        key over the shard), ids int32 [rows] = the greedy token of that key, logits bf16 [rows,
+        head rows] -- every output optional (torch.ops.inferd.span_head_shard; stream ordered, no
+        sync).  Chained over all shards, the ids are argmax over the whole vocabulary."""
+        T.span_head_shard(self.handle, normed, rows, keys_in, keys_out, ids, logits)
 
     @torch.no_grad()
     def lm_head(self, hidden: torch.Tensor) -> torch.Tensor:
@@ -473,6 +503,10 @@ class SpanRuntime:
                 if rec_out:      # h1 then the packed act columns (or x then the attention output)
                     rec = torch.empty(out_rec, dtype=torch.bfloat16, device=dev)
                     hid = rec[:total * d.hidden].view(total, d.hidden)
+                if self.final_norm_out and want_hidden:     # the final-normed last rows (packed)
+                    if len(self._plan(requests)) > 1:
+                        raise ValueError("a final_norm_out span hands over one engine call's normed rows")
+                    hid = torch.zeros(self.normed_elems(B), dtype=torch.bfloat16, device=dev)
                 nid = torch.empty((B,), dtype=torch.int32, device=dev) if (want_next_ids and lm) else None
                 lg = torch.empty((B, d.vocab), dtype=torch.bfloat16, device=dev) if (want_logits and lm) else None
                 lay = torch.empty((self.n_layers, total, d.hidden), dtype=torch.bfloat16, device=dev) \
@@ -511,7 +545,8 @@ class SpanRuntime:
                                                             device=dev) if lay is not None else None)
                     self.run(batch, ids=None if ids_d is None else ids_d[r0:r0 + m],
                              x=None if x_d is None else (x_d if rec_in else x_d[r0:r0 + m]),
-                             hidden=None if hid is None else (rec if rec is not None else hid[r0:r0 + m]),
+                             hidden=None if hid is None else (rec if rec is not None else
+                                                              hid if self.final_norm_out else hid[r0:r0 + m]),
                              next_ids=c_nid, logits=c_lg, layers=c_lay)
                     for i, _, t in call:
                         self.kv.advance(states[i].seq, t)

@@ -730,6 +730,94 @@ def test_q8b_pipeline_token_exact_vs_oracle(tmp_path, sizes, q8b_oracle_greedy):
            masked_checked_steps=masked, tick=last["tick"], steps=steps)
 
 
+def _pipe_vocab_worker(rank, world, port, sizes, out_dir, profile, n_mb, steps):
+    """A pipeline rank with the greedy head vocab-parallel over the stages (bench.py's shard split)."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from inferd_amd.pipeline import PipelineStage
+    from inferd_amd.runtime import MODELS
+    import bench
+    d = MODELS["qwen3-8b"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    ranges = _ranges(sizes)
+    rg = ranges[rank]
+    shards = bench.head_shards(d, ranges, B8X, T8X)
+    st = PipelineStage(d, rank, world, rg.first_layer, rg.n_layers, device=dev, seed=SEED, n_microbatches=n_mb,
+                       batch=B8X, max_ctx=T8X + steps + 8, prefill_chunk=2, profile=profile, sharded_head=True,
+                       head_shard=shards[rank], **rg.span_kwargs())
+    st.prefill([_q8b_exact_prompts()] * n_mb)
+    st.prepare_decode(steps)
+    rec = []
+    st.decode(2, record=rec)
+    st.decode(steps - 2, record=rec)
+    torch.cuda.synchronize()
+    st.span.check_errors()
+    if rank == 0:
+        torch.save({"rec": [(k, m, t.cpu()) for k, m, t in rec], "next": [t.cpu() for t in st.ids],
+                    "shards": shards, "tick": st.tick_stats}, os.path.join(out_dir, "ids.pt"))
+    dist.barrier()
+    st.release()
+    dist.destroy_process_group()
+
+
+def _single_small_worker(port, out_dir, profile, steps):
+    """One 36-layer HIP span (whole head), the same prompts, free-running greedy."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    from inferd_amd.pipeline import PipelineStage
+    from inferd_amd.runtime import MODELS
+    d = MODELS["qwen3-8b"]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    st = PipelineStage(d, 0, 1, 0, d.layers, device=dev, seed=SEED, n_microbatches=1, batch=B8X,
+                       max_ctx=T8X + steps + 8, prefill_chunk=2, profile=profile)
+    st.prefill([_q8b_exact_prompts()])
+    st.prepare_decode(steps)
+    rec = []
+    st.decode(steps, record=rec)
+    torch.cuda.synchronize()
+    torch.save({"rec": [t.cpu() for _, _, t in rec], "next": st.ids[0].cpu()}, os.path.join(out_dir, "single.pt"))
+    st.release()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("profile", ["peaked_deep", "random"])
+def test_q8b_pipeline_vocab_parallel_head(tmp_path, profile, q8b_oracle_greedy):
+    """BASELINE config 3's 8-stage even split with the greedy head vocab-parallel (round 6: the
+    1.24 GB lm_head sharded over the stages by bench.head_shards, the normed rows and running
+    (max, first index) keys handed round the ring, n_mb = 2S + 1 = 17 microbatches): 8 ranks sharing
+    this box's GPU over gloo, real HIP spans.  Every microbatch holds the same prompts, so every id
+    fed to stage 0 must equal (a) a single 36-layer HIP span's free-running greedy ids (whole head)
+    and, on the "peaked_deep" profile, (b) the 36-layer CPU oracle's (q8b_oracle_greedy)."""
+    sizes = [5, 5, 5, 5, 4, 4, 4, 4]
+    world, steps = 8, 6
+    n_mb = 2 * world + 1
+    port = _free_port()
+    _spawn(_pipe_vocab_worker, [(r, world, port, sizes, str(tmp_path), profile, n_mb, steps) for r in range(world)])
+    _spawn(_single_small_worker, [(_free_port(), str(tmp_path), profile, steps)])
+    pipe = torch.load(os.path.join(tmp_path, "ids.pt"), weights_only=True)
+    one = torch.load(os.path.join(tmp_path, "single.pt"), weights_only=True)
+    assert len(pipe["rec"]) == steps * n_mb
+    for k, m, t in pipe["rec"]:
+        assert t.tolist() == one["rec"][k].tolist(), (k, m)
+    assert all(t.tolist() == one["next"].tolist() for t in pipe["next"])
+    if profile == "peaked_deep":
+        ref_ids = q8b_oracle_greedy[0]
+        for k, m, t in pipe["rec"]:
+            assert t.tolist() == ref_ids[k].tolist(), (k, m)
+    print(f"vocab-parallel head, even8, {profile}: {steps} steps x {n_mb} microbatches x {B8X} ids identical to "
+          f"one span{' and the oracle' if profile == 'peaked_deep' else ''}; shards {pipe['shards']}; "
+          f"host {pipe['tick']}")
+    record(f"q8b_pipeline_vocab_head_even8_{profile}", shards=pipe["shards"], microbatches=n_mb, batch=B8X,
+           decode_steps=steps, identical=True, tick=pipe["tick"])
+
+
 # teacher-forced random-profile run: sequences x steps checked where the margin allows.  With
 # plain random weights the oracle's top-1 margins are small (CPU oracle, 4 x 25 pairs: 19 % above
 # 0.5, 7 % above 0.7 logits) and the bf16 oracle is 0.29-0.41 logits (max |.|) from the fp32 one, so

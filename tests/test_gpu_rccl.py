@@ -25,7 +25,7 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 dist.init_process_group("nccl", rank=0, world_size=1, timeout=timedelta(seconds=60), device_id=dev)
 st = types.SimpleNamespace(group=None, rank=0, S=1, device=dev, first_layer=0, n_layers=36,
-                           _exchanged=False, _inflight=None)
+                           _exchanged=False, _inflight=None, _global=lambda r: r)
 g = torch.Generator(device=dev).manual_seed(3)
 ok = True
 # decode ticks: fixed buffers (send h_out / ids_out, receive into h_in / ids)

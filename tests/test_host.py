@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 def test_library_loads_and_reports_version():
     from inferd_amd import _lib
     lib = _lib.load()
-    assert lib.inferd_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.inferd_abi_version() == _lib.ABI_VERSION == 5
     # error path without a GPU: a null config is rejected with a message
     h = _lib.c_p()
     rc = lib.inferd_span_create(None, h)
