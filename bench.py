@@ -543,16 +543,35 @@ def projected_scaling(proj: dict, one_gpu: float) -> dict:
     return out
 
 
+def model_costs(d, B: int = 16, ctx: int = 2048, gbs: float = 5000.0) -> dict:
+    """The split search's time / byte model of a model WITHOUT a measured cost table, from its own
+    dimensions (kernel_bytes at gbs GB/s, the rate the 8B decode kernels average): keyword arguments
+    of pipeline.gateup_split / halves_split (the DECODE_US_8B defaults there are Qwen3-8B's)."""
+    kb = kernel_bytes(d, B, ctx)
+    qkv = kb["rmsnorm"] + kb["qkv_gemm"]
+    attn = qkv + kb["qk_norm_rope_kv"] + kb["attention"] + kb["o_gemm"]
+    mlp = kb["rmsnorm"] + kb["gateup_gemm"] + kb["down_gemm"]
+
+    def us(b):
+        return b / gbs / 1e3
+    return {"costs": {"attn_half": us(attn), "mlp_half": us(mlp), "stage_norm": 5.0,
+                      "head": us(kb["lm_head_argmax"]) + 10.0},
+            "mb": {"attn_half": attn / 1e6, "gateup": kb["gateup_gemm"] / 1e6, "down": kb["down_gemm"] / 1e6,
+                   "head": kb["lm_head_argmax"] / 1e6, "o": kb["o_gemm"] / 1e6, "qkv": qkv / 1e6},
+            "gateup_us": us(kb["gateup_gemm"]), "o_us": us(kb["o_gemm"]), "q_us": us(qkv)}
+
+
 def sub_split(d, n: int, o_cuts: bool):
     """The sub-layer splits (pipeline.gateup_split: gate/up boundaries; o_cuts: attention|o
     boundaries too) on the measured boundary-cost table where one exists for the model
-    (pipeline.measured_split, inferd_amd/data/decode_costs_*.json), else on the kernel-mean model."""
+    (pipeline.measured_split, inferd_amd/data/decode_costs_*.json), else on the model's own
+    byte-derived time model (model_costs; ADVICE r05: not Qwen3-8B's kernel means)."""
     import os
     from inferd_amd import pipeline as P
     name = d.name.replace("-", "_")
     if os.path.exists(os.path.join(os.path.dirname(P.__file__), "data", f"decode_costs_{name}.json")):
         return P.measured_split(d.layers, n, d.intermediate, o_cuts=o_cuts, name=name)
-    return P.gateup_split(d.layers, n, d.intermediate, o_cuts=o_cuts)
+    return P.gateup_split(d.layers, n, d.intermediate, o_cuts=o_cuts, **model_costs(d))
 
 
 # BASELINE config 4: uneven, balance.py-like splits (SURVEY §8(d)), 36-layer models
@@ -582,7 +601,9 @@ def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
         bal = [StageRange.layers(f, k) for f, k in stage_split(d, n, B, ctx, "balanced")]
         if bal != out[f"even{n}"]:
             out[f"balanced{n}"] = bal
-        for name, sp in (("halves", halves_split(d.layers, n)), ("gateup", sub_split(d, n, False)),
+        hs = halves_split(d.layers, n) if d.name == "qwen3-8b" else \
+            halves_split(d.layers, n, model_costs(d, B, ctx)["costs"])
+        for name, sp in (("halves", hs), ("gateup", sub_split(d, n, False)),
                          ("sublayer", sub_split(d, n, True))):
             if all(isinstance(v, dict) or sp != v for v in out.values()):
                 out[f"{name}{n}"] = sp
@@ -943,24 +964,34 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)
             out["cpu_baseline_config1"] = cpu_config1(args.seed)
     if world > 1 and not args.no_sublayer_split and args.split == "even" and not args.spans:
-        # north_star's balanced pipeline beside config 3's even split, same run: the sub-layer split
-        # (every stage >= 60 % of the HBM roofline at the tick by the stage projection)
-        st.release()
-        alt = sub_split(d, world, True)
-        r2 = pipeline_run(d, alt, rank, world, dev, dist, args, profile=False)
-        r2["st"].release()
-        if rank == 0:
-            out["sublayer_split"] = {
-                "value": round(K * r2["n_mb"] * B / r2["elapsed"], 2), "unit": "tokens/s",
-                "ms_per_step": round(r2["elapsed"] / K * 1e3, 4), "stage_ranges": [r.label() for r in alt],
-                "microbatches": r2["n_mb"], "tick_ms": round(r2["elapsed"] / K * 1e3 / r2["n_mb"], 4),
-                "exchange_us_per_tick_rank0": r2["tick"]["exchange_us_per_tick"],
-                "note": "the same workload on pipeline.sublayer_split's stages (measured cost table) with the "
-                        "whole lm_head on the last stage; `value` above is BASELINE config 3's even split"}
+        # beside config 3's even split, same run: equal half-layer stages with the vocab-parallel head
+        # (where the layer count does not divide: the stage projection's best 8-stage split) and
+        # north_star's sub-layer split with the whole head on the last stage
+        alts = []
+        if vhead and (2 * d.layers) % world == 0 and (2 * d.layers // world) % 2:
+            alts.append(("halves_vocab_head", P.ranges_from_sizes([d.layers / world] * world), True,
+                         "equal half-layer stages, greedy head vocab-parallel (shards calibrated per rank)"))
+        alts.append(("sublayer_split", sub_split(d, world, True), False,
+                     "pipeline.sublayer_split's stages (measured cost table), the whole lm_head on the last stage"))
+        for key, alt, vh, note in alts:
+            st.release()
+            cal2 = calibrate_shards(d, alt, rank, world, dev, dist, args) if vh and not args.no_calibrate else None
+            r2 = pipeline_run(d, alt, rank, world, dev, dist, args, profile=False, vhead=vh,
+                              shards=cal2["shards"] if cal2 else None)
+            r2["st"].release()
+            st = r2["st"]
+            if rank == 0:
+                out[key] = {
+                    "value": round(K * r2["n_mb"] * B / r2["elapsed"], 2), "unit": "tokens/s",
+                    "ms_per_step": round(r2["elapsed"] / K * 1e3, 4), "stage_ranges": [r.label() for r in alt],
+                    "head_rows": [n for _, n in r2["shards"]] if r2["shards"] else None,
+                    "microbatches": r2["n_mb"], "tick_ms": round(r2["elapsed"] / K * 1e3 / r2["n_mb"], 4),
+                    "exchange_us_per_tick_rank0": r2["tick"]["exchange_us_per_tick"],
+                    "note": note + "; `value` above is BASELINE config 3's even split"}
     if rank == 0:
         # the driver keeps the tail of stdout: the compact results go last
-        for k in ("stage_projection_summary", "projected_scaling", "sublayer_split", "prefill_config5",
-                  "prefill_config5_b4"):
+        for k in ("stage_projection_summary", "projected_scaling", "sublayer_split", "halves_vocab_head",
+                  "prefill_config5", "prefill_config5_b4"):
             if k in out:
                 v = out.pop(k)
                 if k.startswith("prefill_config5") and v is not None:

@@ -422,6 +422,12 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
     import numpy as np
     tm, by, sa = np.array(times), np.array(byts), np.array(sadj)
     sa_lo = float(sa.min())
+    # stages the engine refuses (inferd_span_create: a one-layer span cannot end before the part it
+    # starts at; StageRange: no stage inside one attention unit, none without a whole unit): two cuts
+    # of one layer where the first is the q/k/v|attention cut and the second the attention|o one, the
+    # first the attention|o cut and the second inside the MLP, or both inside the MLP
+    lay = np.array([c[0] for c in cuts])
+    kq, ko, kg = (np.array([c[1] == k for c in cuts]) for k in ("Q", "O", "G"))
 
     def solve(T):
         """(value, boundary cuts) of the best split with every stage within T (every end cut l of
@@ -443,7 +449,10 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
                 J = j0[:, None] + np.arange(W)[None, :]
                 valid = J < ends[:, None]
                 Jc = np.where(valid, J, 0)
-                ok = valid & ((tm[ends][:, None] - tm[Jc] + sa[Jc] + extra) * scale <= T) & (f[Jc] >= 0)
+                e_ = ends[:, None]
+                same = lay[Jc] == lay[e_]
+                bad = same & ((kq[Jc] & ko[e_]) | (ko[Jc] & kg[e_]) | (kg[Jc] & kg[e_]))
+                ok = valid & ~bad & ((tm[ends][:, None] - tm[Jc] + sa[Jc] + extra) * scale <= T) & (f[Jc] >= 0)
                 v = np.where(ok, np.minimum(f[Jc], (by[ends][:, None] - by[Jc] + (mb["head"] if last else 0.0)) / T),
                              -1.0)
                 k = v.argmax(1)
@@ -466,11 +475,21 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
         v, bb = solve(T)
         if v > best_val:
             best_val, best_b, best_T = v, bb, T
+    T = lo_t * 1.08
+    while best_b is None and T <= times[P] + n * sn + hd + emb + 4.0:
+        # few layers per stage: no cover within 8 % of the ideal tick (the fixed stage costs weigh
+        # more, whole units cannot be shared out); widen the bound until one exists
+        T *= 1.02
+        v, bb = solve(T)
+        if v > best_val:
+            best_val, best_b, best_T = v, bb, T
     for T in np.arange(best_T - 4.0, best_T + 4.0, 1.0):
         v, bb = solve(T)
         if v > best_val:
             best_val, best_b = v, bb
     b = best_b
+    if b is None:
+        raise ValueError(f"no split of {n_layers} layers into {n} stages the engine accepts")
     out = []
     for s in range(n):
         (l0, k0, c0), (l1, k1, c1) = cuts[b[s]], cuts[b[s + 1]]

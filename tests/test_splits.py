@@ -14,10 +14,10 @@ def _cover(ranges, n_layers, intermediate):
     shared by the two stages around the cut); a gate/up column boundary continues exactly where
     the previous stage stopped"""
     u = 0
-    prev_col, prev_o = 0, False
+    prev_col, prev_o, prev_q = 0, False, False
     for i, r in enumerate(ranges):
         assert r.first_unit == u, (i, r)
-        assert r.first_col == prev_col and r.first_o == prev_o, (i, r)
+        assert r.first_col == prev_col and r.first_o == prev_o and r.first_q == prev_q, (i, r)
         assert r.first_col % 128 == 0 and r.last_col % 128 == 0
         assert 0 <= r.first_col < intermediate and 0 <= r.last_col < intermediate
         if r.first_col:
@@ -27,10 +27,15 @@ def _cover(ranges, n_layers, intermediate):
         if r.first_o or r.last_o:      # the engine's constraints (span.hip inferd_span_create)
             assert not (r.first_o and r.skip_first_attn) and not (r.last_o and r.skip_last_mlp)
             assert r.n_layers > 1 or not (r.first_o and (r.last_o or r.skip_last_mlp))
+        if r.n_layers == 1:             # inferd_span_create: a one-layer span cannot end before its start part
+            assert not (r.first_q and r.last_o)
+            assert not (r.first_o and (r.last_o or r.skip_last_mlp))
+            assert not (r.skip_first_attn and (r.last_o or r.last_q))
         u = r.end_unit
-        prev_col, prev_o = r.last_col, r.last_o
-    assert u == 2 * n_layers and prev_col == 0 and not prev_o
+        prev_col, prev_o, prev_q = r.last_col, r.last_o, r.last_q
+    assert u == 2 * n_layers and prev_col == 0 and not prev_o and not prev_q
     assert not ranges[0].first_o and not ranges[-1].last_o
+    assert not ranges[0].first_q and not ranges[-1].last_q
 
 
 @pytest.mark.parametrize("n", [1, 2, 4, 8])
@@ -145,3 +150,25 @@ def test_measured_split_model_reaches_north_star():
     _cover(sub, D8.layers, D8.intermediate)
     assert model(sub) >= 0.60
     assert model(P.measured_split(D8.layers, 8, D8.intermediate, o_cuts=False)) < 0.60
+
+
+@pytest.mark.parametrize("n_layers,n", [(2, 3), (2, 4), (3, 5), (4, 7), (3, 8), (4, 12)])
+def test_sublayer_split_small_models_many_stages(n_layers, n):
+    """with few layers per stage the search must not produce a stage the engine refuses
+    (two cuts inside one layer: attention core alone, o + partial gate/up, a gate/up column range
+    alone).  Every split of a 2-4 layer model into nearly as many stages as cut points is a valid
+    cover, on the kernel-mean model and with q/k/v cuts."""
+    from inferd_amd.runtime import ModelDims
+    d = ModelDims("small", 1024, 3072, 16, 8, n_layers, 151936)
+    made = 0
+    for kw in ({"o_cuts": True}, {"o_cuts": True, "q_cuts": True}, {}):
+        try:
+            ranges = P.gateup_split(n_layers, n, d.intermediate, step=256, **kw)
+        except ValueError:          # no valid split at this many stages: refused, not a bad split
+            continue
+        made += 1
+        assert len(ranges) == n
+        _cover(ranges, n_layers, d.intermediate)
+        for r in ranges:
+            assert r.n_units >= 1 and not ((r.first_q or r.first_o) and (r.last_o or r.last_q) and r.n_units == 1)
+    assert made >= 1
