@@ -338,13 +338,12 @@ class _StageHead:
         self.ids = ids if ids is not None else torch.zeros(B, dtype=torch.int32, device=dev)
 
     def __call__(self):
-        if self.span.head_range[1]:
-            self.span.head_shard(self.normed, self.B, keys_in=None if self.first else self.keys,
+        first, rows = self.span.head_range
+        if rows:
+            self.span.head_shard(self.normed, self.B, keys_in=self.keys if first > 0 else None,
                                  keys_out=None if self.last else self.keys, ids=self.ids if self.last else None)
         elif self.last:
             torch.ops.inferd.argmax_combine(self.keys, 1, self.B, self.ids)
-        elif self.first:
-            self.keys.zero_()
 
 
 def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int, warmup: int = 3,

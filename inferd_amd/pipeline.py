@@ -729,7 +729,8 @@ class PipelineStage:
         sub-layer boundaries (StageRange.span_kwargs(); the hand-offs are records, handoff_elems).
         n_microbatches: >= world (ring_microbatches(world, sharded_head) adds the ring's slack).
         sharded_head / head_shard: the greedy head vocab-parallel over the stages, this stage owning
-        lm_head rows [head_shard[0], head_shard[0] + head_shard[1]) (head_shard_split)."""
+        lm_head rows [head_shard[0], head_shard[0] + head_shard[1]) -- the shards in stage order,
+        contiguous from row 0 (head_shard_split)."""
         assert n_microbatches >= world * (2 if sharded_head and world > 1 else 1), \
             "the ring needs a microbatch per stage in flight (two with a vocab-parallel head)"
         assert not (sharded_head and want_logits), "logits capture needs the whole head on the last stage"
@@ -1017,13 +1018,14 @@ class PipelineStage:
     # ------------------------------------------------------------------ head (vocab-parallel)
     def _head(self, normed, keys_in, keys_out, ids):
         """This stage's lm_head shard over the B normed rows, folded into the running keys (or the
-        ids on the last stage); a stage without rows passes the keys on (stage 0 starts them at 0)."""
+        ids on the last stage).  Shards run in stage order from row 0 (head_shard_split), so the
+        running keys are live iff an earlier stage owns rows (head_first > 0): the first stage with
+        rows starts them, a stage without rows passes the record on untouched."""
+        live = self.head_first > 0
         if self.head_rows:
-            self.ex.head(normed, self.B, keys_in=keys_in, keys_out=keys_out, ids=ids)
+            self.ex.head(normed, self.B, keys_in=keys_in if live else None, keys_out=keys_out, ids=ids)
         elif ids is not None:
             self.ex.combine(keys_in, 1, self.B, ids)
-        elif keys_in is None:
-            keys_out.zero_()
 
     # ------------------------------------------------------------------ prefill
     @torch.no_grad()
