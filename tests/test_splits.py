@@ -172,3 +172,40 @@ def test_sublayer_split_small_models_many_stages(n_layers, n):
         for r in ranges:
             assert r.n_units >= 1 and not ((r.first_q or r.first_o) and (r.last_o or r.last_q) and r.n_units == 1)
     assert made >= 1
+
+
+def test_head_shard_split_levels_the_stages():
+    """pipeline.head_shard_split: shards in stage order, contiguous from row 0, covering the
+    vocabulary in multiples of the step; the stage times it levels stay within one step's cost of
+    each other, and a stage whose layers already exceed the level gets no rows."""
+    V = 151936
+    head_us, fixed = 200.0, 7.0
+    for base in ([500.0] * 8, [530.0, 512, 512, 512, 470, 470, 470, 475], [1900.0, 1910.0], [300.0, 900.0]):
+        sh = P.head_shard_split(base, V, head_us, fixed, 128)
+        assert len(sh) == len(base)
+        f = 0
+        for first, rows in sh:
+            assert first == f and rows % 128 == 0 and rows >= 0
+            f += rows
+        assert f == V
+        t = [b + ((fixed + head_us * r / V) if r else 0.0) for b, (_, r) in zip(base, sh)]
+        owners = [x for x, (_, r) in zip(t, sh) if r]
+        assert max(owners) - min(owners) <= head_us * 128 / V + fixed + 1e-6
+        for b, (_, r) in zip(base, sh):      # nobody with rows ends below a stage without rows
+            if not r:
+                assert b >= min(owners) - 1e-6
+    assert P.head_shard_split([500.0, 500.0], 1024, 10.0, 1.0, 128) == [(0, 512), (512, 512)]
+
+
+def test_ring_tick_and_microbatches():
+    """bench.ring_tick_us: the asynchronous ring's period is the slowest stage unless the summed
+    hand-off latency of a lap exceeds the slack; pipeline.ring_microbatches: S (+S) + slack."""
+    import bench
+    assert P.ring_microbatches(8) == 9 and P.ring_microbatches(8, True) == 17 and P.ring_microbatches(1) == 1
+    c = [500.0] * 8
+    assert bench.ring_tick_us(c, [0.0] * 8, False, 9, 48.0) == 500.0          # 8 x 548 / 9 = 487 < 500
+    assert bench.ring_tick_us(c, [0.0] * 8, False, 8, 48.0) == pytest.approx(548.0)   # no slack: c + x
+    h = [30.0] * 8
+    assert bench.ring_tick_us(c, h, True, 17, 48.0) == 500.0
+    # vocab-parallel head without slack: (n_mb - S) P >= sum(c - h) + h_last + S x
+    assert bench.ring_tick_us(c, h, True, 16, 100.0) == pytest.approx((8 * 470 + 30 + 800) / 8)
