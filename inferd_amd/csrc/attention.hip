@@ -908,8 +908,16 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const u16* __restr
   }
 }
 
+#ifdef ATTN_W64
+// lab builds only (tools/build_w64_lab.sh): the one-wave-per-SIMD body of tools/labsrc/attn_w64.hip
+bool launch_attn_prefill_w64(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale,
+                             u16* out, hipStream_t s);
+#endif
 void launch_attn_prefill(const u16* q, const u16* kv_layer, const AttnBatch& b, int H, int KV, float scale, u16* out,
                          hipStream_t s) {
+#ifdef ATTN_W64
+  if (launch_attn_prefill_w64(q, kv_layer, b, H, KV, scale, out, s)) return;
+#endif
   // 48 query rows per wave; XCD-grouped block order whenever the grid allows it
   const int n = (b.max_q_len + 191) / 192 * H;
   hipLaunchKernelGGL(attn_prefill_kernel<3>, dim3(n, b.B), dim3(256), 0, s, q, kv_layer, b, H, KV, scale * LOG2E, out,
