@@ -67,6 +67,24 @@ constexpr int NA = 42;        // softmax values (of a lane's 64 per page) finish
 constexpr float THR = 8.0f;   // lazy rescale threshold, log2 units (attention.hip RESCALE_THR)
 constexpr int PAGE_BYTES = 32768;
 constexpr int NBUF = 5;  // page j in buffer j % 5: DMA issued 4 pages (2 iterations of slack) ahead
+// W64_CUTS (round 6): the round-4 VALU cuts of attention.hip in this body -- Q
+// prescaled by scale*log2(e) once, the running -m on the first S MFMA's C operand (a per-query VGPR
+// tuple, refreshed when m moves), so a score costs v_exp_f32 + a row-sum add + half a cvt_pk; the
+// fillers are placed by tools/labsrc/w64_sched.py (<= 24 issue cycles per MFMA gap)
+#ifndef W64_CUTS
+#define W64_CUTS 0
+#endif
+#if W64_CUTS
+#if W64_SCHED == 46
+#include "w64_sched_dl46.h"
+#else
+#include "w64_sched.h"
+#endif
+#endif
+#ifndef W64_LACC
+#define W64_LACC 2
+#endif
+constexpr int LACC = W64_LACC;  // row-sum chains per query block
 
 // ---- fixed schedule (global slot g: 0..31 phase A, 32..63 phase B) --------------------------
 // softmax value v of a lane: tile tb = v >> 5, query block nq = (v >> 4) & 1, register v & 15
@@ -105,6 +123,9 @@ constexpr int voff(int kk, int db) { return 16384 + (kk >> 1) * 8192 + db * 2048
 
 __device__ __forceinline__ void mfma_s0(f32x16& d, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "a"(a), "a"(b));
+}
+__device__ __forceinline__ void mfma_sc(f32x16& d, const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(d) : "a"(a), "a"(b), "v"(c));
 }
 __device__ __forceinline__ void mfma_s(f32x16& d, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "a"(a), "a"(b));
@@ -232,7 +253,13 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
     lim[nq] = b.positions[tokrow[nq]];
     const u16* qp = q + ((int64_t)tokrow[nq] * H + h) * HEAD_DIM + 8 * hh;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) qf[nq][c] = *(const bf16x8*)(qp + c * 16);
+    for (int c = 0; c < 8; ++c) {
+      qf[nq][c] = *(const bf16x8*)(qp + c * 16);
+#if W64_CUTS
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[nq][c][j] = (__bf16)((float)qf[nq][c][j] * cl);
+#endif
+    }
   }
 #pragma unroll
   for (int nq = 0; nq < 2; ++nq)
@@ -288,7 +315,12 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
     }
   bf16x8 kr[KR];  // K fragment ring (AGPRs)
   bf16x8 vf[4][4];
-  float lacc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+  float lacc[2][LACC];
+#pragma unroll
+  for (int j = 0; j < LACC; ++j) lacc[0][j] = lacc[1][j] = 0.f;
+#if W64_CUTS
+  f32x16 mc[2];  // -m per query row, the C operand of each score tile's first MFMA
+#endif
   float m[2] = {-INFINITY, -INFINITY}, mnew[2] = {-INFINITY, -INFINITY};
   bool pend = false;
 
@@ -317,23 +349,57 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
       const unsigned u = __float_as_uint(a);
       const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
       a = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      mnew[nq] = fmaxf(m[nq], a * cl);
+      mnew[nq] = fmaxf(m[nq], W64_CUTS ? a : a * cl);
     }
     pend = __builtin_amdgcn_ballot_w64(mnew[0] > m[0] + THR || mnew[1] > m[1] + THR) != 0;
   };
+#if W64_CUTS
+  // the C tuples from m (plain code; the s_nop covers VALU write -> MFMA SrcC read)
+  auto set_mc = [&]() AI {
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) mc[nq][j] = -m[nq];
+    asm volatile("s_nop 4" ::: "memory");
+  };
+  // a score set computed against one m moved to another: x += delta[nq]
+  auto shift_set = [&](f32x16 (&ss)[2][2], float d0, float d1) AI {
+#pragma unroll
+    for (int nq = 0; nq < 2; ++nq) {
+      const float dl = nq ? d1 : d0;
+#pragma unroll
+      for (int tb = 0; tb < 2; ++tb)
+        [&]<int... R>(std::integer_sequence<int, R...>) AI {
+          ([&]() AI {
+            constexpr int rr = R;
+            f32x16& x = ss[nq][tb];
+            const float dd = dl;  // named: a variable used only inside an asm operand is not captured
+            A_ADD(x[rr], dd);
+          }(), ...);
+        }(std::make_integer_sequence<int, 16>{});
+    }
+  };
+#endif
   // apply a pending rescale (O, l at the old max -> new max): plain code, rare
-  auto rescale = [&]() AI {
+  auto rescale = [&]<int CUR>() AI {
     if (!pend) return;
     mfma_drain();
+#if W64_CUTS
+    // page i's scores were taken against the old m: move them with O and l
+    shift_set(s[CUR], m[0] - mnew[0], m[1] - mnew[1]);
+#endif
 #pragma unroll
     for (int nq = 0; nq < 2; ++nq) {
       const float alpha = (m[nq] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m[nq] - mnew[nq]);
-      lacc[nq][0] *= alpha;
-      lacc[nq][1] *= alpha;
+#pragma unroll
+      for (int j = 0; j < LACC; ++j) lacc[nq][j] *= alpha;
 #pragma unroll
       for (int db = 0; db < 4; ++db) o[db][nq] *= alpha;
       m[nq] = mnew[nq];
     }
+#if W64_CUTS
+    set_mc();
+#endif
     asm volatile("s_nop 4" ::: "memory");
     pend = false;
   };
@@ -350,12 +416,18 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
             // named references: a variable used only inside an asm operand is not captured
             f32x16& x = s[CUR][nq][tb];
             u32x4v& pw = pf[nq][tb * 2 + (reg >> 3)];
-            float& la = lacc[nq][reg & 1];
+            float& la = lacc[nq][reg % LACC];
+#if W64_CUTS
+            if constexpr (EXP_SLOT[V] == G) A_EXP(x[reg]);
+            if constexpr (ADD_SLOT[V] == G) A_ADD(la, x[reg]);
+            if constexpr ((V & 1) == 0 && CVT_SLOT[V] == G) A_CVT(pw[(reg & 7) >> 1], x[reg], x[reg + 1]);
+#else
             const float mn = mneg[nq], c2 = cl;
             if constexpr (fslot(V) == G) A_FMA(x[reg], c2, mn);
             if constexpr (fslot(V) + 1 == G) A_EXP(x[reg]);
             if constexpr (fslot(V) + 2 == G) A_ADD(la, x[reg]);
             if constexpr ((V & 1) == 0 && fslot(V + 1) + 3 == G) A_CVT(pw[(reg & 7) >> 1], x[reg], x[reg + 1]);
+#endif
           }(),
           ...);
     }(std::make_integer_sequence<int, 64>{});
@@ -372,7 +444,9 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
             constexpr int f = G >> 1, tb = frag_tb(f), c = frag_c(f), nq = G & 1;
             if constexpr (NEXT) {
               if constexpr (f >= 3 && (G & 1) == 0) lgkm_wait_a<rd_wait(G, kslot(f))>(kr[f % KR]);
-              if constexpr (c == 0)
+              if constexpr (c == 0 && W64_CUTS)
+                mfma_sc(s[NXT][nq][tb], kr[f % KR], qf[nq][c], mc[nq]);
+              else if constexpr (c == 0)
                 mfma_s0(s[NXT][nq][tb], kr[f % KR], qf[nq][c]);
               else
                 mfma_s(s[NXT][nq][tb], kr[f % KR], qf[nq][c]);
@@ -406,8 +480,19 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
               (
                   [&]() AI {
                     constexpr int ch = C, cnq = ch >> 1, ctb = ch & 1;
+#if W64_CUTS
+                    // MAX_SLOT[ch][t] == G for at most one t per chain and slot (the schedule keeps a
+                    // chain's steps in separate slots, so the step index is found by search)
+                    constexpr int t = [] {
+                      for (int u = 0; u < 8; ++u)
+                        if (MAX_SLOT[ch][u] == G) return u;
+                      return -1;
+                    }();
+                    if constexpr (AP_PROBE != 4 && NEXT && t >= 0) {
+#else
                     constexpr int t = (G - 44 - (ch >> 1)) / 2;
                     if constexpr (AP_PROBE != 4 && NEXT && G >= 44 && G < 60 && ((G - 44) & 1) == (ch >> 1) && t >= 0 && t < 8) {
+#endif
                       f32x16& x = s[NXT][cnq][ctb];
                       float& mc = mx[cnq][ctb];
                       if constexpr (t == 0)
@@ -426,8 +511,26 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
               const unsigned u = __float_as_uint(a);
               const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
               a = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-              mnew[cnq] = fmaxf(m[cnq], a * cl);
+              mnew[cnq] = W64_CUTS ? m[cnq] + fmaxf(a, 0.f) : fmaxf(m[cnq], a * cl);
             }
+#if W64_CUTS
+            // the next phase A's C tuples (-m; a rescale in between sets them again)
+            [&]<int... J>(std::integer_sequence<int, J...>) AI {
+              (
+                  [&]() AI {
+                    if constexpr (MOV_SLOT[J] == G) {
+                      f32x16& t = mc[J >> 4];
+                      if constexpr ((J & 15) == 0) {  // the tuple's old value is dead from here
+                        f32x16 dead;
+                        t = dead;
+                      }
+                      const float mn = -m[J >> 4];
+                      asm volatile("v_mov_b32 %0, %1" : "=v"(t[J & 15]) : "v"(mn));
+                    }
+                  }(),
+                  ...);
+            }(std::make_integer_sequence<int, 32>{});
+#endif
             if constexpr (NEXT && G == 62) pend = __builtin_amdgcn_ballot_w64(mnew[0] > m[0] + THR || mnew[1] > m[1] + THR) != 0;
             // LDS reads (a slot's V read before its K read)
             [&]<int... R>(std::integer_sequence<int, R...>) AI {
@@ -504,6 +607,10 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
     m[0] = mnew[0];
     m[1] = mnew[1];
     pend = false;
+#if W64_CUTS
+    shift_set(s[0], -m[0], -m[1]);
+    set_mc();
+#endif
     if (wave_last_page >= 1) read_k(1);
   }
 
@@ -535,7 +642,7 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
     }
     stamp(i, 1);
     if (i > wave_last_page) return;
-    rescale();
+    rescale.template operator()<CUR>();
     stamp(i, 2);
     // one code path for every page (a second register assignment for the wave's last page made
     // hipcc shuffle O between AGPR homes): on the last page the S_{i+1} slots score whatever the
@@ -561,7 +668,9 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_w64_kernel(const u16* __r
   mfma_drain();
 #pragma unroll
   for (int nq = 0; nq < 2; ++nq) {
-    float l = lacc[nq][0] + lacc[nq][1];
+    float l = lacc[nq][0];
+#pragma unroll
+    for (int j = 1; j < LACC; ++j) l += lacc[nq][j];
     const unsigned u = __float_as_uint(l);
     const auto sw = __builtin_amdgcn_permlane32_swap(u, u, false, false);
     l = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
