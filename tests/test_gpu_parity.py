@@ -371,6 +371,66 @@ def test_config5_q32b_layer_prefill_b2_8192_high_pages():
            pages=[min(pages[0]), max(pages[1])])
 
 
+@pytest.mark.timeout(600)
+def test_config5_q32b_stage_8_layers_vs_oracle():
+    """BASELINE config 5 as the stage the bench times (bench.py prefill_bench: Qwen3-32B layers
+    8-15 in ONE span, a prompt prefilled in one call, the same constructor arguments): at T = 1024
+    every row of the stage's output against an 8-layer oracle span in bf16 (the span tolerance)
+    and no further from an fp32 oracle than the bf16 oracle is (NOISE_RATIO on the rms)."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = R.CONFIGS["qwen3-32b"]
+    T, L = 1024, 8
+    s = SpanRuntime(MODELS["qwen3-32b"], 8, L, has_embed=False, has_lm_head=False, kv_pages=T // 64 + 2 + 4,
+                    max_tokens=T, max_seqs=1, max_positions=T + 64, device=DEV)
+    s.init_synthetic(SEED)
+    x = (torch.randn(1, T, d.hidden, generator=torch.Generator().manual_seed(31)) * 0.5).to(torch.bfloat16)
+    out = s.forward([(None, T)], x=x[0], want_hidden=True)["hidden"].cpu()
+    del s
+    ref = R.RefSpan(d, SEED, 8, 8 + L - 1, False, False, torch.bfloat16, "sdpa").forward(x)[0]
+    e = errs(out, ref)
+    ref32 = R.RefSpan(d, SEED, 8, 8 + L - 1, False, False, torch.float32, "sdpa").forward(x.float())[0]
+    e32, noise = errs(out, ref32), errs(ref, ref32)
+    print(f"32B stage 8-15, T={T}: vs bf16 oracle max_norm {e['max_norm']:.2e} rms {e['rms_rel']:.2e}; "
+          f"engine vs fp32 rms {e32['rms_rel']:.2e}, bf16 oracle vs fp32 rms {noise['rms_rel']:.2e}")
+    record("config5_q32b_stage_layers_8_15_T1024", **e, engine_vs_fp32=e32, bf16_ref_vs_fp32=noise)
+    assert span_ok(e), e
+    assert e32["rms_rel"] <= NOISE_RATIO * noise["rms_rel"], (e32, noise)
+
+
+@pytest.mark.timeout(600)
+def test_config5_q32b_stage_8192_equals_chained_layers():
+    """The bench's config-5 stage at its full size (layers 8-15, one 8192-token prompt, one call)
+    against the same eight layers run as eight one-layer spans chained on the host -- each of
+    which is the object test_config5_q32b_layer_prefill_8192 checks against the oracle at this T.
+    The stage must not depend on where the span boundaries lie: bit-identical, or (recorded)
+    within TOL_REL."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["qwen3-32b"]
+    T, L = 8192, 8
+
+    def span(first, n):
+        sp = SpanRuntime(d, first, n, has_embed=False, has_lm_head=False, kv_pages=T // 64 + 2 + 4, max_tokens=T,
+                         max_seqs=1, max_positions=T + 64, device=DEV)
+        sp.init_synthetic(SEED)
+        return sp
+    x = (torch.randn(T, d.hidden, generator=torch.Generator().manual_seed(32)) * 0.5).to(torch.bfloat16).to(DEV)
+    s = span(8, L)
+    whole = s.forward([(None, T)], x=x, want_hidden=True)["hidden"].clone()
+    del s
+    h = x
+    for layer in range(8, 8 + L):
+        s = span(layer, 1)
+        h = s.forward([(None, T)], x=h, want_hidden=True)["hidden"].clone()
+        del s
+    torch.cuda.synchronize()
+    same = torch.equal(whole, h)
+    e = errs(whole.cpu(), h.cpu())
+    print(f"32B stage 8-15 at T={T}: one span vs 8 chained one-layer spans: bit-identical {same}, "
+          f"max_norm {e['max_norm']:.2e}")
+    record("config5_q32b_stage_T8192_vs_chained_layers", bit_identical=same, **e)
+    assert same or e["max_norm"] < TOL_REL, e
+
+
 # ------------------------------------------------------------------ BASELINE configs 3/4 on real spans
 def _free_port():
     so = socket.socket()
@@ -422,13 +482,15 @@ def _pipe_worker(rank, world, port, sizes, out_dir):
     st.prefill(_prompts(world), capture=cap)
     st.prepare_decode(STEPS8)
     rec = []
-    st.decode(STEPS8, record=rec)
+    rl = [] if rank == world - 1 else None
+    st.decode(STEPS8, record=rec, record_logits=rl)
     torch.cuda.synchronize()
     if rank == 0:
         torch.save({"rec": [(k, m, t.cpu()) for k, m, t in rec], "hidden": cap["hidden"]},
                    os.path.join(out_dir, "pipe.pt"))
-    if rank == world - 1:   # sequence 0 of microbatch 0: the last stage's prefill logits
+    if rank == world - 1:   # sequence 0 of microbatch 0: the last stage's prefill and decode logits
         torch.save(cap["logits"][0][0].clone(), os.path.join(out_dir, "logits0.pt"))
+        torch.save([t[0].cpu().clone() for k, m, t in rl if m == 0], os.path.join(out_dir, "dlogits0.pt"))
     dist.barrier()
     st.release()
     dist.destroy_process_group()
@@ -476,15 +538,33 @@ def _spawn(target, args_list):
 @pytest.fixture(scope="module")
 def q8b_prefill_logits_oracle():
     """Sequence 0 of microbatch 0 (2048 tokens) through the 36-layer CPU oracle: its last-row
-    logits in bf16 (the reference's arithmetic) and in fp32 (exact arithmetic, the noise floor)."""
+    logits in bf16 (the reference's arithmetic) and in fp32 (exact arithmetic, the noise floor).
+    out["decode"](ids): the same two oracles continued from that prefill, one cached token per
+    step along the given ids (Qwen3Server.send semantics), each step's last-row logits -- computed
+    once per id sequence (every split feeds the same ids: they are asserted equal to one span's)."""
     d = R.CONFIGS["qwen3-8b"]
     ids = _prompts(1)[0][:1]
-    out = {}
+    out, spans, memo = {}, {}, {}
     for name, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
         sp = R.RefSpan(d, SEED, 0, d.layers - 1, True, True, dt, "sdpa")
         out[name] = sp.forward_cached("p", ids)[0, -1].clone()
-        del sp
-    return out
+        spans[name] = sp
+
+    def decode(step_ids):
+        key = tuple(step_ids)
+        if key not in memo:
+            res = {}
+            for name, sp in spans.items():
+                # a fork of the prefilled session (LayerCache.update concatenates: no aliasing)
+                sp.sessions["d"] = [R.LayerCache(c.k, c.v) for c in sp.sessions["p"]]
+                sp.lengths["d"] = sp.lengths["p"]
+                res[name] = [sp.forward_cached("d", torch.tensor([[t]]))[0, -1].clone() for t in key]
+                del sp.sessions["d"]
+            memo[key] = res
+        return memo[key]
+    out["decode"] = decode
+    yield out
+    spans.clear()
 
 
 @pytest.mark.timeout(1200)
@@ -502,7 +582,9 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     bf16 oracle is (NOISE_RATIO on the rms over the vocabulary; the distance to the bf16 oracle is
     recorded); the first stage boundary's hidden state of sequence 0 is no further from an fp32
     oracle than the bf16 oracle is, and (boundaries up to 9 layers deep, sequences 0 and 1) is
-    within the span tolerance of the bf16 oracle.  Checked against a single 36-layer HIP span: the greedy ids fed back to stage 0."""
+    within the span tolerance of the bf16 oracle; the last stage's logits of every decode step (sequence
+    0) obey the same noise-floor rule against the oracle continued along the fed ids.  Checked
+    against a single 36-layer HIP span: the greedy ids fed back to stage 0."""
     world = len(_ranges(sizes))
     port = _free_port()
     _spawn(_pipe_worker, [(r, world, port, sizes, str(tmp_path)) for r in range(world)])
@@ -548,9 +630,30 @@ def test_q8b_pipeline_b16_ctx2048_vs_single_span(tmp_path, sizes, q8b_prefill_lo
     # after 36 random-weight layers the bf16 oracle itself is ~6 % (rms) from fp32 arithmetic on
     # these logits (CPU measurement), so the assertion is the noise-floor rule, not a span tolerance
     assert lratio <= NOISE_RATIO, lnoise
+    # the decode steps of sequence 0 (microbatch 0) against the oracle continued from its prefill
+    # along the ids the pipeline fed: every step's last-stage logits obey the same noise-floor rule,
+    # and whether each fed-back id is the oracle's own greedy choice is recorded
+    fed = [t[0] for k, m, t in got if m == 0]
+    dl = torch.load(os.path.join(tmp_path, "dlogits0.pt"), weights_only=True)
+    assert len(dl) == STEPS8 == len(fed)
+    od = q8b_prefill_logits_oracle["decode"](fed)
+    dsteps = []
+    for k in range(STEPS8):
+        n16, n32 = errs(dl[k], od["bf16"][k]), errs(dl[k], od["fp32"][k])
+        floor = errs(od["bf16"][k], od["fp32"][k])
+        ratio = n32["rms_rel"] / max(floor["rms_rel"], 1e-12)
+        nxt = fed[k + 1] if k + 1 < STEPS8 else int(torch.argmax(dl[k].float()))
+        dsteps.append({"vs_bf16": n16, "noise_ratio": ratio, "engine_id": nxt,
+                       "oracle_id": int(torch.argmax(od["bf16"][k].float())),
+                       "oracle_margin": R.top2_margin(od["bf16"][k].float())})
+    print(f"{sizes}: decode logits (seq 0, {STEPS8} steps after the 2048-token prefill) vs bf16 oracle rms "
+          f"{[round(x['vs_bf16']['rms_rel'], 4) for x in dsteps]}; fp32 noise ratios "
+          f"{[round(x['noise_ratio'], 2) for x in dsteps]}; ids = oracle greedy "
+          f"{[x['engine_id'] == x['oracle_id'] for x in dsteps]}")
+    assert all(x["noise_ratio"] <= NOISE_RATIO for x in dsteps), dsteps
     record(f"q8b_pipeline_{_tag(sizes)}", ids_identical=True, decode_steps=STEPS8,
            microbatches=world, boundary_err=e, noise_floor=noise, last_stage_prefill_logits=el,
-           last_stage_logits_noise=lnoise, last_stage_logits_noise_ratio=lratio)
+           last_stage_logits_noise=lnoise, last_stage_logits_noise_ratio=lratio, decode_vs_oracle=dsteps)
 
 
 # ------------------------------------------------------------------ north star: 8B token-exact through the pipeline
