@@ -715,6 +715,24 @@ def cpu_config1(seed: int, steps: int = 16) -> dict:
 
 
 # ------------------------------------------------------------------ main
+CAL_CLIP = 0.05    # calibrate_shards: measured / predicted stage time clipped to 1 -+ this
+
+
+def clip_calibration(measured, predicted, clip: float = CAL_CLIP):
+    """The per-rank stage times the shards are sized on: each measurement trusted within `clip` of
+    the cost model (device spread 1-3 % plus the 2 % re-measurement noise fit well inside), so one
+    outlier -- a rank whose timing overlapped something else -- cannot hand it the whole
+    vocabulary.  Returns (times used, ranks clipped)."""
+    used, clipped = [], []
+    for r, (m, p) in enumerate(zip(measured, predicted)):
+        ratio = m / p if (m > 0 and p > 0 and m == m) else 1.0
+        c = min(max(ratio, 1.0 - clip), 1.0 + clip)
+        if c != ratio:
+            clipped.append(r)
+        used.append(p * c)
+    return used, clipped
+
+
 def calibrate_shards(d, ranges, rank: int, world: int, dev, dist, args) -> dict:
     """Per-rank calibration before the pipeline is built (vocab-parallel head): every rank times
     its own stage's layers alone (stage_ms with its real role, the whole head excluded) on its own
@@ -733,8 +751,10 @@ def calibrate_shards(d, ranges, rank: int, world: int, dev, dist, args) -> dict:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     us = [float(v) for v in t.cpu()]
     pred, _ = stage_base_us(d, ranges, args.batch, args.ctx)
+    used, clipped = clip_calibration(us, pred)
     return {"stage_us": [round(v, 1) for v in us], "predicted_us": [round(v, 1) for v in pred],
-            "shards": head_shards(d, ranges, args.batch, args.ctx, stage_us=us)}
+            "used_us": [round(v, 1) for v in used], "clipped_ranks": clipped,
+            "shards": head_shards(d, ranges, args.batch, args.ctx, stage_us=used)}
 
 
 def pipeline_run(d, ranges, rank: int, world: int, dev, dist, args, profile: bool = True, vhead: bool = False,

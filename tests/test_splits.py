@@ -209,3 +209,28 @@ def test_ring_tick_and_microbatches():
     assert bench.ring_tick_us(c, h, True, 17, 48.0) == 500.0
     # vocab-parallel head without slack: (n_mb - S) P >= sum(c - h) + h_last + S x
     assert bench.ring_tick_us(c, h, True, 16, 100.0) == pytest.approx((8 * 470 + 30 + 800) / 8)
+
+
+def test_calibration_clipped_to_the_cost_model():
+    """bench.clip_calibration: a rank's measured stage time moves its shard only within CAL_CLIP
+    of the cost model -- the shared-GPU gloo rehearsal measured [2629, 827, 1291, 1204] us against
+    ~920 us predicted and handed one stage the whole vocabulary; clipped, every stage keeps rows
+    inside the band a faster GPU still takes more."""
+    import bench
+    from inferd_amd.pipeline import ranges_from_sizes
+    from inferd_amd.runtime import MODELS
+    d = MODELS["qwen3-8b"]
+    ranges = ranges_from_sizes([9, 9, 9, 9])
+    pred, _ = bench.stage_base_us(d, ranges, 16, 2048)
+    used, clipped = bench.clip_calibration([2629.0, 826.6, 1290.5, 1204.0], pred)
+    assert clipped == [0, 1, 2, 3]
+    assert all(abs(u / p - 1) <= bench.CAL_CLIP + 1e-9 for u, p in zip(used, pred))
+    sh = bench.head_shards(d, ranges, 16, 2048, stage_us=used)
+    print([n for _, n in sh])
+    assert sum(n for _, n in sh) == d.vocab and max(n for _, n in sh) < 0.75 * d.vocab
+    assert sum(1 for _, n in sh if n) >= 2
+    # inside the band a measurement is used as measured
+    m = [p * f for p, f in zip(pred, (1.02, 0.99, 1.0, 0.97))]
+    used, clipped = bench.clip_calibration(m, pred)
+    assert clipped == [] and used == m
+    assert bench.clip_calibration([float("nan"), 0.0], [500.0, 400.0]) == ([500.0, 400.0], [])
