@@ -155,6 +155,13 @@ int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out);
 void inferd_span_destroy(InferdSpan* span);
 /* the configuration the span was created with (hosts size their buffers from it) */
 int inferd_span_get_config(const InferdSpan* span, InferdSpanConfig* out);
+/* bf16 elements the x_in (which = 0) / x_out (which = 1) buffer of a forward or step call of
+ * n_tokens rows over n_seqs sequences (decode: a pure decode call) must hold: the hidden rows plus
+ * the record a sub-layer boundary hands over, or a final_norm_out span's normed rows.  A pure
+ * function of the config (no span needed); -1 on bad arguments.  inferd_span_forward and
+ * inferd_span_step take plain pointers and cannot check sizes: size the buffers with this. */
+int64_t inferd_span_io_elems(const InferdSpanConfig* cfg, int32_t n_tokens, int32_t n_seqs, int32_t decode,
+                             int32_t which);
 
 /* Fill every weight of the span from the counter-based generator (oracle/weightgen.py
  * defines the same values) -- the offline stand-in for the HF checkpoint. */

@@ -52,6 +52,7 @@ SIGNATURES = {
     "inferd_span_profile_start": (C.c_int, [c_p, c_i32]),
     "inferd_span_profile_stop": (C.c_int, [c_p, C.POINTER(C.c_double), C.POINTER(c_i32), c_i32]),
     "inferd_span_lm_head": (C.c_int, [c_p, c_p, c_i32, c_p, c_p]),
+    "inferd_span_io_elems": (C.c_int64, [c_p, c_i32, c_i32, c_i32, c_i32]),
     "inferd_span_head_shard": (C.c_int, [c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "inferd_argmax_combine": (C.c_int, [c_p, c_i32, c_i32, c_p, c_p]),
     "inferd_span_graph_capture": (C.c_int, [c_p, C.POINTER(Batch), c_i32, c_p, c_p, c_p, c_p, c_p, c_p,

@@ -318,6 +318,30 @@ extern "C" int inferd_span_create(const InferdSpanConfig* cfg, InferdSpan** out)
 
 extern "C" void inferd_span_destroy(InferdSpan* span) { delete span; }
 
+// bf16 elements of a forward / step call's x_in (which = 0) or x_out (which = 1): the hidden rows
+// plus the record a sub-layer boundary carries (gate/up: the packed act over 16-row tiles in calls
+// of <= 64 rows; attention|o: the attention output, 16-row tiles in pure decode calls; q/k/v|
+// attention: the raw q/k/v rows in pure decode calls), or a final_norm_out span's normed last rows
+// over 16-row tiles.  A pure function of the config: hosts size buffers before they create a span.
+extern "C" int64_t inferd_span_io_elems(const InferdSpanConfig* c, int32_t n_tokens, int32_t n_seqs, int32_t decode,
+                                        int32_t which) {
+  if (!c || n_tokens < 0 || n_seqs < 0 || (which != 0 && which != 1)) {
+    g_err = "inferd_span_io_elems: a config, n_tokens / n_seqs >= 0 and which 0 (x_in) or 1 (x_out)";
+    return -1;
+  }
+  const int64_t M = n_tokens, h = c->hidden;
+  const bool gemv = M <= 64;
+  const int64_t rec = (M + 15) / 16 * 16 * (int64_t)c->intermediate;
+  const int64_t orec = (decode && gemv ? (M + 15) / 16 * 16 : M) * (int64_t)c->heads * c->head_dim;
+  const int64_t qrec = decode ? M * (int64_t)(c->heads + 2 * c->kv_heads) * c->head_dim : 0;
+  if (which == 0)
+    return M * h + (gemv && c->gateup_split_first ? rec : 0) + (c->o_split_first ? orec : 0) +
+           (c->qkv_split_first ? qrec : 0);
+  if (c->final_norm_out) return ((int64_t)n_seqs + 15) / 16 * 16 * h;
+  return M * h + (gemv && c->gateup_split_last ? rec : 0) + (c->o_split_last ? orec : 0) +
+         (c->qkv_split_last ? qrec : 0);
+}
+
 extern "C" int inferd_span_get_config(const InferdSpan* span, InferdSpanConfig* out) {
   if (!span || !out) return fail(INFERD_ERR_ARG, "null argument");
   *out = span->cfg;

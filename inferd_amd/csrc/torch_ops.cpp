@@ -77,24 +77,11 @@ void check_forward_args(const InferdSpanConfig& c, const at::Tensor& words, cons
   TORCH_CHECK(!c.has_embed || ids, "a first span needs ids");
   TORCH_CHECK(c.has_embed || x, "a span without the embedding needs x");
   TORCH_CHECK(c.has_lm_head || (!next_ids && !logits), "next_ids / logits need a span with lm_head");
-  // decode calls across a gate/up boundary hand over a record: h1 then the packed act
-  const int64_t rec = (M + 15) / 16 * 16 * (int64_t)c.intermediate;
-  const bool dec = M <= 64;
   check_arg(ids, dev, at::kInt, M, "ids");
-  // attention|o boundaries: x then the attention output (16-row tiles in a pure decode call)
-  const int64_t orec = (b.decode && dec ? (M + 15) / 16 * 16 : M) * (int64_t)c.heads * c.head_dim;
-  // q/k/v|attention boundaries: x then the raw q/k/v rows (pure decode calls; else x only)
-  const int64_t qrec = b.decode ? M * (int64_t)(c.heads + 2 * c.kv_heads) * c.head_dim : 0;
-  check_arg(x, dev, at::kBFloat16,
-            M * h + (dec && c.gateup_split_first ? rec : 0) + (c.o_split_first ? orec : 0) +
-                (c.qkv_split_first ? qrec : 0),
-            "x");
-  // a final_norm_out span's x_out: the final-normed last rows, fragment-packed over 16-row tiles
-  check_arg(x_out, dev, at::kBFloat16,
-            c.final_norm_out ? (B + 15) / 16 * 16 * h
-                             : M * h + (dec && c.gateup_split_last ? rec : 0) + (c.o_split_last ? orec : 0) +
-                                   (c.qkv_split_last ? qrec : 0),
-            "x_out");
+  // x / x_out: the hidden rows plus a sub-layer boundary's record, or a final_norm_out span's
+  // normed rows (the C-ABI's own size rule, inferd_span_io_elems)
+  check_arg(x, dev, at::kBFloat16, inferd_span_io_elems(&c, (int32_t)M, (int32_t)B, b.decode, 0), "x");
+  check_arg(x_out, dev, at::kBFloat16, inferd_span_io_elems(&c, (int32_t)M, (int32_t)B, b.decode, 1), "x_out");
   check_arg(next_ids, dev, at::kInt, B, "next_ids");
   check_arg(logits, dev, at::kBFloat16, B * (int64_t)c.vocab, "logits");
   check_arg(layers, dev, at::kBFloat16, (int64_t)c.n_layers * M * h, "layers");

@@ -41,6 +41,33 @@ def test_library_loads_and_reports_version():
     assert rc == 1 and b"null" in lib.inferd_last_error()
 
 
+def test_io_elems_matches_the_pipeline_record_sizes():
+    """inferd_span_io_elems (the C-ABI's buffer-size rule, a pure function of the config; no GPU)
+    agrees with the host's hand-off sizes (pipeline.buffer_elems) at every boundary kind and with
+    the final_norm_out rows, for prefill, gemv-sized and decode calls."""
+    from inferd_amd import _lib
+    from inferd_amd.pipeline import buffer_elems
+    from inferd_amd.runtime import MODELS
+    lib = _lib.load()
+    d = MODELS["qwen3-8b"]
+    base = dict(hidden=d.hidden, intermediate=d.intermediate, heads=d.heads, kv_heads=d.kv_heads,
+                head_dim=d.head_dim, vocab=d.vocab, first_layer=0, n_layers=2, max_seqs=16)
+    kinds = {"layer": {}, "gateup": dict(gateup_split_first=4096, gateup_split_last=4096),
+             "o": dict(o_split_first=1, o_split_last=1), "q": dict(qkv_split_first=1, qkv_split_last=1)}
+    for kind, kw in kinds.items():
+        cfg = _lib.SpanConfig(**base, **kw)
+        for rows, decode in ((1, 1), (5, 1), (16, 1), (48, 0), (64, 0), (65, 0), (300, 0)):
+            want = buffer_elems(d, rows, 4096 if kind == "gateup" else 0, kind == "o", bool(decode), kind == "q")
+            for which in (0, 1):
+                got = lib.inferd_span_io_elems(ctypes.byref(cfg), rows, rows if decode else 1, decode, which)
+                assert got == want, (kind, rows, decode, which, got, want)
+    cfg = _lib.SpanConfig(**base, final_norm_out=1)
+    assert lib.inferd_span_io_elems(ctypes.byref(cfg), 5, 5, 1, 1) == 16 * d.hidden
+    assert lib.inferd_span_io_elems(ctypes.byref(cfg), 5, 5, 1, 0) == 5 * d.hidden
+    assert lib.inferd_span_io_elems(None, 5, 5, 1, 0) == -1 and b"io_elems" in lib.inferd_last_error()
+    assert lib.inferd_span_io_elems(ctypes.byref(cfg), 5, 5, 1, 2) == -1
+
+
 def test_codec_matches_reference_fixture():
     from inferd_amd.partitioned_models import base64_to_tensor, build_decoder_attention_mask, tensor_to_base64
     g = json.load(open(os.path.join(GOLDEN, "codec.json")))
