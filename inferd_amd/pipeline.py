@@ -1227,7 +1227,7 @@ class PipelineStage:
             if self.sharded and 0 <= j < n_items:
                 mj = j % n_mb
                 tx = time.perf_counter()
-                rec = link.need(("n", j) if self.first else ("k", j))
+                link.need(("n", j) if self.first else ("k", j))     # lands in head_rec[mj]
                 t_x += time.perf_counter() - tx
                 rec = self.head_rec[mj]
                 if self.last:
