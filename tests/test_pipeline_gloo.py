@@ -154,7 +154,8 @@ def _forced(n_mb, n_steps, vocab):
 # vocab-parallel head shards of the tiny model (vocab 1024) per world size: (first, rows) per stage;
 # a stage may own none (it passes the running keys on)
 HEAD_SHARDS = {2: [(0, 384), (384, 640)], 3: [(0, 256), (256, 0), (256, 768)], 4: [(0, 0), (0, 512), (512, 256),
-                                                                                  (768, 256)]}
+                                                                                  (768, 256)],
+               8: [(0, 0), (0, 0), (0, 128), (128, 128), (256, 256), (512, 128), (640, 256), (896, 128)]}
 
 
 def _worker(rank, world, port, n_steps, q, sizes=None, force=False, n_mb=None, sharded=False):
@@ -273,6 +274,20 @@ def test_pipeline_vocab_parallel_head(world, sizes, extra):
     torch.argmax over the whole vocabulary, bit for bit, at n_mb = 2S + extra microbatches."""
     n_steps, n_mb = 4, 2 * world + extra
     _check(_run_ring(world, n_steps, sizes, n_mb=n_mb, sharded=True), _reference(n_mb, n_steps, sizes), n_steps,
+           n_mb)
+
+
+@pytest.mark.parametrize("sharded", [False, True], ids=["whole_head", "vocab_head"])
+def test_pipeline_eight_stages(sharded):
+    """bench.py --gpus 8's ring on CPU ranks: the tiny model's 4 layers as eight half-layer stages
+    (attention half | MLP half), S + 1 = 9 microbatches with the whole head, 2S + 1 = 17 with the
+    vocab-parallel head (the first two stages owning no rows, so the running keys start on stage
+    2): ids identical to one span."""
+    from inferd_amd.pipeline import ring_microbatches
+    world, n_steps, sizes = 8, 3, [0.5] * 8
+    n_mb = ring_microbatches(world, sharded)
+    assert n_mb == (17 if sharded else 9)
+    _check(_run_ring(world, n_steps, sizes, n_mb=n_mb, sharded=sharded), _reference(n_mb, n_steps, sizes), n_steps,
            n_mb)
 
 
