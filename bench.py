@@ -568,7 +568,20 @@ def model_costs(d, B: int = 16, ctx: int = 2048, gbs: float = 5000.0) -> dict:
             "gateup_us": us(kb["gateup_gemm"]), "o_us": us(kb["o_gemm"]), "q_us": us(qkv)}
 
 
-def sub_split(d, n: int, o_cuts: bool):
+def vhead_params(d, B: int = 16, ctx: int = 2048) -> dict:
+    """gateup_split's vhead argument: the vocab-parallel head's per-row and fixed costs as
+    head_shards prices them"""
+    from inferd_amd import pipeline as P
+    name = d.name.replace("-", "_")
+    if os.path.exists(os.path.join(os.path.dirname(P.__file__), "data", f"decode_costs_{name}.json")):
+        head_us = P.load_decode_costs(name)["head"] - FINAL_NORM_US
+    else:
+        head_us = d.vocab * d.hidden * 2 / 5e3
+    return {"vocab": d.vocab, "row_mb": d.hidden * 2 / 1e6, "head_us": head_us, "fixed_us": HEAD_SHARD_FIXED_US,
+            "norm_us": FINAL_NORM_US, "step": 128 if d.vocab % 128 == 0 else 16}
+
+
+def sub_split(d, n: int, o_cuts: bool, vhead: bool = False):
     """The sub-layer splits (pipeline.gateup_split: gate/up boundaries; o_cuts: attention|o
     boundaries too) on the measured boundary-cost table where one exists for the model
     (pipeline.measured_split, inferd_amd/data/decode_costs_*.json), else on the model's own
@@ -576,13 +589,49 @@ def sub_split(d, n: int, o_cuts: bool):
     import os
     from inferd_amd import pipeline as P
     name = d.name.replace("-", "_")
+    vh = vhead_params(d) if vhead else None
     if os.path.exists(os.path.join(os.path.dirname(P.__file__), "data", f"decode_costs_{name}.json")):
-        return P.measured_split(d.layers, n, d.intermediate, o_cuts=o_cuts, name=name)
-    return P.gateup_split(d.layers, n, d.intermediate, o_cuts=o_cuts, **model_costs(d))
+        return P.measured_split(d.layers, n, d.intermediate, o_cuts=o_cuts, name=name, vhead=vh)
+    return P.gateup_split(d.layers, n, d.intermediate, o_cuts=o_cuts, vhead=vh, **model_costs(d))
 
 
 # BASELINE config 4: uneven, balance.py-like splits, 36-layer models
 CONFIG4_SPLITS = {3: [5, 27, 4], 4: [6, 12, 12, 6], 8: [2, 3, 5, 6, 6, 6, 5, 3]}
+
+
+def vhead_best_split(d, n: int, B: int, ctx: int, spread: int = 2):
+    """Half-layer stage sizes for the vocab-parallel head chosen on the cost model: every way to
+    give the n stages 2L/n +- `spread` half-layer units (summing to the model's 2L) is priced with
+    stage_base_us, the head shards water-filled on top (head_shards), and the sizes whose lowest
+    stage has the largest share of 8 TB/s at the resulting tick win.  Stages of slow bytes (the
+    embedding stage, attention-heavy ones) take fewer layer units and more lm_head rows, which
+    stream faster than a layer's mix of kernels.  Returns (ranges, predicted lowest fraction)."""
+    import itertools
+    from inferd_amd.pipeline import ranges_from_sizes
+    total, mean = 2 * d.layers, 2 * d.layers / n
+    lo, hi = max(1, int(mean) - spread), int(mean + 0.999) + spread
+    base_cache = {}
+    best = (None, -1.0)
+    per_row = None
+    for sz in itertools.product(range(lo, hi + 1), repeat=n - 1):
+        last = total - sum(sz)
+        if not lo <= last <= hi:
+            continue
+        sizes = [h / 2 for h in sz + (last,)]
+        ranges = ranges_from_sizes(sizes)
+        key = tuple(sizes)
+        base, head_us = stage_base_us(d, ranges, B, ctx)
+        if per_row is None:
+            per_row = head_us / d.vocab
+        shards = head_shards(d, ranges, B, ctx)
+        t = [b + (HEAD_SHARD_FIXED_US + per_row * r if r else 0.0) for b, (_, r) in zip(base, shards)]
+        tick = max(t)
+        nb = [range_bytes(d, r, B, ctx, False) + rows * d.hidden * 2 for r, (_, rows) in zip(ranges, shards)]
+        frac = min(nb) / (tick * 1e-6) / 1e9 / HBM_PEAK_GBS
+        base_cache[key] = frac
+        if frac > best[1]:
+            best = (ranges, frac)
+    return best
 
 
 def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
@@ -598,6 +647,9 @@ def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
                                  "vhead": True}
         if (2 * d.layers) % n == 0 and (2 * d.layers // n) % 2:
             out[f"vhead_halves{n}"] = {"ranges": ranges_from_sizes([d.layers / n] * n), "vhead": True}
+        # sub-layer cuts chosen for the vocab-parallel head (gateup_split(vhead=...)): stages whose
+        # layer bytes run slow give them up for lm_head rows
+        out[f"vhead_sublayer{n}"] = {"ranges": sub_split(d, n, True, vhead=True), "vhead": True}
     if d.layers == 36:
         for n, sp in CONFIG4_SPLITS.items():
             out[f"config4_uneven{n}"] = ranges_from_sizes(sp)

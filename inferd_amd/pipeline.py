@@ -340,7 +340,7 @@ def apply_cost_fit(c: dict) -> dict:
 def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_US_8B, step: int = 256,
                  gateup_us: float = DECODE_US_8B_GATEUP, mb: dict = DECODE_MB_8B, o_cuts: bool = False,
                  o_us: float = DECODE_US_8B_O, cal: dict | None = None, q_cuts: bool = False,
-                 q_us: float = DECODE_US_8B_QKV):
+                 q_us: float = DECODE_US_8B_QKV, vhead: dict | None = None):
     """Stages cut anywhere in the layer timeline a boundary may sit -- a layer start, or inside
     a layer's MLP before gate/up column c (c = 0: the half boundary; 0 < c < intermediate, a
     multiple of `step`: a gate/up boundary), and with o_cuts also between a layer's attention
@@ -358,7 +358,16 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
     in (o + MLP: cal["o_mlp"]; the MLP from gate/up column c: cal["mlp"][c]) + the part of the
     layer it ends in (the attention core: cal["core"]; the attention half + gate/up columns
     [0, c): cal["send"][c]) + head / embedding -- which prices what a boundary really costs
-    (the partial gate/up GEMV's wave quantisation, the extra launches)."""
+    (the partial gate/up GEMV's wave quantisation, the extra launches).
+
+    vhead (the greedy head vocab-parallel, PipelineStage(sharded_head=True)): {"vocab", "row_mb"
+    (one lm_head row, MB), "head_us" (the whole head's GEMV without the final norm), "fixed_us" (a
+    shard's fixed cost), "norm_us" (the last stage's final norm), "step" (rows per shard step)}.
+    The last stage then ends with the final norm, and every stage takes the lm_head rows that fill
+    it up to the tick (water-filling, head_shard_split): for a tick T a stage's value is its bytes
+    plus the rows (T - t - fixed) / per-row cost would stream, over T -- layer bytes that run slower
+    than the head's GEMV are what a stage gives up to another; each candidate split is then priced
+    with its real water-filled shards (every row placed once) and the best of those kept."""
     a, mlp, hd, sn = costs["attn_half"], costs["mlp_half"], costs["head"], costs["stage_norm"]
     ncol = intermediate // step
     emb, fs = 0.0, 1.0
@@ -429,6 +438,23 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
     lay = np.array([c[0] for c in cuts])
     kq, ko, kg = (np.array([c[1] == k for c in cuts]) for k in ("Q", "O", "G"))
 
+    if vhead is not None:
+        per_row = vhead["head_us"] / vhead["vocab"]
+        hd = vhead["norm_us"]                    # the last stage's own extra: the final norm
+        mb = dict(mb, head=0.0)
+
+    def stage_time(s, j, l):
+        extra = sn + (hd if s == n - 1 else 0.0) + (emb if s == 0 else 0.0)
+        return (tm[l] - tm[j] + sa[j] + extra) * (fs if s == 0 else 1.0)
+
+    def real_value(b):
+        """a split's lowest stage share at its tick with the shards water-filled (vhead)"""
+        ts = [stage_time(s, b[s], b[s + 1]) for s in range(n)]
+        rows = [r for _, r in head_shard_split(ts, vhead["vocab"], vhead["head_us"], vhead["fixed_us"],
+                                               vhead["step"])]
+        tick = max(t + (vhead["fixed_us"] + per_row * r if r else 0.0) for t, r in zip(ts, rows))
+        return min(by[b[s + 1]] - by[b[s]] + rows[s] * vhead["row_mb"] for s in range(n)) / tick
+
     def solve(T):
         """(value, boundary cuts) of the best split with every stage within T (every end cut l of
         a stage at once: a [ends, window] matrix of its candidate start cuts j, ascending, so
@@ -452,9 +478,12 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
                 e_ = ends[:, None]
                 same = lay[Jc] == lay[e_]
                 bad = same & ((kq[Jc] & ko[e_]) | (ko[Jc] & kg[e_]) | (kg[Jc] & kg[e_]))
-                ok = valid & ~bad & ((tm[ends][:, None] - tm[Jc] + sa[Jc] + extra) * scale <= T) & (f[Jc] >= 0)
-                v = np.where(ok, np.minimum(f[Jc], (by[ends][:, None] - by[Jc] + (mb["head"] if last else 0.0)) / T),
-                             -1.0)
+                tst = (tm[ends][:, None] - tm[Jc] + sa[Jc] + extra) * scale
+                ok = valid & ~bad & (tst <= T) & (f[Jc] >= 0)
+                stage_mb = by[ends][:, None] - by[Jc] + (mb["head"] if last else 0.0)
+                if vhead is not None:      # + the rows that fill the stage up to T
+                    stage_mb = stage_mb + np.maximum(0.0, (T - tst - vhead["fixed_us"]) / per_row) * vhead["row_mb"]
+                v = np.where(ok, np.minimum(f[Jc], stage_mb / T), -1.0)
                 k = v.argmax(1)
                 r = np.arange(len(ends))
                 g[ends] = v[r, k]
@@ -470,6 +499,13 @@ def gateup_split(n_layers: int, n: int, intermediate: int, costs: dict = DECODE_
         return float(f[P]), b[::-1]
     # the tick: coarse grid from the ideal (total / n), then refined around the best
     lo_t = (times[P] + n * sn + hd + emb) / n
+    if vhead is not None:     # the level every stage is filled to: the layers plus the whole head
+        lo_t = (times[P] + n * sn + hd + emb + vhead["head_us"] + n * vhead["fixed_us"]) / n * 0.97
+        _solve = solve
+
+        def solve(T):       # noqa: F811 -- each T's split priced by its real water-filled shards
+            v, bb = _solve(T)
+            return (real_value(bb), bb) if bb is not None else (v, bb)
     best_val, best_b, best_T = -1.0, None, lo_t
     for T in np.arange(lo_t, lo_t * 1.08, 4.0):
         v, bb = solve(T)

@@ -234,3 +234,27 @@ def test_calibration_clipped_to_the_cost_model():
     used, clipped = bench.clip_calibration(m, pred)
     assert clipped == [] and used == m
     assert bench.clip_calibration([float("nan"), 0.0], [500.0, 400.0]) == ([500.0, 400.0], [])
+
+
+def test_vhead_sublayer_split_covers_and_beats_equal_halves():
+    """gateup_split(vhead=...) (bench.sub_split(vhead=True)): for the vocab-parallel head the sub-layer
+    cuts are chosen with the lm_head rows filling every stage to the tick -- the split covers every
+    unit once with cuts the engine accepts, and on the cost model its lowest stage share is at
+    least that of the equal half-layer stages (vhead_halves8) at 8 stages."""
+    import bench
+    from inferd_amd.pipeline import ranges_from_sizes
+    from inferd_amd.runtime import MODELS
+    d = MODELS["qwen3-8b"]
+
+    def pred(ranges):
+        sh = bench.head_shards(d, ranges, 16, 2048)
+        base, head_us = bench.stage_base_us(d, ranges, 16, 2048)
+        per_row = head_us / d.vocab
+        t = [b + (bench.HEAD_SHARD_FIXED_US + per_row * k if k else 0) for b, (_, k) in zip(base, sh)]
+        nb = [bench.range_bytes(d, x, 16, 2048, False) + k * d.hidden * 2 for x, (_, k) in zip(ranges, sh)]
+        return min(nb) / max(t)
+    for n in (2, 4, 8):
+        r = bench.sub_split(d, n, True, vhead=True)
+        _cover(r, d.layers, d.intermediate)
+        if n == 8:
+            assert pred(r) >= pred(ranges_from_sizes([4.5] * 8)) * 1.005
