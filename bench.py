@@ -1043,13 +1043,14 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args.model, B, ctx, args.seed, args.cpu_layers)
             out["cpu_baseline_config1"] = cpu_config1(args.seed)
     if world > 1 and not args.no_sublayer_split and args.split == "even" and not args.spans:
-        # beside config 3's even split, same run: equal half-layer stages with the vocab-parallel head
-        # (where the layer count does not divide: the stage projection's best 8-stage split) and
-        # north_star's sub-layer split with the whole head on the last stage
+        # beside config 3's even split, same run: the sub-layer split chosen for the vocab-parallel
+        # head (the projection's best-balanced split at 2, 4 and 8 stages) and north_star's
+        # sub-layer split with the whole head on the last stage
         alts = []
-        if vhead and (2 * d.layers) % world == 0 and (2 * d.layers // world) % 2:
-            alts.append(("halves_vocab_head", P.ranges_from_sizes([d.layers / world] * world), True,
-                         "equal half-layer stages, greedy head vocab-parallel (shards calibrated per rank)"))
+        if vhead:
+            alts.append(("sublayer_vocab_head", sub_split(d, world, True, vhead=True), True,
+                         "sub-layer cuts chosen for the vocab-parallel head (gateup_split(vhead=...)), "
+                         "shards calibrated per rank"))
         alts.append(("sublayer_split", sub_split(d, world, True), False,
                      "pipeline.sublayer_split's stages (measured cost table), the whole lm_head on the last stage"))
         for key, alt, vh, note in alts:
@@ -1069,7 +1070,7 @@ def main():
                     "note": note + "; `value` above is BASELINE config 3's even split"}
     if rank == 0:
         # the driver keeps the tail of stdout: the compact results go last
-        for k in ("stage_projection_summary", "projected_scaling", "sublayer_split", "halves_vocab_head",
+        for k in ("stage_projection_summary", "projected_scaling", "sublayer_split", "sublayer_vocab_head",
                   "prefill_config5", "prefill_config5_b4"):
             if k in out:
                 v = out.pop(k)

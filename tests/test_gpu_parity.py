@@ -447,6 +447,10 @@ def _ranges(sizes):
     from inferd_amd.pipeline import measured_split, ranges_from_sizes
     if sizes in ("gateup8", "sublayer8"):   # bench.py --split gateup / sublayer (bench.sub_split)
         return measured_split(36, 8, 12288, o_cuts=sizes == "sublayer8")
+    if sizes == "vsub8":     # bench.py's sublayer_vocab_head line: sub-layer cuts for the vocab-parallel head
+        import bench
+        from inferd_amd.runtime import MODELS
+        return bench.sub_split(MODELS["qwen3-8b"], 8, True, vhead=True)
     return ranges_from_sizes(sizes)
 
 
@@ -890,15 +894,18 @@ def _single_small_worker(port, out_dir, profile, steps):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("profile", ["peaked_deep", "random"])
-def test_q8b_pipeline_vocab_parallel_head(tmp_path, profile, q8b_oracle_greedy):
+@pytest.mark.parametrize("profile,sizes", [("peaked_deep", "even8"), ("random", "even8"), ("peaked_deep", "vsub8")])
+def test_q8b_pipeline_vocab_parallel_head(tmp_path, profile, sizes, q8b_oracle_greedy):
     """BASELINE config 3's 8-stage even split with the greedy head vocab-parallel (round 6: the
     1.24 GB lm_head sharded over the stages by bench.head_shards, the normed rows and running
     (max, first index) keys handed round the ring, n_mb = 2S + 1 = 17 microbatches): 8 ranks sharing
     this box's GPU over gloo, real HIP spans.  Every microbatch holds the same prompts, so every id
     fed to stage 0 must equal (a) a single 36-layer HIP span's free-running greedy ids (whole head)
-    and, on the "peaked_deep" profile, (b) the 36-layer CPU oracle's (q8b_oracle_greedy)."""
-    sizes = [5, 5, 5, 5, 4, 4, 4, 4]
+    and, on the "peaked_deep" profile, (b) the 36-layer CPU oracle's (q8b_oracle_greedy).  "vsub8":
+    bench.py's sublayer_vocab_head split instead (gate/up, q/k/v|attention and attention|o cuts with
+    the vocab-parallel head: the sub-layer records and the head records on the same ring)."""
+    tag = sizes
+    sizes = [5, 5, 5, 5, 4, 4, 4, 4] if sizes == "even8" else sizes
     world, steps = 8, 6
     n_mb = 2 * world + 1
     port = _free_port()
@@ -914,10 +921,10 @@ def test_q8b_pipeline_vocab_parallel_head(tmp_path, profile, q8b_oracle_greedy):
         ref_ids = q8b_oracle_greedy[0]
         for k, m, t in pipe["rec"]:
             assert t.tolist() == ref_ids[k].tolist(), (k, m)
-    print(f"vocab-parallel head, even8, {profile}: {steps} steps x {n_mb} microbatches x {B8X} ids identical to "
-          f"one span{' and the oracle' if profile == 'peaked_deep' else ''}; shards {pipe['shards']}; "
-          f"host {pipe['tick']}")
-    record(f"q8b_pipeline_vocab_head_even8_{profile}", shards=pipe["shards"], microbatches=n_mb, batch=B8X,
+    print(f"vocab-parallel head, {tag} {[r.label() for r in _ranges(sizes)]}, {profile}: {steps} steps x {n_mb} "
+          f"microbatches x {B8X} ids identical to one span{' and the oracle' if profile == 'peaked_deep' else ''}; "
+          f"shards {pipe['shards']}; host {pipe['tick']}")
+    record(f"q8b_pipeline_vocab_head_{tag}_{profile}", shards=pipe["shards"], microbatches=n_mb, batch=B8X,
            decode_steps=steps, identical=True, tick=pipe["tick"])
 
 

@@ -267,7 +267,7 @@ def test_pipeline_microbatch_counts(world, n_mb):
 
 
 @pytest.mark.parametrize("world,sizes,extra", [(2, None, 1), (3, None, 1), (3, None, 0), (3, "o", 2),
-                                               (4, None, 1)])
+                                               (4, None, 1), (3, "gateup", 1), (3, "q_o", 1)])
 def test_pipeline_vocab_parallel_head(world, sizes, extra):
     """The greedy head vocab-parallel over the stages (HEAD_SHARDS: uneven, and stages owning no
     rows), the normed rows and running keys handed round the ring: the ids are the single span's
