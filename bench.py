@@ -461,7 +461,7 @@ def ring_tick_us(c, h, vhead: bool, n_mb: int, x: float) -> float:
     return max(P, (sum(L) + h[-1] + S * x) / (n_mb - S), (sum(L) - L[0] + S * x) / S)
 
 
-def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: int = 3, reps: int = 20,
+def stage_projection(d, splits: dict, B: int, ctx: int, dev, seed: int, warmup: int = 10, reps: int = 60,
                      slack: int = 1) -> dict:
     """Every stage of every split measured alone on this GPU with its real role (stage_ms:
     embedding on stage 0, final norm + lm_head + argmax on the last, or -- a split whose value is
