@@ -42,15 +42,25 @@ def main():
                 continue
             for i, (r, st) in enumerate(zip(rs, v["stages"])):
                 content = P.predicted_stage_us(r, cal, False, False) - cal["stage"]
-                rows.append((content, i == 0, i == len(rs) - 1, st["ms"] * 1e3, f"{os.path.basename(fn)}:{name}:{r.label()}"))
+                last = i == len(rs) - 1
+                if "head_rows" in st:
+                    # vocab-parallel head (bench.stage_projection's vhead splits): the stage's layers
+                    # are its time less its shard's (head_ms); the last one ends with the final norm
+                    ms = (st["ms"] - st.get("head_ms", 0.0)) * 1e3
+                    rows.append((content, i == 0, False, last, ms, f"{os.path.basename(fn)}:{name}:{r.label()}"))
+                else:
+                    rows.append((content, i == 0, last, False, st["ms"] * 1e3,
+                                 f"{os.path.basename(fn)}:{name}:{r.label()}"))
     C = np.array([r[0] for r in rows])
     F = np.array([r[1] for r in rows])
     L = np.array([r[2] for r in rows])
-    M = np.array([r[3] for r in rows])
+    N = np.array([r[3] for r in rows])
+    M = np.array([r[4] for r in rows])
+    norm_us = 5.5     # bench.FINAL_NORM_US: the final norm a vocab-head last stage runs
 
     def model(p):
         a, b, g, fs = p
-        return np.where(F, fs, 1.0) * (a * C + b + L * g * cal["head"] + F * cal["embed"])
+        return np.where(F, fs, 1.0) * (a * C + b + L * g * cal["head"] + F * cal["embed"] + N * norm_us)
     res = least_squares(lambda p: (model(p) - M) / M, [1.0, cal["stage"], 1.0, 1.0])
     a, b, g, fs = (float(x) for x in res.x)
     fit = {"content_scale": round(a, 5), "stage": round(b, 3), "head_scale": round(g, 5), "first_scale": round(fs, 5),
@@ -61,7 +71,7 @@ def main():
         json.dump(raw, f, indent=1)
     print(json.dumps(fit))
     for r, e in sorted(zip(rows, res.fun), key=lambda t: -abs(t[1]))[:12]:
-        print(f"{e:+.4f} {r[4]}")
+        print(f"{e:+.4f} {r[5]}")
 
 
 if __name__ == "__main__":
