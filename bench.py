@@ -372,7 +372,7 @@ def stage_ms(d, r, first: bool, last: bool, B: int, ctx: int, dev, g, seed: int,
         reqs = [(sid, ctx) for sid in sess[c:c + chunk]]
         if first:
             ids = torch.randint(0, d.vocab, (len(reqs) * ctx,), generator=g, dtype=torch.int32)
-            span.forward(reqs, ids=ids, want_hidden=False, want_next_ids=last and not vh)
+            span.forward(reqs, ids=ids, want_hidden=r.last_o or r.last_q, want_next_ids=last and not vh)
         else:     # (a record x | attention output at an attention|o boundary)
             n_in = buffer_elems(d, len(reqs) * ctx, 0, r.first_o, False, r.first_q)
             x = (torch.randn(n_in, generator=g) * 0.5).to(torch.bfloat16)
