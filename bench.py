@@ -599,41 +599,6 @@ def sub_split(d, n: int, o_cuts: bool, vhead: bool = False):
 CONFIG4_SPLITS = {3: [5, 27, 4], 4: [6, 12, 12, 6], 8: [2, 3, 5, 6, 6, 6, 5, 3]}
 
 
-def vhead_best_split(d, n: int, B: int, ctx: int, spread: int = 2):
-    """Half-layer stage sizes for the vocab-parallel head chosen on the cost model: every way to
-    give the n stages 2L/n +- `spread` half-layer units (summing to the model's 2L) is priced with
-    stage_base_us, the head shards water-filled on top (head_shards), and the sizes whose lowest
-    stage has the largest share of 8 TB/s at the resulting tick win.  Stages of slow bytes (the
-    embedding stage, attention-heavy ones) take fewer layer units and more lm_head rows, which
-    stream faster than a layer's mix of kernels.  Returns (ranges, predicted lowest fraction)."""
-    import itertools
-    from inferd_amd.pipeline import ranges_from_sizes
-    total, mean = 2 * d.layers, 2 * d.layers / n
-    lo, hi = max(1, int(mean) - spread), int(mean + 0.999) + spread
-    base_cache = {}
-    best = (None, -1.0)
-    per_row = None
-    for sz in itertools.product(range(lo, hi + 1), repeat=n - 1):
-        last = total - sum(sz)
-        if not lo <= last <= hi:
-            continue
-        sizes = [h / 2 for h in sz + (last,)]
-        ranges = ranges_from_sizes(sizes)
-        key = tuple(sizes)
-        base, head_us = stage_base_us(d, ranges, B, ctx)
-        if per_row is None:
-            per_row = head_us / d.vocab
-        shards = head_shards(d, ranges, B, ctx)
-        t = [b + (HEAD_SHARD_FIXED_US + per_row * r if r else 0.0) for b, (_, r) in zip(base, shards)]
-        tick = max(t)
-        nb = [range_bytes(d, r, B, ctx, False) + rows * d.hidden * 2 for r, (_, rows) in zip(ranges, shards)]
-        frac = min(nb) / (tick * 1e-6) / 1e9 / HBM_PEAK_GBS
-        base_cache[key] = frac
-        if frac > best[1]:
-            best = (ranges, frac)
-    return best
-
-
 def projection_splits(d, B: int, ctx: int, sizes=(2, 4, 8)) -> dict:
     """The splits stage_projection measures: BASELINE config 3's even splits, the layer-granular
     byte-balanced split, the half-layer and sub-layer time-balanced splits at each stage count,
