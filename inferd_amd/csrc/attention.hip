@@ -230,6 +230,43 @@ __device__ __forceinline__ void decode_kv_write(const DecodeFuse& f, u16* __rest
 // (the ATTN_PROBE timing builds -- no q prologue / K fragments as the P*V operand -- live in
 // the round-2 tree, git 6a90f3d, with tools/archive/attn_lab_r03.hip)
 
+// Lab builds only (tools/build_probes.sh attention.hip name=-DATTN_DEC_STAMPS): per-workgroup
+// s_memrealtime stamps (100 MHz) of the decode body's phases into a buffer of its own
+// (inferd_lab_dec_stamps), read by tools/attn_decode_stamps.py.  Slots per workgroup:
+// 0 entry, 1 q ready (wave 0), 2..9 each wave's stream end, 10 after the LDS merge barrier,
+// 11 partials published (before the ticket), 12 after the ticket barrier, 13 exit, 14 flags,
+// 15 the q image landed in LDS (wave 0).
+#ifdef ATTN_DEC_STAMPS
+#define DEC_SLOTS 16
+// __constant__: the pointer comes in by a scalar load, so a stamp adds no vmcnt wait (a vector
+// load of it made every stamp behind the ring prologue drain the ring)
+__constant__ unsigned long long* g_dec_stamps;
+__device__ __forceinline__ unsigned long long* dec_slot(int slot) {
+  const unsigned wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  return g_dec_stamps + (size_t)wg * DEC_SLOTS + slot;
+}
+#define DSTAMP(slot)                                                                              \
+  do {                                                                                            \
+    if (threadIdx.x == 0 && g_dec_stamps) *dec_slot(slot) = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+#define DSTAMP_WAVE(slot)                                                                         \
+  do {                                                                                            \
+    if ((threadIdx.x & 63) == 0 && g_dec_stamps)                                                  \
+      *dec_slot((slot) + (threadIdx.x >> 6)) = __builtin_amdgcn_s_memrealtime();                  \
+  } while (0)
+#define DFLAGS(v)                                                 \
+  do {                                                            \
+    if (threadIdx.x == 0 && g_dec_stamps) *dec_slot(14) = (v);    \
+  } while (0)
+extern "C" int inferd_lab_dec_stamps(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dec_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : 2;
+}
+#else
+#define DSTAMP(slot)
+#define DSTAMP_WAVE(slot)
+#define DFLAGS(v)
+#endif
+
 template <int NW, bool FUSED>
 __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16* __restrict__ kv, const AttnBatch& b,
                                                  int H, int KV, int nc_req, float scale_log2, int n_chunks_max,
@@ -239,6 +276,7 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
   __shared__ float sm_m[NW][16], sm_l[NW][16];
   __shared__ float sm_o[NW][16][HEAD_DIM + 4];
   __shared__ int sm_last;
+  DSTAMP(0);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n_rep = H / KV;
   const int ctx = b.ctx_lens[bseq];
@@ -333,6 +371,7 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
 #pragma unroll
       for (int i = 0; i < QS_MAXC; ++i)
         if ((lane + 64 * i) * 16 < fz.qs_bytes) *(u16x8*)(qs + (lane + 64 * i) * 16) = qsr[i];
+      DSTAMP(15);
       // this wave's own LDS slot: its stores are read back by its own lanes only
       const int d0 = 8 * (lane >> 4);
       float x[4][8];
@@ -391,6 +430,7 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
   // the writer's token K/V when none of its first two items holds the token: its stores land
   // before the ring refills with the token's half page (item(): vm_wait before that issue)
   if (writer && !tok_early) decode_kv_write(fz, kv, b, bseq, tok, g, H, KV, lane);
+  DSTAMP(1);
   float m_i = -INFINITY, l_i = 0.f;
   f32x4 o[8];
 #pragma unroll
@@ -483,6 +523,7 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
       item(S0{}, N{});
     }
   }
+  DSTAMP_WAVE(2);
   // merge the NW waves through LDS
   l_i = sum_q4(l_i);
   if (lane < 16) {
@@ -494,6 +535,7 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
 #pragma unroll
     for (int r = 0; r < 4; ++r) sm_o[wave][hn][db * 16 + 4 * (lane >> 4) + r] = o[db][r];
   __syncthreads();
+  DSTAMP(10);
   u16* op = out + (int64_t)tok * H * HEAD_DIM + (int64_t)g * n_rep * HEAD_DIM;
   const int stride = n_rep * PART_STRIDE;
   float* base = part + ((int64_t)bseq * KV + g) * n_chunks_max * stride;
@@ -522,9 +564,14 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
       }
     }
   }
-  if (nc == 1) return;
+  if (nc == 1) {
+    DSTAMP(13);
+    DFLAGS(1ull | ((unsigned long long)nc << 8) | ((unsigned long long)chunk << 16));
+    return;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  DSTAMP(11);
   if (threadIdx.x == 0) {
     const unsigned prev =
         __hip_atomic_fetch_add(&counters[bseq * KV + g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -532,7 +579,12 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
     if (sm_last) __hip_atomic_store(&counters[bseq * KV + g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (!sm_last) return;
+  DSTAMP(12);
+  DFLAGS((unsigned long long)sm_last | ((unsigned long long)nc << 8) | ((unsigned long long)chunk << 16));
+  if (!sm_last) {
+    DSTAMP(13);
+    return;
+  }
   // Last arriver: every partial was stored write-through (sc1) and drained before its
   // workgroup's ticket add, and every load of one here is an sc1 load, so no acquire fence
   // is needed (MI355X_MICROARCH.md, visibility "Valid forms", row 1: one workgroup per CU,
@@ -579,6 +631,11 @@ __device__ __forceinline__ void attn_decode_body(const u16* __restrict__ q, u16*
     if (fz.pack_ld) out[packed_index(tok, (g * n_rep + n) * HEAD_DIM + d, fz.pack_ld)] = ov;
     else op[n * HEAD_DIM + d] = ov;
   }
+#ifdef ATTN_DEC_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#endif
+  DSTAMP(13);
 }
 
 template <int NW, bool FUSED>
