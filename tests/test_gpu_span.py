@@ -8,6 +8,9 @@ them in fp32).  Greedy tokens are checked on the "peaked" synthetic profile (lar
 margins, oracle/weightgen.py) on EVERY step, and every step's reference margin must exceed
 twice the measured logit error, so agreement is never luck and never skipped.
 """
+import os
+import subprocess
+
 import pytest
 import torch
 
@@ -791,3 +794,36 @@ def test_record_boundaries_refuse_multi_call_forwards():
         so.forward([("b", 10)], x=x[:10], want_hidden=False)
     out = so.forward([("c", 10)], x=x[:10])
     assert out["record"].numel() == 10 * d.hidden + 10 * d.heads * d.head_dim
+
+
+def test_c_host_span_greedy():
+    """The drop-in boundary without Python: tests/c_abi/span_host.c (plain C over
+    include/inferd_span.h and HIP's C API; no Python or torch in its process, built by
+    __graft_entry__.build()) prefills B sessions in one call through the native page table and
+    decodes greedily, one forward call per step for all B.  Every id equals the torch extension's
+    run of the same span (SpanRuntime: same seed, prompts and batching; the kernels are
+    deterministic), on the tiny model and on Qwen3-0.6B (config 2's model)."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "c_abi", "span_host")
+    assert os.path.exists(exe), "tests/c_abi/span_host is not built (__graft_entry__.build())"
+    for model, B, T, steps in (("tiny", 3, 21, 6), ("qwen3-0.6b", 2, 70, 5)):
+        r = subprocess.run([exe, model, str(SEED), str(B), str(T), str(steps)], capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.returncode, r.stdout, r.stderr)
+        c_ids = [[int(v) for v in line.split(":")[1].split()] for line in r.stdout.splitlines()
+                 if line.startswith("ids ")]
+        d = MODELS[model]
+        s = SpanRuntime(d, 0, d.layers, has_embed=True, has_lm_head=True, device=DEV, max_positions=8192,
+                        kv_pages=B * ((T + steps + 63) // 64) + 8, max_tokens=B * T, max_seqs=B)
+        s.init_synthetic(SEED)
+        prompt = torch.tensor([(7919 * t + 104729 * b + 17) % d.vocab for b in range(B) for t in range(T)])
+        out = s.forward([(f"c{b}", T) for b in range(B)], ids=prompt, want_next_ids=True, want_hidden=False)
+        ids = [out["next_ids"].cpu().tolist()]
+        for _ in range(steps):
+            out = s.forward([(f"c{b}", 1) for b in range(B)], ids=torch.tensor(ids[-1]), want_next_ids=True,
+                            want_hidden=False)
+            ids.append(out["next_ids"].cpu().tolist())
+        torch_ids = [[ids[k][b] for k in range(steps + 1)] for b in range(B)]
+        print(f"{model}: C host {c_ids}, torch {torch_ids}")
+        assert c_ids == torch_ids, model
+        s.release_all()

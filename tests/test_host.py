@@ -457,3 +457,26 @@ def test_c_host_kv_table(tmp_path):
                     f"-Wl,-rpath,{lib_dir}", "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "C HOST OK" in r.stdout, r.stdout + r.stderr
+
+
+def test_c_host_span_builds(tmp_path):
+    """The plain-C GPU host of the span engine (tests/c_abi/span_host.c; run against the GPU by
+    tests/test_gpu_span.py::test_c_host_span_greedy) compiles warning-free against
+    include/inferd_span.h and HIP's C API with gcc, links libinferd_span.so, and refuses a bad
+    command line before touching a device."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib_dir = os.path.join(root, "inferd_amd")
+    if not os.path.exists(os.path.join(lib_dir, "libinferd_span.so")):
+        pytest.skip("libinferd_span.so not built")
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None or not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
+        pytest.skip("no C compiler / HIP headers")
+    exe = str(tmp_path / "span_host")
+    subprocess.run([cc, "-std=c11", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(root, "include"),
+                    "-I", "/opt/rocm/include", os.path.join(root, "tests", "c_abi", "span_host.c"), "-L", lib_dir,
+                    "-linferd_span", "-L", "/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{lib_dir}",
+                    "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "usage" in r.stderr, r.stdout + r.stderr
