@@ -222,19 +222,19 @@ def test_rope_table_matches_hf(lib):
     assert ulp_s.max() <= 1 and (ulp_s > 0).float().mean() < 1e-3
 
 
-def _attn_case(lib, H, KV, q_lens, past_lens, seed=0):
+def _attn_case(lib, H, KV, q_lens, past_lens, seed=0, n_pages=256):
     """Random bf16 q/K/V; K/V written into shuffled pages; compare with fp32 SDPA."""
     from inferd_amd.runtime import KvTable, SeqView
     from kv_layout import K_IDX, V_IDX, block, pool_elems
     torch.manual_seed(seed)
     L = lib.load()
-    table = KvTable(256)
+    table = KvTable(n_pages)
     # scatter the free list: one-page sequences released in a random order
-    for i in range(256):
+    for i in range(n_pages):
         table.reserve(10_000 + i, 1)
-    for i in np.random.default_rng(seed).permutation(256):
+    for i in np.random.default_rng(seed).permutation(n_pages):
         table.release(10_000 + int(i))
-    kv = torch.zeros(pool_elems(256, KV), dtype=torch.bfloat16)
+    kv = torch.zeros(pool_elems(n_pages, KV), dtype=torch.bfloat16)
     seqs, Ks, Vs, Qs = [], [], [], []
     for j, (T, P) in enumerate(zip(q_lens, past_lens)):
         st = SeqView(table, j)
@@ -306,6 +306,18 @@ def test_attention_decode_many_chunks(lib, q_lens, past):
     one sequence at 6000 tokens, 16 for two -- the last-arriving chunk merges them 8 at a time
     (attention.hip), so these exercise several merge blocks and a partial last block."""
     err, ref = _attn_case(lib, 32, 8, q_lens, past, seed=7)
+    _attn_check(err, ref, f"decode_chunks_{'_'.join(map(str, past))}")
+
+
+@pytest.mark.parametrize("q_lens,past", [([1], [20000]), ([1, 1, 1], [20000, 9000, 100])],
+                         ids=["b1_ctx20001", "b3_ctx20001_9001_101"])
+def test_attention_decode_max_chunks(lib, q_lens, past):
+    """Long contexts reach the decode launcher's other shape and its chunk cap (attention.hip
+    decode_shape): from 96 pages per sequence on, 4-wave workgroups; one sequence at 20001 cached
+    tokens splits into MAX_DECODE_CHUNKS = 64 chunks (the last arriver merges all 64 partials, 8
+    blocks of 8), three sequences into 21 each (blocks of 8, 8, 5; the 101-token sequence has only
+    2 pages, so 2 of them); against fp32 SDPA with the same bounds."""
+    err, ref = _attn_case(lib, 32, 8, q_lens, past, seed=11, n_pages=480)
     _attn_check(err, ref, f"decode_chunks_{'_'.join(map(str, past))}")
 
 
