@@ -557,6 +557,33 @@ def test_decode_fused_rope_vs_oracle():
         assert e < TOL_REL
 
 
+def test_decode_fused_long_context_vs_oracle():
+    """The fused decode attention's long-context shape: from 96 cached pages per sequence the
+    launcher takes 4-wave workgroups with more chunks (attention.hip decode_shape; here 24 per
+    sequence and kv head), a path the 8B-dims test above does not reach.  Tiny-model span (n_rep 2,
+    the q-staging prologue), two sequences whose new tokens land at a page start (6144) and
+    mid-page (6200), 3 decode steps, every step's hidden states against the oracle's cached
+    forward."""
+    from inferd_amd.runtime import MODELS, SpanRuntime
+    d = MODELS["tiny"]
+    lens = [6144, 6200]
+    s = SpanRuntime(d, 0, d.layers, has_embed=True, has_lm_head=False, device=DEV, max_positions=8192,
+                    kv_pages=2 * 100 + 8, max_tokens=sum(lens), max_seqs=2)
+    s.init_synthetic(SEED)
+    oracle = R.RefSpan(R.CONFIGS["tiny"], SEED, 0, d.layers - 1, True, False, torch.bfloat16, "sdpa")
+    prompts = [torch.randint(0, d.vocab, (n,), generator=torch.Generator().manual_seed(n)) for n in lens]
+    s.forward([(f"s{i}", n) for i, n in enumerate(lens)], ids=torch.cat(prompts), want_hidden=False)
+    for i, p in enumerate(prompts):
+        oracle.forward_cached(f"s{i}", p[None])
+    for step in range(3):
+        ids = torch.tensor([(11 * step + 5 * i) % d.vocab for i in range(len(lens))])
+        h = s.forward([(f"s{i}", 1) for i in range(len(lens))], ids=ids, want_hidden=True)["hidden"].cpu()
+        ref = torch.cat([oracle.forward_cached(f"s{i}", ids[i].reshape(1, 1))[0] for i in range(len(lens))])
+        e = rel_err(h, ref)
+        print(f"fused long-context decode step {step}: rel err {e:.2e}")
+        assert e < TOL_REL
+
+
 @pytest.mark.parametrize("B", [4, 16, 40, 64])
 def test_decode_packed_act_bit_exact(B):
     """The decode path's fragment-packed activations (residual stream, SwiGLU output, attention
