@@ -211,6 +211,10 @@ def _make_stage(span, first, last):
 
 
 def _model_key(model_name: str) -> str:
+    """runtime.MODELS key of a model name for synthetic stages (no checkpoint): the Qwen3 size in
+    the name, else qwen3-0.6b -- the reference's default config names Qwen/Qwen2-0.5B
+    (petals/inferd.yaml:1); the engine runs the Qwen3 layer of the same scale.  Checkpoints carry
+    their own geometry (split_model.checkpoint_dims), which refuses non-Qwen3 architectures."""
     n = model_name.lower()
     for k in ("32b", "8b", "0.6b"):
         if k in n:

@@ -15,7 +15,9 @@ entries (split_model.py:91-102) does not carry over.
 
 Weight sources: a HF-format safetensors checkpoint directory (keys `model.layers.{i}.*`,
 `model.embed_tokens.weight`, `model.norm.weight`, `lm_head.weight`, tied embeddings
-allowed) or the counter-based synthetic generator (`--synthetic-seed`).
+allowed; the model geometry from its config.json, so any Qwen3 size loads; other
+architectures -- the reference's default Qwen2-0.5B among them -- are refused with the reason)
+or the counter-based synthetic generator (`--synthetic-seed`).
 """
 from __future__ import annotations
 
@@ -55,8 +57,44 @@ def write_stage_file(path: str, dims: ModelDims, start: int, end: int, first: bo
     save_file(tensors, path, metadata=meta)
 
 
+def checkpoint_dims(ckpt_dir: str, name: str | None = None) -> ModelDims | None:
+    """The model geometry of a HF checkpoint directory from its config.json (None without one),
+    so any Qwen3 size loads (4B, 14B, ... -- not only the sizes in runtime.MODELS).  Anything
+    but a Qwen3 decoder is refused here with the reason, instead of failing later on a missing
+    key or a shape: the reference's petals config names Qwen/Qwen2-0.5B (petals/inferd.yaml:1,
+    loaded by split_model.py:81 as Qwen2ForCausalLM), whose layers carry q/k/v biases, no
+    QK-norm and 64-dim heads; this engine implements the Qwen3 layer (qwen3_server_module.py,
+    BASELINE north_star).  Rotary scaling other than the default is refused too (the rope
+    tables are the HF default formula, client.py:56-71)."""
+    p = os.path.join(ckpt_dir, "config.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        c = json.load(f)
+    mt = c.get("model_type", "")
+    if mt != "qwen3":
+        raise ValueError(f"{ckpt_dir}: model_type {mt!r} -- this engine runs Qwen3 decoder layers (QK-norm, "
+                         "no q/k/v bias, 128-dim heads); a Qwen2 checkpoint (the reference's default "
+                         "Qwen/Qwen2-0.5B) has biases, no QK-norm and 64-dim heads")
+    hd = c.get("head_dim") or c["hidden_size"] // c["num_attention_heads"]
+    if hd != 128:
+        raise ValueError(f"{ckpt_dir}: head_dim {hd}; the engine's attention kernels take 128")
+    if c.get("attention_bias"):
+        raise ValueError(f"{ckpt_dir}: attention_bias is set; the engine's projections have no bias")
+    if c.get("rope_scaling"):
+        raise ValueError(f"{ckpt_dir}: rope_scaling {c['rope_scaling']!r}; the engine's rope tables are the "
+                         "default (unscaled) formula")
+    return ModelDims(name=name or os.path.basename(os.path.normpath(ckpt_dir)), hidden=c["hidden_size"],
+                     intermediate=c["intermediate_size"], heads=c["num_attention_heads"],
+                     kv_heads=c["num_key_value_heads"], layers=c["num_hidden_layers"], vocab=c["vocab_size"],
+                     head_dim=hd, eps=float(c.get("rms_norm_eps", 1e-6)),
+                     rope_theta=float(c.get("rope_theta", 1_000_000.0)),
+                     max_positions=int(c.get("max_position_embeddings", 40960)))
+
+
 def hf_checkpoint_source(ckpt_dir: str):
-    """Lazy accessors over a HF safetensors checkpoint (sharded or single file)."""
+    """Lazy accessors over a HF safetensors checkpoint (sharded or single file).  Refuses biased
+    projections (Qwen2-style layers) up front (checkpoint_dims)."""
     from safetensors import safe_open
     files = [os.path.join(ckpt_dir, f) for f in sorted(os.listdir(ckpt_dir)) if f.endswith(".safetensors")]
     where = {}
@@ -64,6 +102,10 @@ def hf_checkpoint_source(ckpt_dir: str):
         with safe_open(fn, framework="pt", device="cpu") as f:
             for k in f.keys():
                 where[k] = fn
+    biased = sorted(k for k in where if k.endswith("_proj.bias"))
+    if biased:
+        raise ValueError(f"{ckpt_dir}: biased projections ({biased[0]}, ...) -- Qwen2-style layers, not a Qwen3 "
+                         "checkpoint (checkpoint_dims)")
 
     def get(key):
         with safe_open(where[key], framework="pt", device="cpu") as f:
@@ -106,6 +148,8 @@ def main():
     from .partitioned_models import _model_key
     dims = MODELS[a.model or _model_key(cfg["model_name"])]
     if a.checkpoint:
+        if not a.model:      # the checkpoint's own geometry (config.json) when it has one
+            dims = checkpoint_dims(a.checkpoint, name=cfg["model_name"]) or dims
         gl, gg = hf_checkpoint_source(a.checkpoint)
     elif a.synthetic_seed is not None:
         gl, gg = synthetic_source(dims, a.synthetic_seed)

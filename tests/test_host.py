@@ -480,3 +480,44 @@ def test_c_host_span_builds(tmp_path):
                     "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "usage" in r.stderr, r.stdout + r.stderr
+
+
+def test_split_model_checkpoint_config_dims_and_refusals(tmp_path):
+    """A HF checkpoint's config.json gives the stage files their geometry (any Qwen3 size, not only
+    runtime.MODELS's), and checkpoints the engine cannot run are refused with the reason: a Qwen2
+    config (the reference's default Qwen/Qwen2-0.5B), 64-dim heads, rope scaling, biased
+    projections."""
+    import json
+    from dataclasses import asdict
+    from safetensors import safe_open
+    from safetensors.torch import save_file
+    from hf_fixtures import write_hf_checkpoint
+    from inferd_amd.runtime import MODELS
+    from inferd_amd.split_model import checkpoint_dims, hf_checkpoint_source, split
+    from oracle import qwen3_ref as R
+    d = R.CONFIGS["tiny"]
+    ck = write_hf_checkpoint(str(tmp_path / "hf"), d, 7)
+    assert checkpoint_dims(ck) is None          # no config.json: the caller's dims
+    conf = {"model_type": "qwen3", "hidden_size": d.hidden, "intermediate_size": d.intermediate,
+            "num_attention_heads": d.heads, "num_key_value_heads": d.kv_heads, "num_hidden_layers": d.layers,
+            "vocab_size": d.vocab, "head_dim": 128, "rms_norm_eps": 1e-6, "rope_theta": 1000000.0,
+            "max_position_embeddings": 40960, "attention_bias": False, "rope_scaling": None}
+    with open(tmp_path / "hf" / "config.json", "w") as f:
+        json.dump(conf, f)
+    dims = checkpoint_dims(ck, name="tiny")
+    assert asdict(dims) == asdict(MODELS["tiny"])
+    cfg = {"model_name": "tiny", "parts_dir": str(tmp_path / "out"), "stages_count": 1,
+           "stages": [{"name": "n0", "stage": 0, "start_layer": 0, "end_layer": d.layers - 1}]}
+    (path,) = split(cfg, dims, *hf_checkpoint_source(ck))
+    with safe_open(path, framework="pt") as f:
+        assert json.loads(f.metadata()["dims"]) == asdict(dims)
+    for bad, why in (({"model_type": "qwen2", "head_dim": 64}, "qwen2"), ({"head_dim": 64}, "head_dim"),
+                     ({"rope_scaling": {"type": "yarn", "factor": 4.0}}, "rope_scaling"),
+                     ({"attention_bias": True}, "attention_bias")):
+        with open(tmp_path / "hf" / "config.json", "w") as f:
+            json.dump({**conf, **bad}, f)
+        with pytest.raises(ValueError, match=why):
+            checkpoint_dims(ck)
+    save_file({"model.layers.0.self_attn.q_proj.bias": torch.zeros(4)}, str(tmp_path / "hf" / "bias.safetensors"))
+    with pytest.raises(ValueError, match="biased"):
+        hf_checkpoint_source(ck)
