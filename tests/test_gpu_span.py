@@ -854,3 +854,37 @@ def test_c_host_span_greedy():
         print(f"{model}: C host {c_ids}, torch {torch_ids}")
         assert c_ids == torch_ids, model
         s.release_all()
+
+
+@pytest.mark.parametrize("name,hidden,inter,heads,kv", [("qwen3-1.7b", 2048, 6144, 16, 8),
+                                                       ("qwen3-4b", 2560, 9728, 32, 8),
+                                                       ("qwen3-14b", 5120, 17408, 40, 8)])
+def test_other_qwen3_sizes_layer_vs_oracle(name, hidden, inter, heads, kv):
+    """Qwen3 sizes the bench does not run, which split_model.checkpoint_dims now loads from a
+    checkpoint's config.json (public Qwen3 configs): one layer of each, a ragged 600 + 77-token
+    prefill (the persistent prefill GEMMs on partial tiles) then 3 cached decode steps (the decode
+    GEMVs at these K / N; at 14B, 5 query heads per kv head: the fused decode attention without
+    the q-staging prologue), every output against the oracle at the span tolerance."""
+    from inferd_amd.runtime import ModelDims, SpanRuntime
+    d = ModelDims(name, hidden, inter, heads, kv, 1, 151936)
+    od = R.Qwen3Dims(name, hidden, inter, heads, kv, 1, 151936)
+    s = SpanRuntime(d, 0, 1, has_embed=False, has_lm_head=False, device=DEV, max_positions=1024, kv_pages=24,
+                    max_tokens=700, max_seqs=2)
+    s.init_synthetic(SEED)
+    oracle = R.RefSpan(od, SEED, 0, 0, False, False, torch.bfloat16, "sdpa")
+    g = torch.Generator().manual_seed(3)
+    lens = [600, 77]
+    xs = [(torch.randn(n, hidden, generator=g) * 0.5).to(torch.bfloat16) for n in lens]
+    h = s.forward([(f"s{i}", n) for i, n in enumerate(lens)], x=torch.cat(xs))["hidden"].cpu()
+    ref = torch.cat([oracle.forward_cached(f"s{i}", x[None])[0] for i, x in enumerate(xs)])
+    e = rel_err(h, ref)
+    print(f"{name} prefill: rel err {e:.2e}")
+    assert e < TOL_REL
+    for step in range(3):
+        xd = [(torch.randn(1, hidden, generator=g) * 0.5).to(torch.bfloat16) for _ in lens]
+        h = s.forward([(f"s{i}", 1) for i in range(len(lens))], x=torch.cat(xd))["hidden"].cpu()
+        ref = torch.cat([oracle.forward_cached(f"s{i}", x[None])[0] for i, x in enumerate(xd)])
+        e = rel_err(h, ref)
+        print(f"{name} decode step {step}: rel err {e:.2e}")
+        assert e < TOL_REL
+    s.release_all()
